@@ -1,0 +1,114 @@
+"""``create_image`` -- drop-in for the reference's map renderer, running on MI355X.
+
+Reference: /root/reference/src/astro_sph_tools/tools/projections/_projector.py:75-120
+(with process_chunk :13-73 and calculate_pixel_value, _pixel_calculations.pyx:9-36).
+
+Same signature, argument meaning and result: a fresh ``np.float64`` array of shape
+``(Nx, Ny)`` indexed ``img[x_index, y_index]``; pixel (xi, yi) samples the lower-left
+corner ``(x_min + xi*dx, y_min + yi*dy)`` with ``dy = (y_max - y_min)/Nx`` (reference
+quirk S2); the value is the sum of ``A_p W(r_p, h_p)`` over particles passing the
+reference's cull of the ``chunk_size`` tile holding the pixel and ``r_p^2 < (2h_p)^2``.
+
+Differences, all documented in DESIGN.md §6: values accumulate in float32 on the GPU
+(upcast on return; neighbour sets are decided with the reference's fp64 arithmetic
+and are identical); ``kernel_func`` must be one of this package's kernels (Python
+callables cannot run on the device -> TypeError); ``x_max > x_min`` and
+``y_max > y_min`` are required (ValueError); non-finite particle inputs are excluded.
+"""
+from __future__ import annotations
+
+import numbers
+
+import numpy as np
+
+from ... import _lib
+from ..._axes import AXIS_COLUMNS, axis_index
+from ._kernels import kernel_id_of, quartic_spline_kernel
+
+
+def _soa(positions, smoothing_lengths, particle_properties, projection_axis):
+    pos = np.asarray(positions)
+    if pos.ndim != 2 or pos.shape[1] != 3:
+        raise ValueError(f"positions must have shape (N, 3), got {pos.shape}")
+    h = np.asarray(smoothing_lengths).reshape(-1)
+    A = np.asarray(particle_properties).reshape(-1)
+    n = pos.shape[0]
+    if h.shape[0] != n or A.shape[0] != n:
+        raise ValueError(f"positions ({n}), smoothing_lengths ({h.shape[0]}) and "
+                         f"particle_properties ({A.shape[0]}) differ in length")
+    a, b = AXIS_COLUMNS[axis_index(projection_axis)]
+    f32 = np.float32
+    return (np.ascontiguousarray(pos[:, a], dtype=f32), np.ascontiguousarray(pos[:, b], dtype=f32),
+            np.ascontiguousarray(h, dtype=f32), np.ascontiguousarray(A, dtype=f32))
+
+
+def _check_chunk_size(chunk_size):
+    # the reference feeds chunk_size to range(0, N, chunk_size)
+    if not isinstance(chunk_size, numbers.Integral):
+        raise TypeError(f"'{type(chunk_size).__name__}' object cannot be interpreted as an integer")
+    if chunk_size == 0:
+        raise ValueError("range() arg 3 must not be zero")
+    return int(chunk_size)
+
+
+def _run(u, v, h, a0, a1, image_size, chunk_size, extent, kernel_id, flags, device):
+    nx, ny = int(image_size[0]), int(image_size[1])
+    out0 = np.zeros((nx, ny), dtype=np.float32)
+    out1 = None if a1 is None else np.zeros((nx, ny), dtype=np.float32)
+    if nx <= 0 or ny <= 0 or chunk_size < 0:
+        # empty image, or range(0, N, negative) -> no tiles -> all zeros (reference)
+        return out0, out1
+    _lib.require_gpu(device)
+    x_min, x_max, y_min, y_max = (float(np.asarray(e)) for e in extent)
+    P = _lib.ptr
+    _lib.check(_lib.lib().asp_project2d(
+        P(u), P(v), P(h), P(a0), P(a1), u.shape[0], x_min, x_max, y_min, y_max, nx, ny,
+        chunk_size, kernel_id, flags, P(out0), P(out1), device, None))
+    return out0, out1
+
+
+def create_image(positions: np.ndarray, smoothing_lengths: np.ndarray,
+                 particle_properties: np.ndarray, image_size: tuple, chunk_size: int,
+                 projection_axis, x_min: float, x_max: float, y_min: float, y_max: float,
+                 kernel_func=quartic_spline_kernel, *, device: int = 0,
+                 dtype=np.float64) -> np.ndarray:
+    """Project particle property A onto an (Nx, Ny) pixel grid (reference semantics).
+
+    ``device`` selects the GPU; ``dtype=np.float32`` skips the host upcast (opt-in).
+    """
+    cs = _check_chunk_size(chunk_size)
+    kid = kernel_id_of(kernel_func)
+    u, v, h, A = _soa(positions, smoothing_lengths, particle_properties, projection_axis)
+    img, _ = _run(u, v, h, A, None, image_size, cs, (x_min, x_max, y_min, y_max), kid, 0,
+                  device)
+    return img.astype(dtype, copy=False)
+
+
+def create_weighted_image(positions, smoothing_lengths, weights, values, image_size,
+                          chunk_size, projection_axis, x_min, x_max, y_min, y_max,
+                          kernel_func=quartic_spline_kernel, *, device: int = 0,
+                          return_components: bool = False, dtype=np.float64):
+    """Weighted-average map, e.g. mass-weighted temperature.
+
+    ``sum(w v W) / sum(w W)`` per pixel over the same neighbour sets as
+    :func:`create_image`, 0 where the denominator is 0.  Equals
+    ``create_image(.., w*v, ..) / create_image(.., w, ..)`` (two reference calls), computed
+    in one pass with both maps accumulated together.  With ``return_components`` the two
+    sums are returned as well: ``(ratio, sum_wvW, sum_wW)``.
+    """
+    cs = _check_chunk_size(chunk_size)
+    kid = kernel_id_of(kernel_func)
+    u, v, h, w = _soa(positions, smoothing_lengths, weights, projection_axis)
+    vals = np.asarray(values, dtype=np.float64).reshape(-1)
+    if vals.shape[0] != u.shape[0]:
+        raise ValueError("values and positions differ in length")
+    wv = np.ascontiguousarray(np.asarray(weights, np.float64).reshape(-1) * vals, dtype=np.float32)
+    if return_components:
+        s0, s1 = _run(u, v, h, wv, w, image_size, cs, (x_min, x_max, y_min, y_max), kid, 0,
+                      device)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ratio = np.where(s1 != 0, s0.astype(np.float64) / s1, 0.0)
+        return ratio.astype(dtype, copy=False), s0.astype(dtype), s1.astype(dtype)
+    r, _ = _run(u, v, h, wv, w, image_size, cs, (x_min, x_max, y_min, y_max), kid,
+                _lib.ASP_F_RATIO, device)
+    return r.astype(dtype, copy=False)

@@ -1,0 +1,1168 @@
+// asp_project2d.hip -- MI355X (gfx950) SPH particle -> pixel-grid projection.
+//
+// Replaces the reference's create_image / process_chunk / calculate_pixel_value /
+// quartic_spline_kernel path (/root/reference/src/astro_sph_tools/tools/projections/
+// _projector.py:13-120, _pixel_calculations.pyx:9-36, _kernels.pyx:9-20) with a
+// scatter formulation built for CDNA4:
+//
+//   K1 count     one streaming pass over (u, v, h): per-workgroup LDS histogram of
+//                (particle, GPU tile) insertions -> hist[block][tile]
+//   K2a colscan  per tile, exclusive prefix over blocks (in place) + tile totals
+//   K2b tilescan one workgroup: tile start offsets in Morton order of the tiles, and
+//                the deposit work list (runs of <= CH records of one tile)
+//   K3 scatter   second streaming pass: each insertion written as a 16/32-byte record
+//                into its tile's run (LDS cursors; coalesced record stores)
+//   K4 deposit   one workgroup per work item: records -> LDS tile accumulators
+//                (ds_add_f32), small footprints lane-per-record, large ones swept by
+//                a whole wave; tile written once (plain store or float atomics)
+//   K5 wide      particles overlapping > kWideTiles tiles, per tile, wave sweeps
+//   K6 ratio     optional out0 / out1 (mass-weighted maps)
+//
+// No MFMA: this is gather/scatter work; the bounds are HBM bytes and VALU/LDS-atomic
+// issue.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/asp.h"
+#include "asp_device.hpp"
+
+namespace asp {
+
+// ----------------------------------------------------------------------------------
+// K1: count insertions per (block, tile)
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_count(const float* __restrict__ u,
+                                                  const float* __restrict__ v,
+                                                  const float* __restrict__ h, long long n,
+                                                  long long per_block, Grid g,
+                                                  int* __restrict__ hist,
+                                                  int* __restrict__ wide_count) {
+    extern __shared__ __attribute__((aligned(16))) int lh[];
+    for (int t = threadIdx.x; t < g.ntiles; t += kBlock) lh[t] = 0;
+    __syncthreads();
+    long long p0 = (long long)blockIdx.x * per_block;
+    long long p1 = min(n, p0 + per_block);
+    int nwide = 0;
+    for (long long p = p0 + threadIdx.x; p < p1; p += kBlock) {
+        Box b;
+        if (!footprint(g, u[p], v[p], h[p], b)) continue;
+        int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
+        int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
+        if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > kWideTiles) {
+            ++nwide;
+            continue;
+        }
+        for (int tx = tx0; tx <= tx1; ++tx)
+            for (int ty = ty0; ty <= ty1; ++ty) atomicAdd(&lh[tx * g.nty + ty], 1);
+    }
+    if (nwide) atomicAdd(wide_count, nwide);
+    __syncthreads();
+    int* row = hist + (long long)blockIdx.x * g.ntiles;
+    for (int t = threadIdx.x; t < g.ntiles; t += kBlock) row[t] = lh[t];
+}
+
+// ----------------------------------------------------------------------------------
+// K2a: per tile, exclusive prefix of hist over blocks (in place); tile totals.
+// 64 tiles per workgroup (one per lane), the 4 waves split the block range.
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_colscan(int* __restrict__ hist, int nblk, int ntiles,
+                                                    int* __restrict__ tile_total) {
+    __shared__ int part[4][64];
+    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int t = blockIdx.x * 64 + lane;
+    int b0 = (int)((long long)nblk * w / 4), b1 = (int)((long long)nblk * (w + 1) / 4);
+    int s = 0;
+    if (t < ntiles) {
+        int b = b0;
+        for (; b + 8 <= b1; b += 8) {
+            int c[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) c[k] = hist[(long long)(b + k) * ntiles + t];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                hist[(long long)(b + k) * ntiles + t] = s;
+                s += c[k];
+            }
+        }
+        for (; b < b1; ++b) {
+            int c = hist[(long long)b * ntiles + t];
+            hist[(long long)b * ntiles + t] = s;
+            s += c;
+        }
+    }
+    part[w][lane] = s;
+    __syncthreads();
+    int off = 0;
+    for (int k = 0; k < w; ++k) off += part[k][lane];
+    if (t < ntiles) {
+        if (off)
+            for (int b = b0; b < b1; ++b) hist[(long long)b * ntiles + t] += off;
+        if (w == 3) tile_total[t] = off + s;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// K2b: single workgroup.  Tile start offsets in Morton order of the tiles (spatially
+// adjacent tiles' records are adjacent in HBM), and the deposit work list.
+// counters[0] = work items, counters[1] = total records (low 31 bits), counters[3] =
+// records per item.  Work items are also emitted in Morton order.
+// ----------------------------------------------------------------------------------
+constexpr int kScanThreads = 1024;
+constexpr int kTargetItems = 8192;
+constexpr int kMinItemRecords = 1024;
+
+__global__ __launch_bounds__(kScanThreads) void k_tilescan(const int* __restrict__ tile_total,
+                                                           const int* __restrict__ morton,
+                                                           int ntiles,
+                                                           long long* __restrict__ tile_start,
+                                                           Item* __restrict__ items,
+                                                           int* __restrict__ counters) {
+    __shared__ long long sred[kScanThreads];
+    __shared__ int sitem[kScanThreads];
+    int tid = threadIdx.x;
+    int per = (ntiles + kScanThreads - 1) / kScanThreads;
+    int r0 = min(ntiles, tid * per), r1 = min(ntiles, r0 + per);
+    long long loc = 0;
+    for (int r = r0; r < r1; ++r) loc += tile_total[morton[r]];
+    sred[tid] = loc;
+    __syncthreads();
+    // Hillis-Steele inclusive scan (1024 entries, once per call)
+    for (int o = 1; o < kScanThreads; o <<= 1) {
+        long long x = tid >= o ? sred[tid - o] : 0;
+        __syncthreads();
+        sred[tid] += x;
+        __syncthreads();
+    }
+    long long total = sred[kScanThreads - 1];
+    long long base = sred[tid] - loc;
+    int ch = (int)max((long long)kMinItemRecords, (total + kTargetItems - 1) / kTargetItems);
+    int nloc = 0;
+    for (int r = r0; r < r1; ++r) {
+        int t = morton[r];
+        int c = tile_total[t];
+        tile_start[t] = base;
+        base += c;
+        nloc += (c + ch - 1) / ch;
+    }
+    sitem[tid] = nloc;
+    __syncthreads();
+    for (int o = 1; o < kScanThreads; o <<= 1) {
+        int x = tid >= o ? sitem[tid - o] : 0;
+        __syncthreads();
+        sitem[tid] += x;
+        __syncthreads();
+    }
+    int ibase = sitem[tid] - nloc;
+    for (int r = r0; r < r1; ++r) {
+        int t = morton[r];
+        int c = tile_total[t];
+        int k = (c + ch - 1) / ch;
+        long long s0 = tile_start[t];
+        for (int j = 0; j < k; ++j) {
+            Item it;
+            it.start = s0 + (long long)j * ch;
+            it.tile = t;
+            it.count = min(ch, c - j * ch);
+            it.multi = k > 1;
+            it.pad = 0;
+            items[ibase + j] = it;
+        }
+        ibase += k;
+    }
+    if (tid == kScanThreads - 1) {
+        counters[0] = sitem[kScanThreads - 1];
+        counters[1] = (int)min(total, (long long)0x7fffffff);
+        counters[3] = ch;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// K3: scatter records into their tiles' runs.  Same particle partition as K1.
+// Record layout: NOUT == 1 -> float4 {u, v, h, a0};  NOUT == 2 -> 2 x float4
+// {u, v, h, a0}, {a1, 0, 0, 0}.
+// ----------------------------------------------------------------------------------
+template <int NOUT>
+__global__ __launch_bounds__(kBlock) void k_scatter(
+    const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
+    const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long per_block,
+    Grid g, const int* __restrict__ hist, const long long* __restrict__ tile_start,
+    float4* __restrict__ recs, int* __restrict__ wide_list, int* __restrict__ wide_cursor) {
+    extern __shared__ __attribute__((aligned(16))) int cur[];
+    const int* row = hist + (long long)blockIdx.x * g.ntiles;
+    for (int t = threadIdx.x; t < g.ntiles; t += kBlock) cur[t] = row[t];
+    __syncthreads();
+    long long p0 = (long long)blockIdx.x * per_block;
+    long long p1 = min(n, p0 + per_block);
+    for (long long p = p0 + threadIdx.x; p < p1; p += kBlock) {
+        float pu = u[p], pv = v[p], ph = h[p];
+        Box b;
+        if (!footprint(g, pu, pv, ph, b)) continue;
+        int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
+        int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
+        if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > kWideTiles) {
+            wide_list[atomicAdd(wide_cursor, 1)] = (int)p;
+            continue;
+        }
+        float4 r0 = make_float4(pu, pv, ph, a0[p]);
+        float4 r1 = make_float4(NOUT == 2 ? a1[p] : 0.0f, 0.0f, 0.0f, 0.0f);
+        for (int tx = tx0; tx <= tx1; ++tx)
+            for (int ty = ty0; ty <= ty1; ++ty) {
+                int t = tx * g.nty + ty;
+                long long slot = tile_start[t] + atomicAdd(&cur[t], 1);
+                if constexpr (NOUT == 1) {
+                    recs[slot] = r0;
+                } else {
+                    recs[2 * slot] = r0;
+                    recs[2 * slot + 1] = r1;
+                }
+            }
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// Pair accumulation into the LDS tile
+// ----------------------------------------------------------------------------------
+template <int KID, int NOUT>
+__device__ __forceinline__ void accumulate(const Prep& P, float r2, float* acc0, float* acc1,
+                                           int k) {
+    float q = __builtin_sqrtf(r2) * P.hinv;
+    float w = kernel_shape<KID>(q);
+    atomicAdd(&acc0[k], P.c0 * w);
+    if constexpr (NOUT == 2) atomicAdd(&acc1[k], P.c1 * w);
+}
+
+// One wave sweeps the (clipped) box of one wave-uniform record: lanes along y (the
+// contiguous image axis), so LDS atomics of a wave hit distinct consecutive words.
+template <int KID, int NOUT>
+__device__ __forceinline__ void sweep(const Grid& g, const Prep& P, int X0, int Y0,
+                                      const float* xt, const float* yt, float* acc0,
+                                      float* acc1, int lane) {
+    int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
+    if (bh <= 64) {
+        int rps = 64 / bh;
+        int r = lane / bh, c = lane - r * bh;
+        if (r < rps) {
+            int yi = P.b.y0 + c;
+            float Y = yt[yi - Y0];
+            for (int xi = P.b.x0 + r; xi <= P.b.x1; xi += rps) {
+                float r2;
+                if (decide(g, P, xi, yi, xt[xi - X0], Y, r2))
+                    accumulate<KID, NOUT>(P, r2, acc0, acc1, (xi - X0) * kTile + (yi - Y0));
+            }
+        }
+    } else {
+        for (int xi = P.b.x0; xi <= P.b.x1; ++xi) {
+            float X = xt[xi - X0];
+            for (int c = lane; c < bh; c += 64) {
+                int yi = P.b.y0 + c;
+                float r2;
+                if (decide(g, P, xi, yi, X, yt[yi - Y0], r2))
+                    accumulate<KID, NOUT>(P, r2, acc0, acc1, (xi - X0) * kTile + (yi - Y0));
+            }
+        }
+    }
+    (void)bw;
+}
+
+__device__ __forceinline__ Prep bcast_prep(const Prep& P, int l) {
+    Prep Q;
+    Q.u = bcast(P.u, l);
+    Q.v = bcast(P.v, l);
+    Q.h = bcast(P.h, l);
+    Q.thr = bcast(P.thr, l);
+    Q.band = bcast(P.band, l);
+    Q.hinv = bcast(P.hinv, l);
+    Q.c0 = bcast(P.c0, l);
+    Q.c1 = bcast(P.c1, l);
+    Q.b.x0 = bcast(P.b.x0, l);
+    Q.b.x1 = bcast(P.b.x1, l);
+    Q.b.y0 = bcast(P.b.y0, l);
+    Q.b.y1 = bcast(P.b.y1, l);
+    return Q;
+}
+
+__device__ __forceinline__ bool clip(Box& b, int X0, int Y0, int TW, int TH) {
+    b.x0 = max(b.x0, X0);
+    b.x1 = min(b.x1, X0 + TW - 1);
+    b.y0 = max(b.y0, Y0);
+    b.y1 = min(b.y1, Y0 + TH - 1);
+    return b.x0 <= b.x1 && b.y0 <= b.y1;
+}
+
+template <int NOUT>
+__device__ __forceinline__ void load_rec(const float4* recs, long long i, float& u, float& v,
+                                         float& h, float& a0, float& a1) {
+    if constexpr (NOUT == 1) {
+        float4 r = recs[i];
+        u = r.x; v = r.y; h = r.z; a0 = r.w; a1 = 0.0f;
+    } else {
+        float4 r = recs[2 * i];
+        float4 s = recs[2 * i + 1];
+        u = r.x; v = r.y; h = r.z; a0 = r.w; a1 = s.x;
+    }
+}
+
+// Tile prologue: zero accumulators, fp32 corner tables (exact fp64 corners rounded).
+template <int NOUT>
+__device__ __forceinline__ void tile_prologue(const Grid& g, int X0, int Y0, float* smem) {
+    for (int i = threadIdx.x; i < NOUT * kTile * kTile; i += kBlock) smem[i] = 0.0f;
+    float* xt = smem + NOUT * kTile * kTile;
+    float* yt = xt + kTile;
+    if (threadIdx.x < kTile)
+        xt[threadIdx.x] = (float)corner_x(g, X0 + threadIdx.x);
+    else if (threadIdx.x < 2 * kTile)
+        yt[threadIdx.x - kTile] = (float)corner_y(g, Y0 + threadIdx.x - kTile);
+    __syncthreads();
+}
+
+template <int NOUT>
+__device__ __forceinline__ void tile_epilogue(const Grid& g, int X0, int Y0, int TW, int TH,
+                                              const float* smem, float* out0, float* out1,
+                                              bool atomic) {
+    __syncthreads();
+    for (int k = threadIdx.x; k < kTile * kTile; k += kBlock) {
+        int lx = k >> kTileShift, ly = k & (kTile - 1);
+        if (lx >= TW || ly >= TH) continue;
+        long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
+        float a = smem[k];
+        if (atomic) {
+            if (a != 0.0f) atomicAdd(&out0[o], a);
+        } else {
+            out0[o] = a;
+        }
+        if constexpr (NOUT == 2) {
+            float b = smem[kTile * kTile + k];
+            if (atomic) {
+                if (b != 0.0f) atomicAdd(&out1[o], b);
+            } else {
+                out1[o] = b;
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// K4: deposit one work item (a run of records of one tile) into LDS, write the tile.
+// ----------------------------------------------------------------------------------
+template <int KID, int NOUT>
+__global__ __launch_bounds__(kBlock) void k_deposit(Grid g, const float4* __restrict__ recs,
+                                                    const Item* __restrict__ items,
+                                                    float* __restrict__ out0,
+                                                    float* __restrict__ out1, int accumulate_all) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* acc0 = smem;
+    float* acc1 = smem + kTile * kTile;
+    const float* xt = smem + NOUT * kTile * kTile;
+    const float* yt = xt + kTile;
+    const Item it = items[blockIdx.x];
+    int tx = it.tile / g.nty, ty = it.tile - (it.tile / g.nty) * g.nty;
+    int X0 = tx * kTile, Y0 = ty * kTile;
+    int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
+    tile_prologue<NOUT>(g, X0, Y0, smem);
+    int lane = threadIdx.x & 63;
+    for (int base = 0; base < it.count; base += kBlock) {
+        int i = base + threadIdx.x;
+        Prep P;
+        P.b = Box{0, -1, 0, -1};
+        bool live = false;
+        if (i < it.count) {
+            float pu, pv, ph, pa0, pa1;
+            load_rec<NOUT>(recs, it.start + i, pu, pv, ph, pa0, pa1);
+            live = prep_record<KID>(g, pu, pv, ph, pa0, pa1, P) && clip(P.b, X0, Y0, TW, TH);
+        }
+        int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
+        bool small = live && bw <= 4 && bh <= 4;
+        if (small) {
+            // lane-per-record: <= 4 x 4 box, dy^2 per column kept in registers
+            float dy2[4];
+            int yc[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                int yi = min(P.b.y0 + j, P.b.y1);
+                yc[j] = yi;
+                float dy = P.v - yt[yi - Y0];
+                dy2[j] = dy * dy;
+            }
+#pragma unroll
+            for (int ii = 0; ii < 4; ++ii) {
+                if (ii < bw) {
+                    int xi = P.b.x0 + ii;
+                    float X = xt[xi - X0];
+                    float dx = P.u - X;
+                    float dx2 = dx * dx;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (j < bh) {
+                            float r2 = dx2 + dy2[j];
+                            bool in = r2 < P.thr;
+                            if (fabsf(r2 - P.thr) <= P.band)
+                                in = exact_pair(g, P.u, P.v, P.h, xi, yc[j]);
+                            if (in)
+                                accumulate<KID, NOUT>(P, r2, acc0, acc1,
+                                                      (xi - X0) * kTile + (yc[j] - Y0));
+                        }
+                    }
+                }
+            }
+        }
+        unsigned long long big = __ballot(live && !small);
+        while (big) {
+            int l = __builtin_ctzll(big);
+            big &= big - 1;
+            Prep Q = bcast_prep(P, l);
+            sweep<KID, NOUT>(g, Q, X0, Y0, xt, yt, acc0, acc1, lane);
+        }
+    }
+    tile_epilogue<NOUT>(g, X0, Y0, TW, TH, smem, out0, out1, accumulate_all || it.multi);
+}
+
+// ----------------------------------------------------------------------------------
+// K5: wide particles (footprint over > kWideTiles tiles).  One workgroup per tile,
+// each wave takes every 4th wide particle and sweeps its clipped box.
+// ----------------------------------------------------------------------------------
+template <int KID, int NOUT>
+__global__ __launch_bounds__(kBlock) void k_wide(Grid g, const float* __restrict__ u,
+                                                 const float* __restrict__ v,
+                                                 const float* __restrict__ h,
+                                                 const float* __restrict__ a0,
+                                                 const float* __restrict__ a1,
+                                                 const int* __restrict__ wide_list, int n_wide,
+                                                 float* __restrict__ out0,
+                                                 float* __restrict__ out1) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* acc0 = smem;
+    float* acc1 = smem + kTile * kTile;
+    const float* xt = smem + NOUT * kTile * kTile;
+    const float* yt = xt + kTile;
+    int t = blockIdx.x;
+    int tx = t / g.nty, ty = t - (t / g.nty) * g.nty;
+    int X0 = tx * kTile, Y0 = ty * kTile;
+    int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
+    tile_prologue<NOUT>(g, X0, Y0, smem);
+    int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int* any = (int*)(smem + NOUT * kTile * kTile + 2 * kTile);
+    if (threadIdx.x == 0) *any = 0;
+    __syncthreads();
+    for (int k = wv; k < n_wide; k += kBlock / 64) {
+        int p = wide_list[k];
+        Prep P;
+        if (!prep_record<KID>(g, u[p], v[p], h[p], a0[p], NOUT == 2 ? a1[p] : 0.0f, P)) continue;
+        if (!clip(P.b, X0, Y0, TW, TH)) continue;
+        if (lane == 0) *any = 1;
+        sweep<KID, NOUT>(g, P, X0, Y0, xt, yt, acc0, acc1, lane);
+    }
+    __syncthreads();
+    if (*any) tile_epilogue<NOUT>(g, X0, Y0, TW, TH, smem, out0, out1, true);
+}
+
+// K6: out0 <- out0 / out1 (0 where out1 == 0).
+__global__ __launch_bounds__(kBlock) void k_ratio(float* __restrict__ out0,
+                                                  const float* __restrict__ out1, long long m) {
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    long long stride = (long long)gridDim.x * kBlock;
+    for (; i < m; i += stride) {
+        float d = out1[i];
+        out0[i] = d != 0.0f ? out0[i] / d : 0.0f;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// Auxiliary entry points: kernel evaluation, chunk ranges, neighbour lists.
+// ----------------------------------------------------------------------------------
+__global__ void k_kernel_eval(int kid, const double* __restrict__ r, const double* __restrict__ h,
+                              double* __restrict__ w, long long n) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double q = r[i] / h[i];
+    double res = 0.0;
+    if (kid == ASP_KERNEL_CUBIC_SPLINE) {  // _kernels.pyx:13-19, same branch order
+        if (q < 1.0)
+            res = (1 - 1.5 * pow(q, 2.0) + 0.75 * pow(q, 3.0)) / (M_PI * pow(h[i], 3.0));
+        else if (q < 2.0)
+            res = (0.25 * pow((2 - q), 3.0)) / (M_PI * pow(h[i], 3.0));
+    } else if (kid == ASP_KERNEL_WENDLAND_C2) {
+        if (q < 2.0) {
+            double t = 1.0 - 0.5 * q;
+            res = 21.0 / (16.0 * M_PI * pow(h[i], 3.0)) * pow(t, 4.0) * (1.0 + 2.0 * q);
+        }
+    } else {
+        res = 1.0;
+    }
+    w[i] = res;
+}
+
+__global__ void k_chunk_ranges(Grid g, const float* __restrict__ u, const float* __restrict__ v,
+                               const float* __restrict__ h, long long n, int* cx0, int* cx1,
+                               int* cy0, int* cy1) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int a, b, c, d;
+    chunk_range((double)u[i], (double)h[i], g.x_min, g.psx, g.nx, g.cs, a, b);
+    chunk_range((double)v[i], (double)h[i], g.y_min, g.psy_cull, g.ny, g.cs, c, d);
+    cx0[i] = a;
+    cx1[i] = b;
+    cy0[i] = c;
+    cy1[i] = d;
+}
+
+// Neighbour lists: one workgroup per pixel, particles in ascending order.  The decision
+// is the deposit's (footprint box, then decide()), so this lists exactly the pairs the
+// deposit accumulates.  pass 0 counts, pass 1 writes at offsets[pixel].
+__global__ __launch_bounds__(kBlock) void k_neighbours(Grid g, const float* __restrict__ u,
+                                                       const float* __restrict__ v,
+                                                       const float* __restrict__ h, long long n,
+                                                       const long long* __restrict__ pixels,
+                                                       long long* __restrict__ counts,
+                                                       const long long* __restrict__ offsets,
+                                                       int* __restrict__ index, long long cap,
+                                                       int pass) {
+    __shared__ int wsum[kBlock / 64];
+    __shared__ long long run;
+    long long pix = pixels[blockIdx.x];
+    int xi = (int)(pix / g.ny), yi = (int)(pix - (pix / g.ny) * g.ny);
+    float X = (float)corner_x(g, xi), Y = (float)corner_y(g, yi);
+    if (threadIdx.x == 0) run = pass ? offsets[blockIdx.x] : 0;
+    __syncthreads();
+    int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (long long base = 0; base < n; base += kBlock) {
+        long long p = base + threadIdx.x;
+        bool in = false;
+        if (p < n) {
+            Prep P;
+            if (prep_record<2>(g, u[p], v[p], h[p], 0.0f, 0.0f, P) && xi >= P.b.x0 &&
+                xi <= P.b.x1 && yi >= P.b.y0 && yi <= P.b.y1) {
+                float r2;
+                in = decide(g, P, xi, yi, X, Y, r2);
+            }
+        }
+        unsigned long long m = __ballot(in);
+        if (lane == 0) wsum[wv] = __popcll(m);
+        __syncthreads();
+        int before = 0, tot = 0;
+        for (int k = 0; k < kBlock / 64; ++k) {
+            if (k < wv) before += wsum[k];
+            tot += wsum[k];
+        }
+        if (pass && in) {
+            long long slot = run + before + __popcll(m & ((1ull << lane) - 1ull));
+            if (slot < cap) index[slot] = (int)p;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) run += tot;
+        __syncthreads();
+    }
+    if (!pass && threadIdx.x == 0) counts[blockIdx.x] = run;
+}
+
+// ----------------------------------------------------------------------------------
+// Host runtime
+// ----------------------------------------------------------------------------------
+static thread_local std::string t_err;
+
+static int fail(int code, const std::string& msg) {
+    t_err = msg;
+    return code;
+}
+
+#define ASP_HIP(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail(ASP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+constexpr int kStages = 8;  // memset, count, colscan, tilescan, scatter, deposit, wide, ratio
+enum Stage { kSMemset = 0, kSCount, kSColscan, kSTilescan, kSScatter, kSDeposit, kSWide, kSRatio };
+
+struct Workspace {
+    std::mutex mu;
+    // HIP-event profiling (asp_profile): per-stage start/stop events of the last call,
+    // folded into the running sums at the next call or at asp_profile_read.
+    bool prof = false;
+    hipEvent_t ev[2 * kStages] = {};
+    bool ev_live[kStages] = {};
+    double stage_ms[kStages] = {};
+    long long stage_n[kStages] = {};
+    Buf in[5], out[2], hist, tile_total, tile_start, items, counters, recs, wide, morton, aux[6];
+    int* h_counters = nullptr;  // pinned
+    int morton_ntx = -1, morton_nty = -1;
+    long long stats[8] = {0};
+};
+
+static Workspace g_ws[64];
+
+static int prof_fold(Workspace& ws) {
+    for (int k = 0; k < kStages; ++k) {
+        if (!ws.ev_live[k]) continue;
+        ASP_HIP(hipEventSynchronize(ws.ev[2 * k + 1]));
+        float ms = 0.0f;
+        ASP_HIP(hipEventElapsedTime(&ms, ws.ev[2 * k], ws.ev[2 * k + 1]));
+        ws.stage_ms[k] += ms;
+        ws.stage_n[k] += 1;
+        ws.ev_live[k] = false;
+    }
+    return ASP_OK;
+}
+
+// RAII-free stage bracket: record start/stop events around a launch when profiling.
+struct StageMark {
+    Workspace& ws;
+    int k;
+    hipStream_t st;
+    StageMark(Workspace& w, int stage, hipStream_t s) : ws(w), k(stage), st(s) {
+        if (ws.prof) (void)hipEventRecord(ws.ev[2 * k], st);
+    }
+    void done() {
+        if (ws.prof) {
+            (void)hipEventRecord(ws.ev[2 * k + 1], st);
+            ws.ev_live[k] = true;
+        }
+    }
+};
+
+static int ensure(Buf& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return ASP_OK;
+    if (b.p) {
+        hipError_t e = hipFree(b.p);
+        (void)e;
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    size_t want = bytes + bytes / 4;
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) {
+        e = hipMalloc(&b.p, bytes);
+        want = bytes;
+    }
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        return fail(ASP_ERR_NOMEM, "hipMalloc(" + std::to_string(bytes) + ") failed: " +
+                                       hipGetErrorString(e));
+    }
+    b.cap = want;
+    return ASP_OK;
+}
+
+#define ASP_TRY(expr)             \
+    do {                          \
+        int rc_ = (expr);         \
+        if (rc_ != ASP_OK) return rc_; \
+    } while (0)
+
+static uint32_t spread_bits(uint32_t x) {
+    x &= 0xffff;
+    x = (x | (x << 8)) & 0x00ff00ff;
+    x = (x | (x << 4)) & 0x0f0f0f0f;
+    x = (x | (x << 2)) & 0x33333333;
+    x = (x | (x << 1)) & 0x55555555;
+    return x;
+}
+
+static int ensure_morton(Workspace& ws, int ntx, int nty, hipStream_t st) {
+    if (ws.morton_ntx == ntx && ws.morton_nty == nty) return ASP_OK;
+    std::vector<std::pair<uint32_t, int>> key((size_t)ntx * nty);
+    for (int tx = 0; tx < ntx; ++tx)
+        for (int ty = 0; ty < nty; ++ty)
+            key[(size_t)tx * nty + ty] = {spread_bits(tx) << 1 | spread_bits(ty), tx * nty + ty};
+    std::sort(key.begin(), key.end());
+    std::vector<int> order(key.size());
+    for (size_t i = 0; i < key.size(); ++i) order[i] = key[i].second;
+    ASP_TRY(ensure(ws.morton, order.size() * sizeof(int)));
+    ASP_HIP(hipMemcpyAsync(ws.morton.p, order.data(), order.size() * sizeof(int),
+                           hipMemcpyHostToDevice, st));
+    ASP_HIP(hipStreamSynchronize(st));
+    ws.morton_ntx = ntx;
+    ws.morton_nty = nty;
+    return ASP_OK;
+}
+
+static bool make_grid(double x_min, double x_max, double y_min, double y_max, int nx, int ny,
+                      int cs, Grid& g) {
+    if (!(nx > 0 && ny > 0 && cs > 0)) return false;
+    if (!(x_max > x_min) || !(y_max > y_min)) return false;
+    if (!std::isfinite(x_min) || !std::isfinite(x_max) || !std::isfinite(y_min) ||
+        !std::isfinite(y_max))
+        return false;
+    g.x_min = x_min;
+    g.y_min = y_min;
+    g.psx = (x_max - x_min) / nx;
+    g.psy_pix = (y_max - y_min) / nx;
+    g.psy_cull = (y_max - y_min) / ny;
+    double mg = std::max({std::fabs(x_min), std::fabs(x_min + nx * g.psx), std::fabs(y_min),
+                          std::fabs(y_min + ny * g.psy_pix)});
+    g.mg = (float)(mg * (1.0 + 1e-6));
+    g.nx = nx;
+    g.ny = ny;
+    g.cs = cs;
+    g.ncx = (nx + cs - 1) / cs;
+    g.ncy = (ny + cs - 1) / cs;
+    g.ntx = (nx + kTile - 1) / kTile;
+    g.nty = (ny + kTile - 1) / kTile;
+    g.ntiles = g.ntx * g.nty;
+    g.nonsquare = nx != ny;
+    return true;
+}
+
+constexpr int kMaxTiles = 16384;  // K1/K3 LDS histogram limit (64 KiB)
+
+template <int KID, int NOUT>
+static int launch_deposit(const Grid& g, Workspace& ws, int n_items, const float* u,
+                          const float* v, const float* h, const float* a0, const float* a1,
+                          int n_wide, float* o0, float* o1, bool accumulate, hipStream_t st) {
+    size_t lds = (size_t)(NOUT * kTile * kTile + 2 * kTile + 4) * sizeof(float);
+    if (n_items > 0) {
+        StageMark m(ws, kSDeposit, st);
+        hipLaunchKernelGGL((k_deposit<KID, NOUT>), dim3(n_items), dim3(kBlock), lds, st, g,
+                           (const float4*)ws.recs.p, (const Item*)ws.items.p, o0, o1,
+                           accumulate ? 1 : 0);
+        ASP_HIP(hipGetLastError());
+        m.done();
+    }
+    if (n_wide > 0) {
+        StageMark m(ws, kSWide, st);
+        hipLaunchKernelGGL((k_wide<KID, NOUT>), dim3(g.ntiles), dim3(kBlock), lds, st, g, u, v,
+                           h, a0, a1, (const int*)ws.wide.p, n_wide, o0, o1);
+        ASP_HIP(hipGetLastError());
+        m.done();
+    }
+    return ASP_OK;
+}
+
+static int project2d(const float* u, const float* v, const float* h, const float* a0,
+                     const float* a1, long long n, double x_min, double x_max, double y_min,
+                     double y_max, int nx, int ny, int cs, int kid, int flags, float* out0,
+                     float* out1, int device, void* stream) {
+    if (n < 0) return fail(ASP_ERR_INVALID, "n < 0");
+    if (kid < 0 || kid > 2) return fail(ASP_ERR_INVALID, "unknown kernel_id");
+    if (!out0) return fail(ASP_ERR_INVALID, "out0 is NULL");
+    if ((a1 == nullptr) != (out1 == nullptr))
+        return fail(ASP_ERR_INVALID, "a1 and out1 must both be given or both be NULL");
+    if ((flags & ASP_F_RATIO) && !out1) return fail(ASP_ERR_INVALID, "ASP_F_RATIO needs out1");
+    if ((flags & ASP_F_RATIO) && (flags & ASP_F_ACCUMULATE))
+        return fail(ASP_ERR_INVALID, "ASP_F_RATIO cannot be combined with ASP_F_ACCUMULATE");
+    if (n > 0 && (!u || !v || !h || !a0)) return fail(ASP_ERR_INVALID, "NULL particle array");
+    if (n > 0x7fffffffLL) return fail(ASP_ERR_UNSUPPORTED, "n >= 2^31 particles per call");
+    Grid g;
+    if (!make_grid(x_min, x_max, y_min, y_max, nx, ny, cs, g))
+        return fail(ASP_ERR_INVALID,
+                    "invalid grid: need nx, ny, chunk_size >= 1, finite x_max > x_min, "
+                    "y_max > y_min");
+    if (g.ntiles > kMaxTiles)
+        return fail(ASP_ERR_UNSUPPORTED, "grid too large (more than 16384 64x64 tiles)");
+    if (device < 0 || device >= 64) return fail(ASP_ERR_INVALID, "bad device");
+    int ndev = 0;
+    ASP_HIP(hipGetDeviceCount(&ndev));
+    if (device >= ndev) return fail(ASP_ERR_INVALID, "device index out of range");
+    ASP_HIP(hipSetDevice(device));
+    Workspace& ws = g_ws[device];
+    std::lock_guard<std::mutex> lock(ws.mu);
+    hipStream_t st = (hipStream_t)stream;
+    const int nout = out1 ? 2 : 1;
+    const bool dev = flags & ASP_F_DEVICE_PTRS;
+    const long long npix = (long long)nx * ny;
+
+    // stage host inputs
+    const float* du = u;
+    const float* dv = v;
+    const float* dh = h;
+    const float* da0 = a0;
+    const float* da1 = a1;
+    float* d0 = out0;
+    float* d1 = out1;
+    if (!dev) {
+        const float* src[5] = {u, v, h, a0, a1};
+        for (int k = 0; k < 4 + (nout == 2); ++k) {
+            ASP_TRY(ensure(ws.in[k], (size_t)n * sizeof(float)));
+            if (n > 0)
+                ASP_HIP(hipMemcpyAsync(ws.in[k].p, src[k], (size_t)n * sizeof(float),
+                                       hipMemcpyHostToDevice, st));
+        }
+        du = (const float*)ws.in[0].p;
+        dv = (const float*)ws.in[1].p;
+        dh = (const float*)ws.in[2].p;
+        da0 = (const float*)ws.in[3].p;
+        da1 = nout == 2 ? (const float*)ws.in[4].p : nullptr;
+        for (int k = 0; k < nout; ++k) ASP_TRY(ensure(ws.out[k], (size_t)npix * sizeof(float)));
+        d0 = (float*)ws.out[0].p;
+        d1 = nout == 2 ? (float*)ws.out[1].p : nullptr;
+        if (flags & ASP_F_ACCUMULATE) {
+            ASP_HIP(hipMemcpyAsync(d0, out0, npix * sizeof(float), hipMemcpyHostToDevice, st));
+            if (d1)
+                ASP_HIP(hipMemcpyAsync(d1, out1, npix * sizeof(float), hipMemcpyHostToDevice, st));
+        }
+    }
+    const bool accumulate = flags & ASP_F_ACCUMULATE;
+    if (ws.prof) ASP_TRY(prof_fold(ws));
+    if (!accumulate) {
+        StageMark m(ws, kSMemset, st);
+        ASP_HIP(hipMemsetAsync(d0, 0, npix * sizeof(float), st));
+        if (d1) ASP_HIP(hipMemsetAsync(d1, 0, npix * sizeof(float), st));
+        m.done();
+    }
+
+    int n_items = 0, n_wide = 0;
+    long long n_recs = 0;
+    if (n > 0) {
+        ASP_TRY(ensure_morton(ws, g.ntx, g.nty, st));
+        long long nblk = std::min<long long>(1024, std::max<long long>(1, (n + 4095) / 4096));
+        long long per_block = (n + nblk - 1) / nblk;
+        nblk = (n + per_block - 1) / per_block;
+        ASP_TRY(ensure(ws.hist, (size_t)nblk * g.ntiles * sizeof(int)));
+        ASP_TRY(ensure(ws.tile_total, (size_t)g.ntiles * sizeof(int)));
+        ASP_TRY(ensure(ws.tile_start, (size_t)g.ntiles * sizeof(long long)));
+        ASP_TRY(ensure(ws.items, (size_t)(g.ntiles + kTargetItems + 16) * sizeof(Item)));
+        ASP_TRY(ensure(ws.counters, 16 * sizeof(int)));
+        if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, 16 * sizeof(int)));
+        int* dc = (int*)ws.counters.p;
+        ASP_HIP(hipMemsetAsync(dc, 0, 16 * sizeof(int), st));
+        size_t lds_hist = (size_t)g.ntiles * sizeof(int);
+        {
+            StageMark m(ws, kSCount, st);
+            hipLaunchKernelGGL(k_count, dim3((unsigned)nblk), dim3(kBlock), lds_hist, st, du, dv,
+                               dh, n, per_block, g, (int*)ws.hist.p, dc + 2);
+            ASP_HIP(hipGetLastError());
+            m.done();
+        }
+        {
+            StageMark m(ws, kSColscan, st);
+            hipLaunchKernelGGL(k_colscan, dim3((g.ntiles + 63) / 64), dim3(kBlock), 0, st,
+                               (int*)ws.hist.p, (int)nblk, g.ntiles, (int*)ws.tile_total.p);
+            ASP_HIP(hipGetLastError());
+            m.done();
+        }
+        {
+            StageMark m(ws, kSTilescan, st);
+            hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(kScanThreads), 0, st,
+                               (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles,
+                               (long long*)ws.tile_start.p, (Item*)ws.items.p, dc);
+            ASP_HIP(hipGetLastError());
+            m.done();
+        }
+        ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, 16 * sizeof(int), hipMemcpyDeviceToHost, st));
+        ASP_HIP(hipStreamSynchronize(st));
+        n_items = ws.h_counters[0];
+        n_recs = ws.h_counters[1];
+        n_wide = ws.h_counters[2];
+        if (n_recs >= 0x7fffffffLL)
+            return fail(ASP_ERR_UNSUPPORTED, "more than 2^31 particle-tile records");
+        ASP_TRY(ensure(ws.recs, (size_t)n_recs * nout * sizeof(float4)));
+        ASP_TRY(ensure(ws.wide, (size_t)n_wide * sizeof(int)));
+        StageMark ms(ws, kSScatter, st);
+        if (nout == 1)
+            hipLaunchKernelGGL((k_scatter<1>), dim3((unsigned)nblk), dim3(kBlock), lds_hist, st,
+                               du, dv, dh, da0, da1, n, per_block, g, (const int*)ws.hist.p,
+                               (const long long*)ws.tile_start.p, (float4*)ws.recs.p,
+                               (int*)ws.wide.p, dc + 4);
+        else
+            hipLaunchKernelGGL((k_scatter<2>), dim3((unsigned)nblk), dim3(kBlock), lds_hist, st,
+                               du, dv, dh, da0, da1, n, per_block, g, (const int*)ws.hist.p,
+                               (const long long*)ws.tile_start.p, (float4*)ws.recs.p,
+                               (int*)ws.wide.p, dc + 4);
+        ASP_HIP(hipGetLastError());
+        ms.done();
+        int rc;
+#define ASP_DEP(K, N) \
+    launch_deposit<K, N>(g, ws, n_items, du, dv, dh, da0, da1, n_wide, d0, d1, accumulate, st)
+        if (kid == 0)
+            rc = nout == 1 ? ASP_DEP(0, 1) : ASP_DEP(0, 2);
+        else if (kid == 1)
+            rc = nout == 1 ? ASP_DEP(1, 1) : ASP_DEP(1, 2);
+        else
+            rc = nout == 1 ? ASP_DEP(2, 1) : ASP_DEP(2, 2);
+#undef ASP_DEP
+        if (rc != ASP_OK) return rc;
+    }
+    if (flags & ASP_F_RATIO) {
+        long long blocks = std::min<long long>((npix + kBlock - 1) / kBlock, 8192);
+        StageMark m(ws, kSRatio, st);
+        hipLaunchKernelGGL(k_ratio, dim3((unsigned)std::max<long long>(1, blocks)), dim3(kBlock),
+                           0, st, d0, (const float*)d1, npix);
+        ASP_HIP(hipGetLastError());
+        m.done();
+    }
+    if (!dev) {
+        ASP_HIP(hipMemcpyAsync(out0, d0, npix * sizeof(float), hipMemcpyDeviceToHost, st));
+        if (out1)
+            ASP_HIP(hipMemcpyAsync(out1, d1, npix * sizeof(float), hipMemcpyDeviceToHost, st));
+        ASP_HIP(hipStreamSynchronize(st));
+    }
+    ws.stats[0] = n_recs;
+    ws.stats[1] = n_items;
+    ws.stats[2] = n_wide;
+    ws.stats[3] = kTile;
+    ws.stats[4] = g.ntiles;
+    ws.stats[5] = n > 0 && ws.h_counters ? ws.h_counters[3] : 0;
+    return ASP_OK;
+}
+
+}  // namespace asp
+
+// ==================================================================================
+// C-ABI
+// ==================================================================================
+using namespace asp;
+
+extern "C" {
+
+int asp_version(void) { return ASP_API_VERSION * 10000 + 1; }
+
+const char* asp_last_error(void) { return t_err.c_str(); }
+
+int asp_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int asp_project2d(const float* u, const float* v, const float* h, const float* a0,
+                  const float* a1, int64_t n, double u_min, double u_max, double v_min,
+                  double v_max, int32_t nx, int32_t ny, int32_t chunk_size, int32_t kernel_id,
+                  int32_t flags, float* out0, float* out1, int32_t device, void* stream) {
+    t_err.clear();
+    return project2d(u, v, h, a0, a1, n, u_min, u_max, v_min, v_max, nx, ny, chunk_size,
+                     kernel_id, flags, out0, out1, device, stream);
+}
+
+int asp_kernel_eval(int32_t kernel_id, const double* r, const double* h, double* w, int64_t n,
+                    int32_t flags, int32_t device, void* stream) {
+    t_err.clear();
+    if (kernel_id < 0 || kernel_id > 2) return fail(ASP_ERR_INVALID, "unknown kernel_id");
+    if (n < 0) return fail(ASP_ERR_INVALID, "n < 0");
+    if (n == 0) return ASP_OK;
+    int ndev = 0;
+    ASP_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(ASP_ERR_INVALID, "bad device");
+    ASP_HIP(hipSetDevice(device));
+    Workspace& ws = g_ws[device];
+    std::lock_guard<std::mutex> lock(ws.mu);
+    hipStream_t st = (hipStream_t)stream;
+    const double *dr = r, *dh = h;
+    double* dw = w;
+    bool dev = flags & ASP_F_DEVICE_PTRS;
+    if (!dev) {
+        ASP_TRY(ensure(ws.aux[0], n * sizeof(double)));
+        ASP_TRY(ensure(ws.aux[1], n * sizeof(double)));
+        ASP_TRY(ensure(ws.aux[2], n * sizeof(double)));
+        ASP_HIP(hipMemcpyAsync(ws.aux[0].p, r, n * sizeof(double), hipMemcpyHostToDevice, st));
+        ASP_HIP(hipMemcpyAsync(ws.aux[1].p, h, n * sizeof(double), hipMemcpyHostToDevice, st));
+        dr = (const double*)ws.aux[0].p;
+        dh = (const double*)ws.aux[1].p;
+        dw = (double*)ws.aux[2].p;
+    }
+    hipLaunchKernelGGL(k_kernel_eval, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       (int)kernel_id, dr, dh, dw, (long long)n);
+    ASP_HIP(hipGetLastError());
+    if (!dev) {
+        ASP_HIP(hipMemcpyAsync(w, dw, n * sizeof(double), hipMemcpyDeviceToHost, st));
+        ASP_HIP(hipStreamSynchronize(st));
+    }
+    return ASP_OK;
+}
+
+int asp_chunk_ranges(const float* u, const float* v, const float* h, int64_t n, double u_min,
+                     double u_max, double v_min, double v_max, int32_t nx, int32_t ny,
+                     int32_t chunk_size, int32_t* cx0, int32_t* cx1, int32_t* cy0, int32_t* cy1,
+                     int32_t flags, int32_t device, void* stream) {
+    t_err.clear();
+    Grid g;
+    if (!make_grid(u_min, u_max, v_min, v_max, nx, ny, chunk_size, g))
+        return fail(ASP_ERR_INVALID, "invalid grid");
+    if (n < 0) return fail(ASP_ERR_INVALID, "n < 0");
+    if (n == 0) return ASP_OK;
+    int ndev = 0;
+    ASP_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(ASP_ERR_INVALID, "bad device");
+    ASP_HIP(hipSetDevice(device));
+    Workspace& ws = g_ws[device];
+    std::lock_guard<std::mutex> lock(ws.mu);
+    hipStream_t st = (hipStream_t)stream;
+    bool dev = flags & ASP_F_DEVICE_PTRS;
+    const float *du = u, *dv = v, *dh = h;
+    int* o[4] = {cx0, cx1, cy0, cy1};
+    if (!dev) {
+        const float* src[3] = {u, v, h};
+        for (int k = 0; k < 3; ++k) {
+            ASP_TRY(ensure(ws.in[k], n * sizeof(float)));
+            ASP_HIP(hipMemcpyAsync(ws.in[k].p, src[k], n * sizeof(float), hipMemcpyHostToDevice,
+                                   st));
+        }
+        du = (const float*)ws.in[0].p;
+        dv = (const float*)ws.in[1].p;
+        dh = (const float*)ws.in[2].p;
+        for (int k = 0; k < 4; ++k) {
+            ASP_TRY(ensure(ws.aux[k], n * sizeof(int)));
+            o[k] = (int*)ws.aux[k].p;
+        }
+    }
+    hipLaunchKernelGGL(k_chunk_ranges, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g,
+                       du, dv, dh, (long long)n, o[0], o[1], o[2], o[3]);
+    ASP_HIP(hipGetLastError());
+    if (!dev) {
+        int* dst[4] = {cx0, cx1, cy0, cy1};
+        for (int k = 0; k < 4; ++k)
+            ASP_HIP(hipMemcpyAsync(dst[k], o[k], n * sizeof(int), hipMemcpyDeviceToHost, st));
+        ASP_HIP(hipStreamSynchronize(st));
+    }
+    return ASP_OK;
+}
+
+int asp_pixel_neighbours(const float* u, const float* v, const float* h, int64_t n,
+                         double u_min, double u_max, double v_min, double v_max, int32_t nx,
+                         int32_t ny, int32_t chunk_size, const int64_t* pixels, int64_t npix,
+                         int64_t* offsets, int32_t* index, int64_t cap, int64_t* total,
+                         int32_t device) {
+    t_err.clear();
+    Grid g;
+    if (!make_grid(u_min, u_max, v_min, v_max, nx, ny, chunk_size, g))
+        return fail(ASP_ERR_INVALID, "invalid grid");
+    if (n < 0 || npix < 0 || cap < 0) return fail(ASP_ERR_INVALID, "negative size");
+    for (int64_t k = 0; k < npix; ++k)
+        if (pixels[k] < 0 || pixels[k] >= (int64_t)nx * ny)
+            return fail(ASP_ERR_INVALID, "pixel id out of range");
+    offsets[0] = 0;
+    if (total) *total = 0;
+    if (npix == 0) return ASP_OK;
+    if (n == 0) {
+        for (int64_t k = 0; k < npix; ++k) offsets[k + 1] = 0;
+        return ASP_OK;
+    }
+    int ndev = 0;
+    ASP_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(ASP_ERR_INVALID, "bad device");
+    ASP_HIP(hipSetDevice(device));
+    Workspace& ws = g_ws[device];
+    std::lock_guard<std::mutex> lock(ws.mu);
+    hipStream_t st = nullptr;
+    const float* src[3] = {u, v, h};
+    for (int k = 0; k < 3; ++k) {
+        ASP_TRY(ensure(ws.in[k], n * sizeof(float)));
+        ASP_HIP(hipMemcpyAsync(ws.in[k].p, src[k], n * sizeof(float), hipMemcpyHostToDevice, st));
+    }
+    ASP_TRY(ensure(ws.aux[0], npix * sizeof(long long)));
+    ASP_TRY(ensure(ws.aux[1], npix * sizeof(long long)));
+    ASP_TRY(ensure(ws.aux[2], (npix + 1) * sizeof(long long)));
+    ASP_HIP(hipMemcpyAsync(ws.aux[0].p, pixels, npix * sizeof(long long), hipMemcpyHostToDevice,
+                           st));
+    hipLaunchKernelGGL(k_neighbours, dim3((unsigned)npix), dim3(kBlock), 0, st, g,
+                       (const float*)ws.in[0].p, (const float*)ws.in[1].p,
+                       (const float*)ws.in[2].p, (long long)n, (const long long*)ws.aux[0].p,
+                       (long long*)ws.aux[1].p, (const long long*)nullptr, (int*)nullptr, 0LL, 0);
+    ASP_HIP(hipGetLastError());
+    std::vector<long long> cnt(npix);
+    ASP_HIP(hipMemcpyAsync(cnt.data(), ws.aux[1].p, npix * sizeof(long long),
+                           hipMemcpyDeviceToHost, st));
+    ASP_HIP(hipStreamSynchronize(st));
+    for (int64_t k = 0; k < npix; ++k) offsets[k + 1] = offsets[k] + cnt[k];
+    long long tot = offsets[npix];
+    if (total) *total = tot;
+    long long wcap = std::min<long long>(cap, tot);
+    if (wcap > 0) {
+        ASP_TRY(ensure(ws.aux[3], wcap * sizeof(int)));
+        ASP_HIP(hipMemcpyAsync(ws.aux[2].p, offsets, npix * sizeof(long long),
+                               hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_neighbours, dim3((unsigned)npix), dim3(kBlock), 0, st, g,
+                           (const float*)ws.in[0].p, (const float*)ws.in[1].p,
+                           (const float*)ws.in[2].p, (long long)n, (const long long*)ws.aux[0].p,
+                           (long long*)ws.aux[1].p, (const long long*)ws.aux[2].p,
+                           (int*)ws.aux[3].p, wcap, 1);
+        ASP_HIP(hipGetLastError());
+        ASP_HIP(hipMemcpyAsync(index, ws.aux[3].p, wcap * sizeof(int), hipMemcpyDeviceToHost, st));
+        ASP_HIP(hipStreamSynchronize(st));
+    }
+    return ASP_OK;
+}
+
+int asp_ratio(float* out0, const float* out1, int64_t n, int32_t device, void* stream) {
+    t_err.clear();
+    if (n < 0 || !out0 || !out1) return fail(ASP_ERR_INVALID, "bad argument");
+    if (n == 0) return ASP_OK;
+    int ndev = 0;
+    ASP_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(ASP_ERR_INVALID, "bad device");
+    ASP_HIP(hipSetDevice(device));
+    long long blocks = std::min<long long>((n + kBlock - 1) / kBlock, 8192);
+    hipLaunchKernelGGL(k_ratio, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream,
+                       out0, out1, (long long)n);
+    ASP_HIP(hipGetLastError());
+    return ASP_OK;
+}
+
+int asp_profile(int32_t device, int32_t enable) {
+    t_err.clear();
+    int ndev = asp_device_count();
+    if (device < 0 || device >= ndev) return fail(ASP_ERR_INVALID, "bad device");
+    ASP_HIP(hipSetDevice(device));
+    Workspace& ws = g_ws[device];
+    std::lock_guard<std::mutex> lock(ws.mu);
+    if (enable && !ws.ev[0])
+        for (int k = 0; k < 2 * kStages; ++k) ASP_HIP(hipEventCreate(&ws.ev[k]));
+    for (int k = 0; k < kStages; ++k) {
+        ws.stage_ms[k] = 0.0;
+        ws.stage_n[k] = 0;
+        ws.ev_live[k] = false;
+    }
+    ws.prof = enable != 0;
+    return ASP_OK;
+}
+
+int asp_profile_read(int32_t device, double* ms_sum, int64_t* launches, int32_t nstages) {
+    t_err.clear();
+    if (device < 0 || device >= 64 || !ms_sum || !launches)
+        return fail(ASP_ERR_INVALID, "bad argument");
+    Workspace& ws = g_ws[device];
+    std::lock_guard<std::mutex> lock(ws.mu);
+    if (ws.prof) {
+        ASP_HIP(hipSetDevice(device));
+        ASP_TRY(prof_fold(ws));
+    }
+    for (int k = 0; k < nstages; ++k) {
+        ms_sum[k] = k < kStages ? ws.stage_ms[k] : 0.0;
+        launches[k] = k < kStages ? ws.stage_n[k] : 0;
+    }
+    return ASP_OK;
+}
+
+int asp_last_stats(int32_t device, int64_t* stats, int32_t nstats) {
+    if (device < 0 || device >= 64 || !stats) return fail(ASP_ERR_INVALID, "bad argument");
+    for (int k = 0; k < nstats && k < 8; ++k) stats[k] = g_ws[device].stats[k];
+    return ASP_OK;
+}
+
+int asp_release(int32_t device) {
+    int lo = device < 0 ? 0 : device, hi = device < 0 ? 63 : device;
+    int ndev = asp_device_count();
+    for (int d = lo; d <= hi && d < ndev; ++d) {
+        Workspace& ws = g_ws[d];
+        std::lock_guard<std::mutex> lock(ws.mu);
+        if (hipSetDevice(d) != hipSuccess) continue;
+        Buf* all[] = {&ws.in[0], &ws.in[1], &ws.in[2], &ws.in[3], &ws.in[4], &ws.out[0],
+                      &ws.out[1], &ws.hist, &ws.tile_total, &ws.tile_start, &ws.items,
+                      &ws.counters, &ws.recs, &ws.wide, &ws.morton, &ws.aux[0], &ws.aux[1],
+                      &ws.aux[2], &ws.aux[3], &ws.aux[4], &ws.aux[5]};
+        for (Buf* b : all) {
+            if (b->p) (void)hipFree(b->p);
+            b->p = nullptr;
+            b->cap = 0;
+        }
+        if (ws.h_counters) (void)hipHostFree(ws.h_counters);
+        ws.h_counters = nullptr;
+        ws.morton_ntx = ws.morton_nty = -1;
+    }
+    return ASP_OK;
+}
+
+}  // extern "C"

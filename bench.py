@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark: 10^8-particle -> 4096^2 projection on 1..8 MI355X.
+
+Workload (BASELINE.json configs[2], the metric's "10^8-particle 4096^2 projection"):
+10^8 Plummer particles -> 4096^2 mass-weighted-temperature map (sum m T W / sum m W),
+Wendland-C2, fp32, pixel-scale smoothing lengths (h = 0.75 px, the HBM-bound case of
+SURVEY.md §8(d)).  Inputs are generated on the device and resident in HBM before the
+timed region.  With N ranks the particles are Z-slab sharded (equal counts) and one RCCL
+reduce sums the two component maps on rank 0 (strong scaling: total work fixed).
+
+One "step" = one full map: binning + deposit + (N > 1) RCCL reduce + ratio.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      torchrun --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "astro-sph-tools_amd"))
+
+METRIC = "Mpixels/s + particles/s, 10^8-particle 4096² projection at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=100_000_000)
+    ap.add_argument("--grid", type=int, default=4096)
+    ap.add_argument("--h-law", default="pixel", choices=["pixel", "physical"])
+    ap.add_argument("--kernel", default="wendland_c2", choices=["wendland_c2", "cubic"])
+    ap.add_argument("--map", default="weighted", choices=["weighted", "surface"])
+    ap.add_argument("--op", default="reduce", choices=["reduce", "allreduce", "reduce_scatter"])
+    ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="budget for the bounded CPU-baseline sample")
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_latest.json"),
+                    help="PMC summary (tools/pmc_summary.py) for roofline.traffic")
+    ap.add_argument("--quiet", action="store_true")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(args, extent):
+    """The oracle's gather restatement of the reference path on the host cores, over a
+    bounded random sample of the map's 64x64 chunks (all particles culled per chunk, as
+    the reference does); extrapolated to the full map."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    from asp_amd.plummer import plummer
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    t0 = time.time()
+    p = plummer(args.n, seed=0, h_law=args.h_law, grid=args.grid, extent=extent)
+    pos = p["pos"].astype(np.float32).astype(np.float64)
+    h = p["h"].astype(np.float32).astype(np.float64)
+    m = p["m"].astype(np.float32).astype(np.float64)
+    T = p["T"].astype(np.float32).astype(np.float64)
+    del p
+    maps = [m * T, m] if args.map == "weighted" else [m]
+    log(f"[cpu] host data {time.time() - t0:.1f}s; sampling chunks with {cores} threads")
+    cs = 64
+    nch = (args.grid // cs) ** 2
+    order = np.random.default_rng(0).permutation(nch)
+    done, spent, batch = 0, 0.0, max(cores, 8)
+    while done < nch and spent < args.cpu_seconds:
+        ids = order[done:done + batch]
+        t = time.perf_counter()
+        for A in maps:
+            pyoracle.create_image(pos, h, A, (args.grid, args.grid), cs, 2, *([-extent, extent] * 2),
+                                  kernel=args.kernel, nthreads=cores, chunk_ids=ids)
+        spent += time.perf_counter() - t
+        done += ids.size
+    full_s = spent * nch / done
+    mpix = args.grid * args.grid / full_s / 1e6
+    return {"value": mpix, "unit": "Mpixels/s", "cores": cores, "kind": "port",
+            "particles_per_s": args.n / full_s,
+            "sample": f"{done} of {nch} random 64x64 chunks of the {args.n:.0e}-particle "
+                      f"{args.grid}^2 map ({len(maps)} reference-style create_image call(s)), "
+                      f"oracle gather restatement (fp64, per-chunk O(N) cull), {spent:.1f}s "
+                      f"measured, extrapolated to the full map"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    from asp_amd import _lib
+    from asp_amd.device import project2d, stats
+    from asp_amd.distributed import project2d_sharded, zslab_bounds
+    from asp_amd.plummer import plummer_torch
+
+    G, extent = args.grid, 4.0
+    ext = (-extent, extent, -extent, extent)
+    t0 = time.time()
+    d = plummer_torch(args.n, seed=0, h_law=args.h_law, extent=extent, grid=G, device=dev)
+    if world > 1:
+        e = zslab_bounds(d["z"], world)
+        keep = (d["z"] >= e[rank]) & (d["z"] < e[rank + 1])
+        d = {k: v[keep].contiguous() for k, v in d.items()}
+    u, v, h = d["x"], d["y"], d["h"]
+    if args.map == "weighted":
+        a0, a1 = (d["m"] * d["T"]).contiguous(), d["m"]
+    else:
+        a0, a1 = d["m"], None
+    del d["z"], d["T"]
+    n_local = u.shape[0]
+    torch.cuda.synchronize()
+    if not args.quiet:
+        log(f"[rank {rank}] data ready: {n_local} particles in {time.time() - t0:.1f}s")
+
+    ratio = args.map == "weighted"
+    out0 = torch.empty((G, G), dtype=torch.float32, device=dev)
+    out1 = torch.empty((G, G), dtype=torch.float32, device=dev) if a1 is not None else None
+
+    def step():
+        if world > 1:
+            return project2d_sharded(u, v, h, a0, a1, image_size=(G, G), extent=ext,
+                                     kernel=args.kernel, ratio=ratio, op=args.op, out0=out0,
+                                     out1=out1)
+        return project2d(u, v, h, a0, a1, image_size=(G, G), extent=ext, kernel=args.kernel,
+                         ratio=ratio, out0=out0, out1=out1)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _lib.profile(local, True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t
+    prof = _lib.profile_read(local)
+    _lib.profile(local, False)
+    st = stats(local)
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ok = bool(torch.isfinite(out0).all().item()) and float(out0.abs().sum().item()) > 0
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    ms_step = elapsed / args.steps * 1e3
+    mpix = G * G * args.steps / elapsed / 1e6
+    pps = args.n * args.steps / elapsed
+    nout = 2 if a1 is not None else 1
+    b_p = 4 * (3 + nout)  # u, v, h + one property per output map
+    bytes_alg = n_local * b_p + nout * G * G * 4
+    stages = {k: {"ms_per_launch": (ms / n if n else 0.0), "launches": n}
+              for k, (ms, n) in prof.items()}
+    dom = max(prof, key=lambda k: prof[k][0])
+    dom_ms = prof[dom][0] / max(1, prof[dom][1])
+    achieved = bytes_alg / (dom_ms * 1e-3) / 1e9
+    pipeline_ms = sum(ms for ms, n in prof.values()) / args.steps
+    traffic = None
+    traffic_src = None
+    try:
+        with open(args.pmc) as f:
+            pm = json.load(f)
+        key = f"n{args.n}_g{G}_{args.kernel}_{args.h_law}_{args.map}"
+        if key in pm and dom in pm[key]:
+            traffic = pm[key][dom]["hbm_bytes_per_launch"]
+            traffic_src = pm[key].get("source")
+    except (OSError, ValueError, KeyError):
+        pass
+    res = {
+        "metric": METRIC, "value": round(mpix, 3), "unit": "Mpixels/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic Plummer sphere (a=1, M=1, seed 0) generated in HBM",
+        "config": {"workload": f"cfg3: {args.n:.0e} particles -> {G}^2 "
+                               f"{'mass-weighted temperature' if ratio else 'surface density'} "
+                               f"map, {args.kernel}, {args.h_law}-scale h, fp32"
+                               + (f", Z-slab x{world} + RCCL {args.op}" if world > 1 else ""),
+                   "particles": args.n, "grid": G, "kernel": args.kernel, "h_law": args.h_law,
+                   "map": args.map, "parallelism": f"zslab{world}" if world > 1 else "single"},
+        "particles_per_s": pps,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "bytes_alg_per_launch": bytes_alg,
+                     "pipeline_frac": round(bytes_alg / (pipeline_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "stages": stages,
+        "records_per_particle": round(st["records"] / max(1, n_local), 4),
+        "work_items": st["items"], "wide_particles": st["wide"],
+        "output_ok": ok,
+    }
+    want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
+    if want_cpu:
+        try:
+            res["cpu_baseline"] = cpu_baseline(args, extent)
+        except Exception as exc:  # a baseline failure must not hide the GPU number
+            res["cpu_baseline"] = {"error": repr(exc)}
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,150 @@
+/*
+ * asp.h -- C-ABI of the MI355X-native SPH particle-to-grid projector (libasp_hip.so).
+ *
+ * Drop-in boundary for astro_sph_tools' map-rendering path.  Each entry point names
+ * the reference interface it replaces (paths under
+ * /root/reference/src/astro_sph_tools/).  The Python mirror of the reference API
+ * (astro-sph-tools_amd/asp_amd/) binds these with ctypes; INTEGRATION.md shows the
+ * binding a maintainer would add to the reference itself.
+ *
+ * Conventions
+ *  - plain pointers and sizes only; no C++ or torch types cross this boundary;
+ *  - every function returns ASP_OK (0) or a negative ASP_ERR_* code, and sets a
+ *    thread-local message readable with asp_last_error();
+ *  - inputs are borrowed and never written; outputs are written in full;
+ *  - particle inputs are float32 structure-of-arrays, already axis-selected: (u, v) are
+ *    the two projected coordinates (X -> (y, z), Y -> (x, z), Z -> (x, y);
+ *    _projector.py:38-46, _pixel_calculations.pyx:20-28);
+ *  - images are (nx, ny) C-order float32, element [xi * ny + yi] (_projector.py:88,117);
+ *  - by default pointers are HOST pointers (the library stages them through HBM);
+ *    with ASP_F_DEVICE_PTRS they are device pointers on `device` and the call is
+ *    ordered on `stream` (a hipStream_t, NULL = the legacy default stream);
+ *  - thread-safe: a per-device workspace cache guarded by a mutex; one call at a time
+ *    per device.
+ */
+#ifndef ASP_H
+#define ASP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ASP_API_VERSION 1
+
+/* kernel_id: the SPH kernel W(r, h), support 2h, 3-D normalisation, evaluated at the
+ * projected 2-D distance (reference semantics S6). */
+#define ASP_KERNEL_CUBIC_SPLINE 0 /* _kernels.pyx:9-20 quartic_spline_kernel (M4 cubic)  */
+#define ASP_KERNEL_WENDLAND_C2 1  /* 21/(16 pi h^3) (1-q/2)^4 (1+2q), build-defined      */
+#define ASP_KERNEL_INDICATOR 2    /* W = 1 for every included pair: neighbour counting    */
+
+/* flags */
+#define ASP_F_DEVICE_PTRS 0x1 /* inputs/outputs are device pointers on `device`            */
+#define ASP_F_RATIO 0x2       /* two outputs: out0 <- out0 / out1 (0 where out1 == 0)      */
+#define ASP_F_ACCUMULATE 0x4  /* add into out0/out1 instead of overwriting                 */
+
+/* errors */
+#define ASP_OK 0
+#define ASP_ERR_INVALID -1     /* bad argument (ValueError on the Python side)             */
+#define ASP_ERR_HIP -2         /* HIP runtime error                                         */
+#define ASP_ERR_NOMEM -3       /* device allocation failed                                  */
+#define ASP_ERR_UNSUPPORTED -4 /* valid request this build does not implement               */
+
+/* Library version (ASP_API_VERSION * 10000 + build number). */
+int asp_version(void);
+
+/* Message for the last failing call on this thread ("" if none). */
+const char *asp_last_error(void);
+
+/* Number of visible HIP devices (0 on a host without a GPU; never fails). */
+int asp_device_count(void);
+
+/*
+ * 2-D projection: replaces create_image (_projector.py:75-120) together with
+ * process_chunk (:13-73), calculate_pixel_value (_pixel_calculations.pyx:9-36) and the
+ * kernel (_kernels.pyx:9-20).
+ *
+ *   out0[xi, yi] = sum_p a0[p] * W(r_p, h_p)   over p passing the reference's cull of
+ *                  the chunk_size tile holding (xi, yi) AND r_p^2 < (2 h_p)^2,
+ *   r_p^2 = (u_p - X_xi)^2 + (v_p - Y_yi)^2,  X_xi = u_min + xi * (u_max-u_min)/nx,
+ *   Y_yi = v_min + yi * (v_max - v_min)/nx   (sic: nx -- reference quirk S2).
+ *
+ * Neighbour membership is decided with the reference's fp64 arithmetic (bit-exact
+ * neighbour sets); values are accumulated in fp32.  a1/out1 (both non-NULL or both
+ * NULL) give a second map over the same neighbour sets (mass-weighted maps:
+ * a0 = m*T, a1 = m, with ASP_F_RATIO).  n == 0 is valid (all-zero image).
+ * chunk_size >= 1 is the reference's tile size; it only changes results for
+ * non-square images (quirk S2), exactly as in the reference.
+ */
+int asp_project2d(const float *u, const float *v, const float *h, const float *a0,
+                  const float *a1, int64_t n, double u_min, double u_max, double v_min,
+                  double v_max, int32_t nx, int32_t ny, int32_t chunk_size, int32_t kernel_id,
+                  int32_t flags, float *out0, float *out1, int32_t device, void *stream);
+
+/*
+ * Kernel evaluation on the device: replaces quartic_spline_kernel(r, h)
+ * (_kernels.pyx:9-20) for kernel_id 0; fp64 in and out, same formula and branch order.
+ * Host pointers unless ASP_F_DEVICE_PTRS.
+ */
+int asp_kernel_eval(int32_t kernel_id, const double *r, const double *h, double *w, int64_t n,
+                    int32_t flags, int32_t device, void *stream);
+
+/*
+ * Bin assignment (the reference's process_chunk cull, _projector.py:38-48): for every
+ * particle, the inclusive range of chunk indices [cx0, cx1] x [cy0, cy1] whose cull it
+ * passes (empty when cx0 > cx1 or cy0 > cy1).  Computed on the device in fp64 with the
+ * reference's operation order; bit-exact membership.  Host pointers unless
+ * ASP_F_DEVICE_PTRS.
+ */
+int asp_chunk_ranges(const float *u, const float *v, const float *h, int64_t n, double u_min,
+                     double u_max, double v_min, double v_max, int32_t nx, int32_t ny,
+                     int32_t chunk_size, int32_t *cx0, int32_t *cx1, int32_t *cy0,
+                     int32_t *cy1, int32_t flags, int32_t device, void *stream);
+
+/*
+ * Neighbour sets of selected pixels (calculate_pixel_value's mask,
+ * _pixel_calculations.pyx:30-31, restricted to the chunk cull): for pixel k
+ * (id = xi * ny + yi), the ascending particle indices in
+ * index[offsets[k] .. offsets[k+1]).  Uses the same device inclusion test as
+ * asp_project2d.  *total receives the number of pairs; when it exceeds cap, nothing
+ * beyond cap is written and the call returns ASP_OK with *total > cap.
+ * Host pointers only (a test/inspection entry point).
+ */
+int asp_pixel_neighbours(const float *u, const float *v, const float *h, int64_t n,
+                         double u_min, double u_max, double v_min, double v_max, int32_t nx,
+                         int32_t ny, int32_t chunk_size, const int64_t *pixels, int64_t npix,
+                         int64_t *offsets, int32_t *index, int64_t cap, int64_t *total,
+                         int32_t device);
+
+/*
+ * Weighted-map finalisation: out0[i] <- out1[i] != 0 ? out0[i] / out1[i] : 0 for the n
+ * elements (what ASP_F_RATIO does inside asp_project2d; used after a cross-GPU sum of
+ * the two component maps).  Device pointers only, ordered on `stream`.
+ */
+int asp_ratio(float *out0, const float *out1, int64_t n, int32_t device, void *stream);
+
+/*
+ * Statistics of the last asp_project2d call on `device` (inspection / roofline):
+ * stats[0] = records binned (particle x GPU-tile insertions), stats[1] = work items,
+ * stats[2] = wide particles, stats[3] = GPU tile edge (pixels), stats[4] = GPU tiles.
+ */
+int asp_last_stats(int32_t device, int64_t *stats, int32_t nstats);
+
+/*
+ * Stage timing with HIP events recorded on the call's stream around every launch
+ * (enable != 0 starts and resets, 0 stops).  asp_profile_read returns, per stage, the
+ * summed milliseconds and the number of launches since the last reset.  Stages:
+ * 0 memset, 1 count, 2 colscan, 3 tilescan, 4 scatter, 5 deposit, 6 wide, 7 ratio.
+ */
+int asp_profile(int32_t device, int32_t enable);
+int asp_profile_read(int32_t device, double *ms_sum, int64_t *launches, int32_t nstages);
+
+/* Release the cached device workspace of `device` (-1: all devices). */
+int asp_release(int32_t device);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ASP_H */

@@ -1,0 +1,160 @@
+"""ctypes binding of the CPU oracle (oracle/asp_oracle.c).
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` as the checker.  The product path never imports it.
+
+Inputs are the reference's own: positions (N, 3) float64, smoothing lengths, properties,
+``CoordinateAxes`` value (0/1/2) -> (u, v) columns exactly as
+``_projector.py:38-46`` / ``_pixel_calculations.pyx:20-28`` select them.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+KERNELS = {"cubic": 0, "quartic_spline_kernel": 0, "wendland_c2": 1, "indicator": 2}
+AXIS_COLS = {0: (1, 2), 1: (0, 2), 2: (0, 1)}
+
+_lib = None
+
+_d = C.POINTER(C.c_double)
+_i64 = C.POINTER(C.c_int64)
+_i32 = C.POINTER(C.c_int32)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.oracle_kernel_eval.argtypes = [C.c_int, _d, _d, _d, C.c_int64]
+        L.oracle_create_image.argtypes = [_d, _d, _d, _d, C.c_int64, C.c_int, C.c_int, C.c_int,
+                                          C.c_double, C.c_double, C.c_double, C.c_double, C.c_int,
+                                          _i64, C.c_int64, C.c_int, _d]
+        L.oracle_chunk_members.argtypes = [_d, _d, _d, C.c_int64, C.c_int, C.c_int, C.c_int,
+                                           C.c_double, C.c_double, C.c_double, C.c_double,
+                                           _i64, _i32, C.c_int64]
+        L.oracle_chunk_members.restype = C.c_int64
+        L.oracle_pixel_neighbours.argtypes = [_d, _d, _d, C.c_int64, C.c_int, C.c_int, C.c_int,
+                                              C.c_double, C.c_double, C.c_double, C.c_double,
+                                              _i64, C.c_int64, _i64, _i32, C.c_int64]
+        L.oracle_pixel_neighbours.restype = C.c_int64
+        L.oracle_project_scatter.argtypes = [_d, _d, _d, _d, _d, C.c_int64, C.c_int, C.c_int,
+                                             C.c_int, C.c_double, C.c_double, C.c_double,
+                                             C.c_double, C.c_int, C.c_int, _d, _d]
+        L.oracle_chunk_ranges.argtypes = [_d, _d, _d, C.c_int64, C.c_int, C.c_int, C.c_int,
+                                          C.c_double, C.c_double, C.c_double, C.c_double,
+                                          _i32, _i32, _i32, _i32]
+        _lib = L
+    return _lib
+
+
+def _p(a, t=_d):
+    return a.ctypes.data_as(t) if a is not None else None
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _uv(positions, axis):
+    positions = np.asarray(positions, dtype=np.float64).reshape(-1, 3)
+    a, b = AXIS_COLS[int(getattr(axis, "value", axis))]
+    return _f64(positions[:, a]), _f64(positions[:, b])
+
+
+def kernel_eval(kernel, r, h):
+    r, h = _f64(r), _f64(h)
+    w = np.empty_like(r)
+    lib().oracle_kernel_eval(KERNELS[kernel], _p(r), _p(h), _p(w), r.size)
+    return w
+
+
+def create_image(positions, smoothing_lengths, particle_properties, image_size, chunk_size,
+                 projection_axis, x_min, x_max, y_min, y_max, kernel="cubic", nthreads=0,
+                 chunk_ids=None):
+    """Reference-exact restatement of ``create_image`` (gather, fp64)."""
+    u, v = _uv(positions, projection_axis)
+    h, A = _f64(smoothing_lengths), _f64(particle_properties)
+    nx, ny = int(image_size[0]), int(image_size[1])
+    img = np.zeros((nx, ny), dtype=np.float64)
+    ids = None if chunk_ids is None else np.ascontiguousarray(chunk_ids, dtype=np.int64)
+    rc = lib().oracle_create_image(_p(u), _p(v), _p(h), _p(A), u.size, nx, ny, int(chunk_size),
+                                   float(x_min), float(x_max), float(y_min), float(y_max),
+                                   KERNELS[kernel], _p(ids, _i64), 0 if ids is None else ids.size,
+                                   int(nthreads), _p(img))
+    if rc != 0:
+        raise RuntimeError(f"oracle_create_image failed ({rc})")
+    return img
+
+
+def project_scatter(u, v, h, a0, a1, image_size, chunk_size, x_min, x_max, y_min, y_max,
+                    kernel="cubic", nthreads=0):
+    """O(pairs) restatement; returns (out0, out1-or-None), float64 (nx, ny)."""
+    u, v, h, a0 = _f64(u), _f64(v), _f64(h), _f64(a0)
+    a1 = None if a1 is None else _f64(a1)
+    nx, ny = int(image_size[0]), int(image_size[1])
+    o0 = np.empty((nx, ny), np.float64)
+    o1 = None if a1 is None else np.empty((nx, ny), np.float64)
+    rc = lib().oracle_project_scatter(_p(u), _p(v), _p(h), _p(a0), _p(a1), u.size, nx, ny,
+                                      int(chunk_size), float(x_min), float(x_max), float(y_min),
+                                      float(y_max), KERNELS[kernel], int(nthreads), _p(o0), _p(o1))
+    if rc != 0:
+        raise RuntimeError(f"oracle_project_scatter failed ({rc})")
+    return o0, o1
+
+
+def chunk_members(positions, smoothing_lengths, image_size, chunk_size, projection_axis,
+                  x_min, x_max, y_min, y_max):
+    u, v = _uv(positions, projection_axis)
+    h = _f64(smoothing_lengths)
+    nx, ny, cs = int(image_size[0]), int(image_size[1]), int(chunk_size)
+    nch = ((nx + cs - 1) // cs) * ((ny + cs - 1) // cs)
+    offs = np.zeros(nch + 1, np.int64)
+    cap = max(1, u.size * 4)
+    while True:
+        idx = np.empty(cap, np.int32)
+        t = lib().oracle_chunk_members(_p(u), _p(v), _p(h), u.size, nx, ny, cs, float(x_min),
+                                       float(x_max), float(y_min), float(y_max), _p(offs, _i64),
+                                       _p(idx, _i32), cap)
+        if t >= 0:
+            return offs, idx[:t]
+        cap = -t
+
+
+def pixel_neighbours(positions, smoothing_lengths, image_size, chunk_size, projection_axis,
+                     x_min, x_max, y_min, y_max, pixels):
+    u, v = _uv(positions, projection_axis)
+    h = _f64(smoothing_lengths)
+    pix = np.ascontiguousarray(pixels, dtype=np.int64)
+    offs = np.zeros(pix.size + 1, np.int64)
+    cap = max(1, u.size)
+    while True:
+        idx = np.empty(cap, np.int32)
+        t = lib().oracle_pixel_neighbours(_p(u), _p(v), _p(h), u.size, int(image_size[0]),
+                                          int(image_size[1]), int(chunk_size), float(x_min),
+                                          float(x_max), float(y_min), float(y_max), _p(pix, _i64),
+                                          pix.size, _p(offs, _i64), _p(idx, _i32), cap)
+        if t >= 0:
+            return offs, idx[:t]
+        cap = -t
+
+
+def chunk_ranges(u, v, h, image_size, chunk_size, x_min, x_max, y_min, y_max):
+    u, v, h = _f64(u), _f64(v), _f64(h)
+    out = [np.empty(u.size, np.int32) for _ in range(4)]
+    lib().oracle_chunk_ranges(_p(u), _p(v), _p(h), u.size, int(image_size[0]), int(image_size[1]),
+                              int(chunk_size), float(x_min), float(x_max), float(y_min),
+                              float(y_max), *[_p(o, _i32) for o in out])
+    return tuple(out)

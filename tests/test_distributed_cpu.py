@@ -1,0 +1,103 @@
+"""Multi-rank path on CPU: world_size 2 over gloo (127.0.0.1).
+
+Each rank keeps one Z-slab of the particles, projects it onto the full grid, and
+``project2d_sharded`` combines the grids with one collective.  The local projection is
+injected (the CPU oracle), so this checks the sharding and collective logic; the GPU
+projection itself is covered by the -m gpu parity tests.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import PKG_ROOT, REPO
+
+G = 64
+EXT = (-2.0, 2.0, -2.0, 2.0)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _oracle_projector(u, v, h, a0, a1, *, image_size, extent, chunk_size, kernel, ratio,
+                      out0, out1):
+    import pyoracle
+    o0, o1 = pyoracle.project_scatter(u.numpy(), v.numpy(), h.numpy(), a0.numpy(),
+                                      None if a1 is None else a1.numpy(), image_size,
+                                      chunk_size, *extent, kernel=kernel)
+    t0 = torch.from_numpy(o0.astype(np.float32))
+    t1 = None if o1 is None else torch.from_numpy(o1.astype(np.float32))
+    return t0, t1
+
+
+def _data():
+    import sys
+    sys.path.insert(0, PKG_ROOT)
+    from asp_amd.plummer import plummer
+    p = plummer(4000, seed=2, h_law="physical")
+    f = lambda a: torch.tensor(np.asarray(a, np.float32))  # noqa: E731
+    return f(p["pos"][:, 0]), f(p["pos"][:, 1]), f(p["pos"][:, 2]), f(p["h"]), f(p["m"]), f(p["T"])
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, PKG_ROOT)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from asp_amd.distributed import project2d_sharded, zslab_bounds
+        x, y, z, h, m, T = _data()
+        e = zslab_bounds(z, world)
+        keep = (z >= e[rank]) & (z < e[rank + 1])
+        sl = [t[keep].contiguous() for t in (x, y, h, m, T)]
+        res = {}
+        for op in ("reduce", "allreduce", "reduce_scatter"):
+            o0, o1 = project2d_sharded(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3],
+                                       image_size=(G, G), extent=EXT, chunk_size=16,
+                                       kernel="cubic", op=op, projector=_oracle_projector)
+            res[op] = (o0.numpy().copy(), o1.numpy().copy())
+        res["n_local"] = int(keep.sum())
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_zslab_sharded_sum_world2():
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    x, y, z, h, m, T = _data()
+    full0, full1 = pyoracle.project_scatter(x.numpy(), y.numpy(), h.numpy(), (m * T).numpy(),
+                                            m.numpy(), (G, G), 16, *EXT, kernel="cubic")
+    assert out[0]["n_local"] + out[1]["n_local"] == x.numel()
+    assert abs(out[0]["n_local"] - out[1]["n_local"]) < 0.1 * x.numel()
+    tol = 1e-5 * np.abs(full0).max()
+    np.testing.assert_allclose(out[0]["reduce"][0], full0, atol=tol, rtol=0)  # dst = 0
+    np.testing.assert_allclose(out[0]["reduce"][1], full1, atol=1e-5 * np.abs(full1).max(), rtol=0)
+    for r in range(world):
+        np.testing.assert_allclose(out[r]["allreduce"][0], full0, atol=tol, rtol=0)
+        rows = slice(r * G // world, (r + 1) * G // world)
+        np.testing.assert_allclose(out[r]["reduce_scatter"][0], full0[rows], atol=tol, rtol=0)
+    # the slabs really are partial maps: neither rank alone holds the full map
+    assert not np.allclose(out[1]["reduce"][0], full0, atol=tol)

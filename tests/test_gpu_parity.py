@@ -1,0 +1,322 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's golden vectors and
+the CPU oracle on identical inputs.
+
+Bars (stated here):
+* neighbour sets, per-pixel neighbour counts, bin (chunk) membership: BIT-EXACT;
+* pixel values (fp32 accumulation vs the fp64 reference):
+    |g - r| <= 2e-5 * max|r|   everywhere, and
+    |g - r| <= 1e-4 * |r|      where |r| >= 1e-3 * max|r|;
+  pixels where the reference is exactly 0 are exactly 0.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+ABS_TOL = 2e-5
+REL_TOL = 1e-4
+
+
+def assert_map_close(g, r, abs_tol=ABS_TOL, rel_tol=REL_TOL):
+    g = np.asarray(g, np.float64)
+    r = np.asarray(r, np.float64)
+    assert g.shape == r.shape
+    assert np.all(g[r == 0] == 0), "pixels that are 0 in the reference must be exactly 0"
+    m = np.max(np.abs(r)) if r.size else 0.0
+    if m == 0:
+        assert np.all(g == 0)
+        return
+    err = np.abs(g - r)
+    assert err.max() <= abs_tol * m, f"max abs err {err.max() / m:.3e} x max"
+    big = np.abs(r) >= 1e-3 * m
+    rel = err[big] / np.abs(r[big])
+    assert rel.max() <= rel_tol, f"max rel err {rel.max():.3e}"
+
+
+def g3():
+    g = golden("g3_plummer_1e4_256.npz")
+    return (g["pos"].astype(np.float64), g["h"].astype(np.float64), g["A"].astype(np.float64),
+            tuple(g["size"]), int(g["cs"]), tuple(g["ext"]), g["img"])
+
+
+# ------------------------------------------------------------------ golden vectors
+def test_g1_kernel_eval_on_device(gpu):
+    from asp_amd.tools.projections import quartic_spline_kernel
+    g = golden("g1_kernel_table.npz")
+    w = quartic_spline_kernel(g["r"], g["h"])
+    assert np.array_equal(w == 0, g["w"] == 0)
+    np.testing.assert_allclose(w, g["w"], rtol=4e-16 * 8, atol=0)
+    with pytest.raises(ValueError):
+        quartic_spline_kernel(g["r"].astype(np.float32), g["h"])
+
+
+@pytest.mark.parametrize("case", list(range(11)))
+def test_g2_hand_cases(gpu, case):
+    from asp_amd.tools.projections import create_image
+    g = golden("g2_hand_cases.npz")
+    c = {k: g[f"c{case}_{k}"] for k in ("pos", "h", "A", "size", "cs", "axis", "ext", "img")}
+    img = create_image(c["pos"].reshape(-1, 3), c["h"], c["A"], tuple(c["size"]), int(c["cs"]),
+                       int(c["axis"]), *c["ext"])
+    assert img.dtype == np.float64 and img.shape == c["img"].shape
+    assert_map_close(img, c["img"])
+    assert np.array_equal(img != 0, c["img"] != 0)
+
+
+def test_g3_plummer_cubic(gpu):
+    from asp_amd import CoordinateAxes
+    from asp_amd.tools.projections import create_image
+    pos, h, A, size, cs, ext, ref = g3()
+    img = create_image(pos, h, A, size, cs, CoordinateAxes.Z, *ext)
+    assert_map_close(img, ref)
+
+
+def test_g3_neighbour_counts_bitexact(gpu, oracle):
+    """Indicator kernel: per-pixel neighbour counts and index checksums, bit-exact."""
+    from asp_amd.tools.projections import create_image, indicator_kernel
+    pos, h, A, size, cs, ext, ref = g3()
+    ones = np.ones_like(h)
+    cnt = create_image(pos, h, ones, size, cs, 2, *ext, kernel_func=indicator_kernel)
+    want = oracle.create_image(pos, h, ones, size, cs, 2, *ext, kernel="indicator")
+    assert np.array_equal(cnt, want)
+    assert np.array_equal(cnt != 0, ref != 0)
+    ids = (np.arange(h.size) % 4096).astype(np.float64)
+    chk = create_image(pos, h, ids, size, cs, 2, *ext, kernel_func=indicator_kernel)
+    want = oracle.create_image(pos, h, ids, size, cs, 2, *ext, kernel="indicator")
+    assert np.array_equal(chk, want)
+
+
+def test_g4_chunk_membership_bitexact(gpu):
+    import ctypes as C
+    from asp_amd import _lib
+    pos, h, A, size, cs, ext, _ = g3()
+    g = golden("g4_tile_membership.npz")
+    u, v, hh = (np.ascontiguousarray(a, np.float32) for a in (pos[:, 0], pos[:, 1], h))
+    out = [np.empty(u.size, np.int32) for _ in range(4)]
+    _lib.check(_lib.lib().asp_chunk_ranges(_lib.ptr(u), _lib.ptr(v), _lib.ptr(hh), u.size,
+                                           *map(float, ext), size[0], size[1], cs,
+                                           *[_lib.ptr(o, _lib._i32) for o in out], 0, 0, None))
+    cx0, cx1, cy0, cy1 = out
+    ncx, ncy = g["n_chunks"]
+    offs = g["offsets"]
+    for cx in range(ncx):
+        for cy in range(ncy):
+            k = cx * ncy + cy
+            got = np.nonzero((cx0 <= cx) & (cx <= cx1) & (cy0 <= cy) & (cy <= cy1))[0]
+            assert np.array_equal(got, g["index"][offs[k]:offs[k + 1]]), (cx, cy)
+    del C
+
+
+def gpu_neighbours(u, v, h, ext, size, cs, pixels):
+    from asp_amd import _lib
+    u, v, h = (np.ascontiguousarray(a, np.float32) for a in (u, v, h))
+    pix = np.ascontiguousarray(pixels, np.int64)
+    offs = np.zeros(pix.size + 1, np.int64)
+    tot = np.zeros(1, np.int64)
+    cap = max(1, 64 * u.size)
+    idx = np.empty(cap, np.int32)
+    _lib.check(_lib.lib().asp_pixel_neighbours(
+        _lib.ptr(u), _lib.ptr(v), _lib.ptr(h), u.size, *map(float, ext), size[0], size[1], cs,
+        _lib.ptr(pix, _lib._i64), pix.size, _lib.ptr(offs, _lib._i64), _lib.ptr(idx, _lib._i32),
+        cap, _lib.ptr(tot, _lib._i64), 0))
+    assert tot[0] <= cap
+    return offs, idx[:tot[0]]
+
+
+def test_g5_neighbour_sets_bitexact(gpu):
+    pos, h, A, size, cs, ext, _ = g3()
+    g = golden("g5_neighbours.npz")
+    offs, idx = gpu_neighbours(pos[:, 0], pos[:, 1], h, ext, size, cs, g["pixels"])
+    assert np.array_equal(offs, g["offsets"]) and np.array_equal(idx, g["index"])
+
+
+def test_g6_wendland(gpu):
+    from asp_amd.tools.projections import create_image, wendland_c2_kernel
+    pos, h, A, size, cs, ext, _ = g3()
+    ref = golden("g6_wendland_c2.npz")["img"]
+    img = create_image(pos, h, A, size, cs, 2, *ext, kernel_func=wendland_c2_kernel)
+    assert_map_close(img, ref)
+
+
+def test_g7_axes_permutation_nonsquare(gpu):
+    from asp_amd import CoordinateAxes
+    from asp_amd.tools.projections import create_image
+    g = golden("g7_axes_permuted.npz")
+    pos, h, A = (g[k].astype(np.float64) for k in ("pos", "h", "A"))
+    ext = tuple(g["ext"])
+    for ax in CoordinateAxes:
+        assert_map_close(create_image(pos, h, A, (64, 64), 8, ax, *ext), g[f"img_{ax.value}"])
+    p = g["perm"]
+    assert_map_close(create_image(pos[p], h[p], A[p], (64, 64), 8, "z", *ext), g["img_z_perm"])
+    assert_map_close(create_image(pos, h, A, (48, 64), 16, 2, *ext), g["img_ns_48x64_c16"])
+    assert_map_close(create_image(pos, h, A, (64, 40), 7, 2, *ext), g["img_ns_64x40_c7"])
+
+
+# ------------------------------------------------------------------ oracle, wider cases
+def plummer_f32(n, seed, h_law="physical", grid=None, extent=4.0):
+    from asp_amd.plummer import plummer
+    p = plummer(n, seed=seed, h_law=h_law, grid=grid, extent=extent)
+    return {k: np.asarray(v, np.float32).astype(np.float64) for k, v in p.items()}
+
+
+@pytest.mark.parametrize("n,G,h_law,kernel", [(200_000, 512, "physical", "cubic"),
+                                              (300_000, 1024, "pixel", "wendland_c2"),
+                                              (50_000, 300, "physical", "wendland_c2")])
+def test_plummer_vs_oracle(gpu, oracle, n, G, h_law, kernel):
+    from asp_amd.tools.projections import (create_image, indicator_kernel,
+                                           quartic_spline_kernel, wendland_c2_kernel)
+    p = plummer_f32(n, seed=n, h_law=h_law, grid=G)
+    ext = (-4.0, 4.0, -4.0, 4.0)
+    kf = {"cubic": quartic_spline_kernel, "wendland_c2": wendland_c2_kernel}[kernel]
+    img = create_image(p["pos"], p["h"], p["m"], (G, G), 64, 2, *ext, kernel_func=kf)
+    ref, _ = oracle.project_scatter(p["pos"][:, 0], p["pos"][:, 1], p["h"], p["m"], None, (G, G),
+                                    64, *ext, kernel=kernel)
+    assert_map_close(img, ref)
+    cnt = create_image(p["pos"], p["h"], np.ones(n), (G, G), 64, 2, *ext,
+                       kernel_func=indicator_kernel)
+    want, _ = oracle.project_scatter(p["pos"][:, 0], p["pos"][:, 1], p["h"], np.ones(n), None,
+                                     (G, G), 64, *ext, kernel="indicator")
+    assert np.array_equal(cnt, want)
+
+
+def test_boundary_pairs_exact(gpu, oracle):
+    """Particles placed at (and 1-4 ulp around) distance exactly 2h from pixel corners:
+    the fp32 test alone would misjudge some of these; the fp64 band path must not."""
+    from asp_amd.tools.projections import create_image, indicator_kernel
+    rng = np.random.default_rng(3)
+    G = 64
+    ext = (-1.0, 1.0, -1.0, 1.0)
+    ps = 2.0 / G
+    n = 20000
+    xi = rng.integers(4, G - 4, n)
+    yi = rng.integers(4, G - 4, n)
+    h = np.float32(ps) * rng.choice([0.5, 0.75, 1.0, 1.25, 1.5], n).astype(np.float32)
+    ang = rng.uniform(0, 2 * np.pi, n)
+    X = -1.0 + xi * ps
+    Y = -1.0 + yi * ps
+    u = (X + 2.0 * h * np.cos(ang)).astype(np.float32)
+    v = (Y + 2.0 * h * np.sin(ang)).astype(np.float32)
+    k = rng.integers(-4, 5, n).astype(np.float32)
+    u = (u + k * np.spacing(u)).astype(np.float32)
+    axis_aligned = rng.random(n) < 0.3  # exact 2h offsets along one axis
+    u[axis_aligned] = (X[axis_aligned] + 2.0 * h[axis_aligned]).astype(np.float32)
+    v[axis_aligned] = Y[axis_aligned].astype(np.float32)
+    pos = np.stack([u, v, np.zeros(n, np.float32)], 1).astype(np.float64)
+    h64 = h.astype(np.float64)
+    ones = np.ones(n)
+    cnt = create_image(pos, h64, ones, (G, G), 8, 2, *ext, kernel_func=indicator_kernel)
+    want = oracle.create_image(pos, h64, ones, (G, G), 8, 2, *ext, kernel="indicator")
+    assert np.array_equal(cnt, want)
+    ids = (np.arange(n) % 4096).astype(np.float64)
+    chk = create_image(pos, h64, ids, (G, G), 8, 2, *ext, kernel_func=indicator_kernel)
+    want = oracle.create_image(pos, h64, ids, (G, G), 8, 2, *ext, kernel="indicator")
+    assert np.array_equal(chk, want)
+
+
+def test_weighted_map(gpu, oracle):
+    from asp_amd.tools.projections import create_weighted_image, wendland_c2_kernel
+    p = plummer_f32(100_000, seed=9, h_law="pixel", grid=512)
+    ext = (-4.0, 4.0, -4.0, 4.0)
+    T = p["T"]
+    r, s0, s1 = create_weighted_image(p["pos"], p["h"], p["m"], T, (512, 512), 64, 2, *ext,
+                                      kernel_func=wendland_c2_kernel, return_components=True)
+    a0 = (p["m"] * T).astype(np.float32).astype(np.float64)  # what the wrapper feeds
+    o0, o1 = oracle.project_scatter(p["pos"][:, 0], p["pos"][:, 1], p["h"], a0, p["m"],
+                                    (512, 512), 64, *ext, kernel="wendland_c2")
+    assert_map_close(s0, o0)
+    assert_map_close(s1, o1)
+    ratio = create_weighted_image(p["pos"], p["h"], p["m"], T, (512, 512), 64, 2, *ext,
+                                  kernel_func=wendland_c2_kernel)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        want = np.where(o1 != 0, o0 / o1, 0.0)
+    np.testing.assert_array_equal(ratio == 0, want == 0)
+    np.testing.assert_allclose(ratio, want, rtol=2e-4, atol=0)
+
+
+def test_wide_particles(gpu, oracle):
+    """Huge smoothing lengths (wide path, > 64 GPU tiles) mixed with small ones."""
+    from asp_amd.tools.projections import create_image, indicator_kernel
+    rng = np.random.default_rng(5)
+    n = 3000
+    pos = np.asarray(rng.uniform(-1, 1, (n, 3)), np.float32).astype(np.float64)
+    h = np.asarray(rng.uniform(0.005, 0.02, n), np.float32).astype(np.float64)
+    h[:40] = np.asarray(rng.uniform(0.3, 2.0, 40), np.float32)
+    A = np.asarray(rng.uniform(0.5, 1.5, n), np.float32).astype(np.float64)
+    G = 1024
+    ext = (-1.0, 1.0, -1.0, 1.0)
+    img = create_image(pos, h, A, (G, G), 32, 2, *ext)
+    ref, _ = oracle.project_scatter(pos[:, 0], pos[:, 1], h, A, None, (G, G), 32, *ext)
+    assert_map_close(img, ref)
+    cnt = create_image(pos, h, np.ones(n), (G, G), 32, 2, *ext, kernel_func=indicator_kernel)
+    want, _ = oracle.project_scatter(pos[:, 0], pos[:, 1], h, np.ones(n), None, (G, G), 32,
+                                     *ext, kernel="indicator")
+    assert np.array_equal(cnt, want)
+    from asp_amd.device import stats
+    assert stats(0)["wide"] > 0
+
+
+def test_split_tile_items(gpu, oracle):
+    """A dense clump puts > 1 work item on one tile (atomic tile merge path)."""
+    from asp_amd.tools.projections import create_image
+    rng = np.random.default_rng(8)
+    n = 40_000
+    pos = np.asarray(rng.normal(0, 0.01, (n, 3)), np.float32).astype(np.float64)
+    h = np.full(n, 0.004)
+    A = np.asarray(rng.uniform(0.5, 1.5, n), np.float32).astype(np.float64)
+    G = 512
+    ext = (-1.0, 1.0, -1.0, 1.0)
+    img = create_image(pos, h, A, (G, G), 64, 2, *ext)
+    from asp_amd.device import stats
+    s = stats(0)
+    assert s["items"] > s["tiles"] // 64  # some tile was split
+    ref, _ = oracle.project_scatter(pos[:, 0], pos[:, 1], h, A, None, (G, G), 64, *ext)
+    assert_map_close(img, ref)
+
+
+def test_edge_cases(gpu):
+    from asp_amd.tools.projections import create_image
+    z = create_image(np.zeros((0, 3)), np.zeros(0), np.zeros(0), (8, 8), 4, 2, -1, 1, -1, 1)
+    assert z.shape == (8, 8) and not z.any()
+    img = create_image([[0.0, 0, 0], [np.nan, 0, 0], [0.2, 0.2, 0]], [0.0, 0.3, 0.3],
+                       [1.0, 1.0, 1.0], (8, 8), 4, 2, -1, 1, -1, 1)
+    only = create_image([[0.2, 0.2, 0]], [0.3], [1.0], (8, 8), 4, 2, -1, 1, -1, 1)
+    assert np.array_equal(img, only)  # h = 0 and NaN particles contribute nothing
+    assert create_image([[0, 0, 0]], [0.5], [1.0], (4, 4), -3, 2, -1, 1, -1, 1).sum() == 0
+    with pytest.raises(ValueError):
+        create_image([[0, 0, 0]], [0.5], [1.0], (4, 4), 0, 2, -1, 1, -1, 1)
+    with pytest.raises(TypeError):
+        create_image([[0, 0, 0]], [0.5], [1.0], (4, 4), 4, 2, -1, 1, -1, 1,
+                     kernel_func=lambda r, h: r)
+    with pytest.raises(ValueError):
+        create_image([[0, 0, 0]], [0.5], [1.0], (4, 4), 4, 2, 1, -1, -1, 1)
+
+
+def test_device_api_ratio_accumulate(gpu, oracle):
+    import torch
+    from asp_amd.device import project2d
+    p = plummer_f32(50_000, seed=4, h_law="pixel", grid=256)
+    t = {k: torch.tensor(p[k], dtype=torch.float32, device="cuda") for k in ("h", "m", "T")}
+    u = torch.tensor(p["pos"][:, 0], dtype=torch.float32, device="cuda")
+    v = torch.tensor(p["pos"][:, 1], dtype=torch.float32, device="cuda")
+    ext = (-4.0, 4.0, -4.0, 4.0)
+    a0 = t["m"] * t["T"]
+    o0, o1 = project2d(u, v, t["h"], a0, t["m"], image_size=(256, 256), extent=ext,
+                       kernel="wendland_c2")
+    # accumulate: project the two halves into the same maps
+    half = u.shape[0] // 2
+    s0 = torch.zeros_like(o0)
+    s1 = torch.zeros_like(o1)
+    for sl in (slice(0, half), slice(half, None)):
+        project2d(u[sl].contiguous(), v[sl].contiguous(), t["h"][sl].contiguous(),
+                  a0[sl].contiguous(), t["m"][sl].contiguous(), image_size=(256, 256),
+                  extent=ext, kernel="wendland_c2", accumulate=True, out0=s0, out1=s1)
+    torch.cuda.synchronize()
+    assert_map_close(s0.cpu().numpy(), o0.cpu().numpy().astype(np.float64), abs_tol=1e-6,
+                     rel_tol=1e-5)
+    r, _ = project2d(u, v, t["h"], a0, t["m"], image_size=(256, 256), extent=ext,
+                     kernel="wendland_c2", ratio=True)
+    o0n, o1n = o0.cpu().numpy().astype(np.float64), o1.cpu().numpy().astype(np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        want = np.where(o1n != 0, o0n / o1n, 0.0)
+    np.testing.assert_allclose(r.cpu().numpy(), want, rtol=1e-6)

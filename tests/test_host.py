@@ -1,0 +1,128 @@
+"""CPU-side tests: the C-ABI library loads and exports every declared symbol, the host
+mirror of the reference interface behaves like the reference, synthetic inputs follow
+their laws.  No GPU compute here."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+
+def test_header_symbols_exported(asp):
+    """Every function include/asp.h declares is exported by libasp_hip.so."""
+    from asp_amd import _lib
+    hdr = open(os.path.join(REPO, "include", "asp.h")).read()
+    declared = set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(asp_\w+)\s*\(", hdr, re.M))
+    assert declared == set(_lib.EXPORTS)
+    L = _lib.lib()
+    for name in declared:
+        assert hasattr(L, name), name
+    assert L.asp_version() // 10000 == 1
+
+
+def test_no_device_is_loud(asp):
+    """On a host without a GPU the product path raises; there is no CPU fallback."""
+    from asp_amd import _lib
+    from asp_amd.tools.projections import create_image
+    if _lib.lib().asp_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        create_image([[0, 0, 0]], [0.5], [1.0], (4, 4), 4, 2, -1, 1, -1, 1)
+
+
+def test_c_abi_argument_validation(asp):
+    """Argument errors are reported as ASP_ERR_INVALID before any device work."""
+    from asp_amd import _lib
+    L = _lib.lib()
+    z = np.zeros(1, np.float32)
+    o = np.zeros(16, np.float32)
+    P = _lib.ptr
+    # x_max < x_min
+    rc = L.asp_project2d(P(z), P(z), P(z), P(z), None, 1, 1.0, -1.0, -1.0, 1.0, 4, 4, 4, 0, 0,
+                         P(o), None, 0, None)
+    assert rc == _lib.ASP_ERR_INVALID and b"grid" in L.asp_last_error()
+    rc = L.asp_project2d(P(z), P(z), P(z), P(z), None, 1, -1.0, 1.0, -1.0, 1.0, 4, 4, 4, 7, 0,
+                         P(o), None, 0, None)
+    assert rc == _lib.ASP_ERR_INVALID
+    rc = L.asp_project2d(P(z), P(z), P(z), P(z), P(z), 1, -1.0, 1.0, -1.0, 1.0, 4, 4, 4, 0, 0,
+                         P(o), None, 0, None)
+    assert rc == _lib.ASP_ERR_INVALID  # a1 without out1
+    with pytest.raises(ValueError):
+        _lib.check(rc)
+
+
+def test_axis_resolution(asp):
+    from asp_amd import CoordinateAxes
+    from asp_amd._axes import axis_index
+    assert [axis_index(a) for a in CoordinateAxes] == [0, 1, 2]
+    assert axis_index("x") == 0 and axis_index("Y") == 1 and axis_index("z") == 2
+    assert axis_index(b"x") == 0 and axis_index(7) == 2  # anything else is Z, as in the ref
+    assert str(CoordinateAxes.X) == "x" and CoordinateAxes.from_string(" Z ") == CoordinateAxes.Z
+    with pytest.raises(ValueError):
+        CoordinateAxes.from_string("w")
+
+    class RefAxes:  # the reference's enum: only .name matters
+        name = "Y"
+    assert axis_index(RefAxes()) == 1
+
+
+def test_kernel_plugin_resolution(asp):
+    from asp_amd.tools.projections import (indicator_kernel, quartic_spline_kernel,
+                                           wendland_c2_kernel)
+    from asp_amd.tools.projections._kernels import kernel_id_of
+    assert kernel_id_of(quartic_spline_kernel) == 0
+    assert kernel_id_of(wendland_c2_kernel) == 1
+    assert kernel_id_of(indicator_kernel) == 2
+
+    def quartic_spline_kernel_ref(r, h):
+        return r
+    quartic_spline_kernel_ref.__name__ = "quartic_spline_kernel"  # the reference's object
+    assert kernel_id_of(quartic_spline_kernel_ref) == 0
+    with pytest.raises(TypeError):
+        kernel_id_of(lambda r, h: r)
+    with pytest.raises(ValueError, match="dtype"):
+        quartic_spline_kernel(np.zeros(3, np.float32), np.ones(3))
+    assert quartic_spline_kernel(np.zeros(0), np.zeros(0)).shape == (0,)
+
+
+def test_create_image_argument_errors(asp):
+    from asp_amd.tools.projections import create_image
+    with pytest.raises(ValueError):
+        create_image(np.zeros((3, 2)), np.ones(3), np.ones(3), (4, 4), 4, 2, -1, 1, -1, 1)
+    with pytest.raises(ValueError):
+        create_image(np.zeros((3, 3)), np.ones(2), np.ones(3), (4, 4), 4, 2, -1, 1, -1, 1)
+    with pytest.raises(ValueError, match="zero"):
+        create_image(np.zeros((3, 3)), np.ones(3), np.ones(3), (4, 4), 0, 2, -1, 1, -1, 1)
+    with pytest.raises(TypeError):
+        create_image(np.zeros((3, 3)), np.ones(3), np.ones(3), (4, 4), 2.5, 2, -1, 1, -1, 1)
+    # negative chunk size: range(0, N, -k) is empty in the reference -> zero image, no GPU
+    img = create_image(np.zeros((3, 3)), np.ones(3), np.ones(3), (4, 5), -2, 2, -1, 1, -1, 1)
+    assert img.shape == (4, 5) and img.dtype == np.float64 and not img.any()
+
+
+def test_plummer_laws():
+    from asp_amd.plummer import plummer
+    p = plummer(20000, seed=0, h_law="physical")
+    r = np.linalg.norm(p["pos"], axis=1)
+    assert np.allclose(r, p["r"])
+    # Plummer enclosed-mass fraction M(<r) = r^3 / (1 + r^2)^1.5 (u capped at 0.999)
+    for rr in (0.5, 1.0, 2.0):
+        frac = np.mean(r < rr)
+        assert abs(frac - rr ** 3 / (1 + rr * rr) ** 1.5) < 0.015
+    assert np.allclose(p["h"], 1.2 * np.cbrt(p["m"] / p["rho"]))
+    q = plummer(100, seed=0, h_law="pixel", grid=4096, extent=4.0)
+    assert np.all(q["h"] == 0.75 * 8.0 / 4096)
+    assert np.array_equal(plummer(50, seed=3)["pos"], plummer(50, seed=3)["pos"])
+
+
+def test_zslab_bounds_equal_count():
+    import torch
+    from asp_amd.distributed import zslab_bounds
+    z = torch.randn(200_000)
+    e = zslab_bounds(z, 4)
+    assert len(e) == 5 and e[0] == float("-inf") and e[-1] == float("inf")
+    counts = [int(((z >= e[r]) & (z < e[r + 1])).sum()) for r in range(4)]
+    assert sum(counts) == z.numel()
+    assert max(counts) - min(counts) < 0.02 * z.numel()
