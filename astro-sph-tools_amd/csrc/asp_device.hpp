@@ -11,6 +11,11 @@
 // rigorous per-record error band; pairs inside the band (~0.1 % near the 2h edge) are
 // re-decided by the reference's own fp64 arithmetic, including the chunk cull.  See
 // DESIGN.md §3 for the bound.
+//
+// Accumulation is fixed point: every term A*W is scaled by a per-tile power of two and
+// rounded to an int64 that is added with ds_add_u64 (LDS fp32 atomics run ~10x slower
+// than integer ones on gfx950: tools/microbench_lds.hip).  Integer sums are associative,
+// so maps are bitwise reproducible regardless of scheduling.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -18,16 +23,20 @@
 
 namespace asp {
 
-constexpr int kBlock = 256;     // threads per workgroup (4 waves)
-constexpr int kTile = 64;       // GPU tile edge in pixels (LDS accumulator 64x64 per map)
+constexpr int kBlock = 256;        // threads per workgroup for streaming kernels
+constexpr int kDepBlock = 512;     // deposit workgroup (8 waves; 2 per CU at 64 KiB LDS)
+constexpr int kTile = 64;          // GPU tile edge in pixels
 constexpr int kTileShift = 6;
-constexpr int kWideTiles = 64;  // particles overlapping more GPU tiles take the wide path
+constexpr int kWideTiles = 64;     // particles overlapping more GPU tiles take the wide path
+constexpr int kScaleBits = 61;     // per-tile bound n_t * max|c| maps to <= 2^61
 
 struct Grid {
     double x_min, y_min;
     double psx;       // (x_max - x_min) / nx                        _projector.py:34
     double psy_pix;   // (y_max - y_min) / nx  (S2 quirk)            .pyx:12
     double psy_cull;  // (y_max - y_min) / ny                        _projector.py:35
+    float xminf, yminf;   // fp32 copies for the candidate-box estimate
+    float ipsx, ipsy;     // fp32 reciprocal pitches (pixel pitches)
     float mg;         // bound on |corner coordinate| over the grid (error band)
     int nx, ny, cs;
     int ncx, ncy;     // reference chunks per axis
@@ -45,15 +54,22 @@ struct Prep {
     float thr;   // (2h)^2 in fp32
     float band;  // |r2_32 - thr_32| <= band  ->  decide in fp64
     float hinv;  // 1/h
-    float c0, c1;  // a0 * norm(h), a1 * norm(h)
+    float s0, s1;  // a * norm(h) * 2^k_tile: fixed-point term = s * shape(q)
     Box b;
 };
 
 struct Item {       // one deposit work item: a run of records of one GPU tile
     long long start;
     int tile;
-    int count;
-    int multi;      // tile split over several items -> accumulate with atomics
+    int count;      // 0: empty tile (write zeros)
+    int slab;       // -1: the tile's only item (writes the map); >= 0: int64 partial slab
+    int pad;
+};
+
+struct Merge {      // a tile split over several items: sum their slabs
+    int tile;
+    int slab0;
+    int nslab;
     int pad;
 };
 
@@ -103,21 +119,26 @@ __device__ __forceinline__ void chunk_range(double w, double h, double w_min, do
     c_hi = cmax;
 }
 
-// Candidate pixel box of a particle: every pixel that can pass the exact test lies in
-// it (margin 1e-6 px >> fp64 rounding of the estimate).  False when nothing can pass.
+// Candidate pixel box of a particle: a superset of the pixels that can pass the exact
+// test.  fp32 estimate of (w - 2|h| - w_min) / pitch with a margin delta that bounds its
+// rounding error (~10x over: 2^-19 relative to the operand magnitudes, plus 2^-12 px so
+// that a corner at exactly 2h stays a candidate).  False when nothing can pass.
 __device__ __forceinline__ bool footprint(const Grid& g, float u, float v, float h, Box& b) {
-    if (!__builtin_isfinite(u) || !__builtin_isfinite(v) || !__builtin_isfinite(h)) return false;
-    double hd = fabs(2.0 * (double)h);
-    if (!(hd > 0.0)) return false;  // h == 0: r2 < 0 never holds (S12)
-    double ud = u, vd = v;
-    double fx0 = ceil((ud - hd - g.x_min) / g.psx - 1e-6);
-    double fx1 = floor((ud + hd - g.x_min) / g.psx + 1e-6);
-    double fy0 = ceil((vd - hd - g.y_min) / g.psy_pix - 1e-6);
-    double fy1 = floor((vd + hd - g.y_min) / g.psy_pix + 1e-6);
-    fx0 = fmax(fx0, 0.0);
-    fy0 = fmax(fy0, 0.0);
-    fx1 = fmin(fx1, (double)(g.nx - 1));
-    fy1 = fmin(fy1, (double)(g.ny - 1));
+    float hd = fabsf(2.0f * h);
+    if (!(hd > 0.0f) || !__builtin_isfinite(hd)) {
+        // h == 0: r2 < 0 never holds (S12).  Non-finite: excluded.
+        // |2h| overflowing fp32 only happens for non-finite h (|h| < 1.7e38).
+        return false;
+    }
+    if (!__builtin_isfinite(u) || !__builtin_isfinite(v)) return false;
+    float cx = (u - g.xminf) * g.ipsx, rx = hd * g.ipsx;
+    float cy = (v - g.yminf) * g.ipsy, ry = hd * g.ipsy;
+    float dx = (fabsf(u) + fabsf(g.xminf) + hd) * g.ipsx * 0x1p-19f + 0x1p-12f;
+    float dy = (fabsf(v) + fabsf(g.yminf) + hd) * g.ipsy * 0x1p-19f + 0x1p-12f;
+    float fx0 = fmaxf(ceilf(cx - rx - dx), 0.0f);
+    float fx1 = fminf(floorf(cx + rx + dx), (float)(g.nx - 1));
+    float fy0 = fmaxf(ceilf(cy - ry - dy), 0.0f);
+    float fy1 = fminf(floorf(cy + ry + dy), (float)(g.ny - 1));
     if (!(fx0 <= fx1) || !(fy0 <= fy1)) return false;
     b.x0 = (int)fx0;
     b.x1 = (int)fx1;
@@ -125,7 +146,7 @@ __device__ __forceinline__ bool footprint(const Grid& g, float u, float v, float
     b.y1 = (int)fy1;
     if (g.nonsquare) {  // S2: the y cull pitch differs from the pixel pitch
         int c0, c1;
-        chunk_range(vd, (double)h, g.y_min, g.psy_cull, g.ny, g.cs, c0, c1);
+        chunk_range((double)v, (double)h, g.y_min, g.psy_cull, g.ny, g.cs, c0, c1);
         b.y0 = max(b.y0, c0 * g.cs);
         b.y1 = min(b.y1, min((c1 + 1) * g.cs, g.ny) - 1);
         if (b.y0 > b.y1) return false;
@@ -133,14 +154,24 @@ __device__ __forceinline__ bool footprint(const Grid& g, float u, float v, float
     return true;
 }
 
+// Kernel normalisation K / h^3 (fp64 for exponent range).
 template <int KID>
-__device__ __forceinline__ double kernel_norm64(double h) {
-    if constexpr (KID == 0) return 1.0 / (M_PI * (h * h * h));          // _kernels.pyx:16,18
-    else if constexpr (KID == 1) return 21.0 / (16.0 * M_PI * (h * h * h));
+__device__ __forceinline__ double kernel_norm64(float h) {
+    double hd = (double)h;
+    double h3 = hd * hd * hd;
+    if constexpr (KID == 0) return (1.0 / M_PI) / h3;                    // _kernels.pyx:16,18
+    else if constexpr (KID == 1) return (21.0 / (16.0 * M_PI)) / h3;
     else return 1.0;
 }
 
-// Kernel shape f(q), W = norm(h) * f(q).
+// Per-record term coefficient c = a * norm(h).  The SAME function feeds the per-tile
+// bound (scatter) and the terms (deposit), so |c| <= max|c| holds bit-for-bit.
+template <int KID>
+__device__ __forceinline__ double term_coef(float a, float h) {
+    return (double)a * kernel_norm64<KID>(h);
+}
+
+// Kernel shape f(q), W = norm(h) * f(q); max f = f(0) = 1 for all three kernels.
 template <int KID>
 __device__ __forceinline__ float kernel_shape(float q) {
     if constexpr (KID == 0) {  // M4 cubic spline (_kernels.pyx:14-19)
@@ -160,7 +191,7 @@ __device__ __forceinline__ float kernel_shape(float q) {
 
 template <int KID>
 __device__ __forceinline__ bool prep_record(const Grid& g, float u, float v, float h, float a0,
-                                            float a1, Prep& P) {
+                                            float a1, int k0, int k1, Prep& P) {
     if (!footprint(g, u, v, h, P.b)) return false;
     P.u = u;
     P.v = v;
@@ -173,9 +204,8 @@ __device__ __forceinline__ bool prep_record(const Grid& g, float u, float v, flo
     // Negative h narrows the chunk cull below the disc: decide every pair in fp64.
     P.band = (h < 0.0f || !__builtin_isfinite(band)) ? __builtin_inff() : band;
     P.hinv = 1.0f / h;
-    double nrm = kernel_norm64<KID>((double)h);
-    P.c0 = (float)((double)a0 * nrm);
-    P.c1 = (float)((double)a1 * nrm);
+    P.s0 = (float)ldexp(term_coef<KID>(a0, h), k0);
+    P.s1 = (float)ldexp(term_coef<KID>(a1, h), k1);
     return true;
 }
 
@@ -200,6 +230,19 @@ __device__ __forceinline__ bool decide(const Grid& g, const Prep& P, int xi, int
     bool in = r2 < P.thr;
     if (fabsf(r2 - P.thr) <= P.band) in = exact_pair(g, P.u, P.v, P.h, xi, yi);
     return in;
+}
+
+// Round a scaled term (|f| < 2^62) to int64, toward zero: for a = |f|, hi = floor(a/2^32)
+// and lo = a - hi*2^32 in [0, 2^32) are both exact in fp32 (lo is a multiple of ulp(a)
+// below 2^32, so it needs <= 23 significant bits); the sign is applied in two's
+// complement.  A pure function of f, so the fixed-point sums are reproducible.
+__device__ __forceinline__ unsigned long long f2fix(float f) {
+    float a = fabsf(f);
+    float hi = floorf(a * 0x1p-32f);
+    float lo = fmaf(-hi, 0x1p32f, a);
+    unsigned long long m =
+        ((unsigned long long)(unsigned int)hi << 32) | (unsigned long long)(unsigned int)lo;
+    return f < 0.0f ? 0ull - m : m;
 }
 
 __device__ __forceinline__ float bcast(float x, int lane) {

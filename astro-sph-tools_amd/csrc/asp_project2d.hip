@@ -8,15 +8,19 @@
 //   K1 count     one streaming pass over (u, v, h): per-workgroup LDS histogram of
 //                (particle, GPU tile) insertions -> hist[block][tile]
 //   K2a colscan  per tile, exclusive prefix over blocks (in place) + tile totals
-//   K2b tilescan one workgroup: tile start offsets in Morton order of the tiles, and
-//                the deposit work list (runs of <= CH records of one tile)
+//   K2b tilescan one workgroup: tile start offsets in Morton order of the tiles, the
+//                deposit work list (runs of <= CH records of one tile; empty tiles get
+//                a zero item) and the merge list of tiles split over several items
 //   K3 scatter   second streaming pass: each insertion written as a 16/32-byte record
-//                into its tile's run (LDS cursors; coalesced record stores)
-//   K4 deposit   one workgroup per work item: records -> LDS tile accumulators
-//                (ds_add_f32), small footprints lane-per-record, large ones swept by
-//                a whole wave; tile written once (plain store or float atomics)
-//   K5 wide      particles overlapping > kWideTiles tiles, per tile, wave sweeps
-//   K6 ratio     optional out0 / out1 (mass-weighted maps)
+//                into its tile's run (LDS cursors) + per-(block, tile) max|A W_norm|
+//   K3b scale    per tile: max over blocks -> power-of-two fixed-point scale
+//   K4 deposit   one workgroup per work item: records -> int64 LDS tile accumulators
+//                (ds_add_u64), small footprints lane-per-record, large ones swept by a
+//                whole wave; the tile is converted and written once, or (split tiles)
+//                stored as an int64 partial slab
+//   K5 merge     split tiles: exact int64 sum of their slabs, convert, write
+//   K6 wide      particles overlapping > kWideTiles tiles, per tile, wave sweeps
+//   K7 ratio     out0 / out1 (mass-weighted maps) when not fused into K4/K5
 //
 // No MFMA: this is gather/scatter work; the bounds are HBM bytes and VALU/LDS-atomic
 // issue.
@@ -36,37 +40,66 @@
 
 namespace asp {
 
+// Counter words (int) shared by the pipeline stages.
+enum Ctr {
+    cItems = 0,     // work items (K2b)
+    cRecs = 1,      // records (K2b)
+    cWideCount = 2, // wide particles (K1)
+    cChunk = 3,     // records per item (K2b)
+    cWideCursor = 4,// wide list fill (K3)
+    cSlabs = 5,     // int64 partial slabs (K2b)
+    cMerges = 6,    // split tiles (K2b)
+    cWideMax0 = 7,  // max |c0| over wide particles, fp32 bits (K3)
+    cWideMax1 = 8,  // max |c1| over wide particles, fp32 bits (K3)
+    cNum = 16
+};
+
+constexpr int kCountBlock = 512;  // count / scatter workgroup
+constexpr int kUnroll = 2;        // particles in flight per thread in count / scatter
+
 // ----------------------------------------------------------------------------------
 // K1: count insertions per (block, tile)
 // ----------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_count(const float* __restrict__ u,
-                                                  const float* __restrict__ v,
-                                                  const float* __restrict__ h, long long n,
-                                                  long long per_block, Grid g,
-                                                  int* __restrict__ hist,
-                                                  int* __restrict__ wide_count) {
+__global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__ u,
+                                                       const float* __restrict__ v,
+                                                       const float* __restrict__ h,
+                                                       long long n, long long per_block, Grid g,
+                                                       int* __restrict__ hist,
+                                                       int* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) int lh[];
-    for (int t = threadIdx.x; t < g.ntiles; t += kBlock) lh[t] = 0;
+    for (int t = threadIdx.x; t < g.ntiles; t += kCountBlock) lh[t] = 0;
     __syncthreads();
     long long p0 = (long long)blockIdx.x * per_block;
     long long p1 = min(n, p0 + per_block);
     int nwide = 0;
-    for (long long p = p0 + threadIdx.x; p < p1; p += kBlock) {
-        Box b;
-        if (!footprint(g, u[p], v[p], h[p], b)) continue;
-        int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
-        int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
-        if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > kWideTiles) {
-            ++nwide;
-            continue;
+    for (long long base = p0; base < p1; base += (long long)kCountBlock * kUnroll) {
+        float pu[kUnroll], pv[kUnroll], ph[kUnroll];
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k) {
+            long long p = base + threadIdx.x + (long long)k * kCountBlock;
+            bool in = p < p1;
+            pu[k] = in ? u[p] : 0.0f;
+            pv[k] = in ? v[p] : 0.0f;
+            ph[k] = in ? h[p] : 0.0f;  // h = 0: no footprint
         }
-        for (int tx = tx0; tx <= tx1; ++tx)
-            for (int ty = ty0; ty <= ty1; ++ty) atomicAdd(&lh[tx * g.nty + ty], 1);
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k) {
+            Box b;
+            if (!footprint(g, pu[k], pv[k], ph[k], b)) continue;
+            int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
+            int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
+            if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > kWideTiles) {
+                ++nwide;
+                continue;
+            }
+            for (int tx = tx0; tx <= tx1; ++tx)
+                for (int ty = ty0; ty <= ty1; ++ty) atomicAdd(&lh[tx * g.nty + ty], 1);
+        }
     }
-    if (nwide) atomicAdd(wide_count, nwide);
+    if (nwide) atomicAdd(&ctr[cWideCount], nwide);
     __syncthreads();
     int* row = hist + (long long)blockIdx.x * g.ntiles;
-    for (int t = threadIdx.x; t < g.ntiles; t += kBlock) row[t] = lh[t];
+    for (int t = threadIdx.x; t < g.ntiles; t += kCountBlock) row[t] = lh[t];
 }
 
 // ----------------------------------------------------------------------------------
@@ -111,141 +144,233 @@ __global__ __launch_bounds__(kBlock) void k_colscan(int* __restrict__ hist, int 
 
 // ----------------------------------------------------------------------------------
 // K2b: single workgroup.  Tile start offsets in Morton order of the tiles (spatially
-// adjacent tiles' records are adjacent in HBM), and the deposit work list.
-// counters[0] = work items, counters[1] = total records (low 31 bits), counters[3] =
-// records per item.  Work items are also emitted in Morton order.
+// adjacent tiles' records are adjacent in HBM), the deposit work list (also Morton
+// order: every tile gets >= 1 item, empty tiles a zero item) and the merge list.
 // ----------------------------------------------------------------------------------
 constexpr int kScanThreads = 1024;
-constexpr int kTargetItems = 8192;
-constexpr int kMinItemRecords = 1024;
+constexpr int kTargetItems = 2048;
+constexpr int kMinItemRecords = 2048;
+
+__device__ __forceinline__ void block_scan_ll(long long* s, int tid) {
+    for (int o = 1; o < kScanThreads; o <<= 1) {
+        long long x = tid >= o ? s[tid - o] : 0;
+        __syncthreads();
+        s[tid] += x;
+        __syncthreads();
+    }
+}
 
 __global__ __launch_bounds__(kScanThreads) void k_tilescan(const int* __restrict__ tile_total,
                                                            const int* __restrict__ morton,
                                                            int ntiles,
                                                            long long* __restrict__ tile_start,
                                                            Item* __restrict__ items,
-                                                           int* __restrict__ counters) {
-    __shared__ long long sred[kScanThreads];
-    __shared__ int sitem[kScanThreads];
+                                                           Merge* __restrict__ merges,
+                                                           int* __restrict__ ctr) {
+    __shared__ long long s_rec[kScanThreads], s_item[kScanThreads], s_slab[kScanThreads],
+        s_merge[kScanThreads];
     int tid = threadIdx.x;
     int per = (ntiles + kScanThreads - 1) / kScanThreads;
     int r0 = min(ntiles, tid * per), r1 = min(ntiles, r0 + per);
     long long loc = 0;
     for (int r = r0; r < r1; ++r) loc += tile_total[morton[r]];
-    sred[tid] = loc;
+    s_rec[tid] = loc;
     __syncthreads();
-    // Hillis-Steele inclusive scan (1024 entries, once per call)
-    for (int o = 1; o < kScanThreads; o <<= 1) {
-        long long x = tid >= o ? sred[tid - o] : 0;
-        __syncthreads();
-        sred[tid] += x;
-        __syncthreads();
-    }
-    long long total = sred[kScanThreads - 1];
-    long long base = sred[tid] - loc;
+    block_scan_ll(s_rec, tid);
+    long long total = s_rec[kScanThreads - 1];
+    long long base = s_rec[tid] - loc;
     int ch = (int)max((long long)kMinItemRecords, (total + kTargetItems - 1) / kTargetItems);
-    int nloc = 0;
+    long long nit = 0, nsl = 0, nmg = 0;
     for (int r = r0; r < r1; ++r) {
         int t = morton[r];
         int c = tile_total[t];
         tile_start[t] = base;
         base += c;
-        nloc += (c + ch - 1) / ch;
+        int k = c > 0 ? (c + ch - 1) / ch : 1;
+        nit += k;
+        if (k > 1) {
+            nsl += k;
+            nmg += 1;
+        }
     }
-    sitem[tid] = nloc;
+    s_item[tid] = nit;
+    s_slab[tid] = nsl;
+    s_merge[tid] = nmg;
     __syncthreads();
-    for (int o = 1; o < kScanThreads; o <<= 1) {
-        int x = tid >= o ? sitem[tid - o] : 0;
-        __syncthreads();
-        sitem[tid] += x;
-        __syncthreads();
-    }
-    int ibase = sitem[tid] - nloc;
+    block_scan_ll(s_item, tid);
+    block_scan_ll(s_slab, tid);
+    block_scan_ll(s_merge, tid);
+    long long ib = s_item[tid] - nit, sb = s_slab[tid] - nsl, mb = s_merge[tid] - nmg;
     for (int r = r0; r < r1; ++r) {
         int t = morton[r];
         int c = tile_total[t];
-        int k = (c + ch - 1) / ch;
+        int k = c > 0 ? (c + ch - 1) / ch : 1;
         long long s0 = tile_start[t];
         for (int j = 0; j < k; ++j) {
             Item it;
             it.start = s0 + (long long)j * ch;
             it.tile = t;
-            it.count = min(ch, c - j * ch);
-            it.multi = k > 1;
+            it.count = c > 0 ? min(ch, c - j * ch) : 0;
+            it.slab = k > 1 ? (int)(sb + j) : -1;
             it.pad = 0;
-            items[ibase + j] = it;
+            items[ib + j] = it;
         }
-        ibase += k;
+        ib += k;
+        if (k > 1) {
+            Merge m;
+            m.tile = t;
+            m.slab0 = (int)sb;
+            m.nslab = k;
+            m.pad = 0;
+            merges[mb++] = m;
+            sb += k;
+        }
     }
     if (tid == kScanThreads - 1) {
-        counters[0] = sitem[kScanThreads - 1];
-        counters[1] = (int)min(total, (long long)0x7fffffff);
-        counters[3] = ch;
+        ctr[cItems] = (int)s_item[kScanThreads - 1];
+        ctr[cRecs] = (int)min(total, (long long)0x7fffffff);
+        ctr[cChunk] = ch;
+        ctr[cSlabs] = (int)s_slab[kScanThreads - 1];
+        ctr[cMerges] = (int)s_merge[kScanThreads - 1];
     }
 }
 
 // ----------------------------------------------------------------------------------
 // K3: scatter records into their tiles' runs.  Same particle partition as K1.
 // Record layout: NOUT == 1 -> float4 {u, v, h, a0};  NOUT == 2 -> 2 x float4
-// {u, v, h, a0}, {a1, 0, 0, 0}.
+// {u, v, h, a0}, {a1, 0, 0, 0}.  Also the per-(block, tile) max |c| (fp32 bits) of the
+// records it inserted, the fixed-point bound of K3b.
 // ----------------------------------------------------------------------------------
-template <int NOUT>
-__global__ __launch_bounds__(kBlock) void k_scatter(
+template <int KID, int NOUT>
+__global__ __launch_bounds__(kCountBlock) void k_scatter(
     const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
     const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long per_block,
     Grid g, const int* __restrict__ hist, const long long* __restrict__ tile_start,
-    float4* __restrict__ recs, int* __restrict__ wide_list, int* __restrict__ wide_cursor) {
+    float4* __restrict__ recs, unsigned* __restrict__ cmx, int* __restrict__ wide_list,
+    int* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) int cur[];
+    unsigned* cm = (unsigned*)(cur + g.ntiles);  // [ntiles][NOUT]
     const int* row = hist + (long long)blockIdx.x * g.ntiles;
-    for (int t = threadIdx.x; t < g.ntiles; t += kBlock) cur[t] = row[t];
+    for (int t = threadIdx.x; t < g.ntiles; t += kCountBlock) {
+        cur[t] = row[t];
+#pragma unroll
+        for (int o = 0; o < NOUT; ++o) cm[t * NOUT + o] = 0u;
+    }
     __syncthreads();
     long long p0 = (long long)blockIdx.x * per_block;
     long long p1 = min(n, p0 + per_block);
-    for (long long p = p0 + threadIdx.x; p < p1; p += kBlock) {
-        float pu = u[p], pv = v[p], ph = h[p];
-        Box b;
-        if (!footprint(g, pu, pv, ph, b)) continue;
-        int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
-        int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
-        if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > kWideTiles) {
-            wide_list[atomicAdd(wide_cursor, 1)] = (int)p;
-            continue;
+    for (long long base = p0; base < p1; base += (long long)kCountBlock * kUnroll) {
+        float pu[kUnroll], pv[kUnroll], ph[kUnroll], pa0[kUnroll], pa1[kUnroll];
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k) {
+            long long p = base + threadIdx.x + (long long)k * kCountBlock;
+            bool in = p < p1;
+            pu[k] = in ? u[p] : 0.0f;
+            pv[k] = in ? v[p] : 0.0f;
+            ph[k] = in ? h[p] : 0.0f;
+            pa0[k] = in ? a0[p] : 0.0f;
+            pa1[k] = (in && NOUT == 2) ? a1[p] : 0.0f;
         }
-        float4 r0 = make_float4(pu, pv, ph, a0[p]);
-        float4 r1 = make_float4(NOUT == 2 ? a1[p] : 0.0f, 0.0f, 0.0f, 0.0f);
-        for (int tx = tx0; tx <= tx1; ++tx)
-            for (int ty = ty0; ty <= ty1; ++ty) {
-                int t = tx * g.nty + ty;
-                long long slot = tile_start[t] + atomicAdd(&cur[t], 1);
-                if constexpr (NOUT == 1) {
-                    recs[slot] = r0;
-                } else {
-                    recs[2 * slot] = r0;
-                    recs[2 * slot + 1] = r1;
-                }
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k) {
+            long long p = base + threadIdx.x + (long long)k * kCountBlock;
+            Box b;
+            if (!footprint(g, pu[k], pv[k], ph[k], b)) continue;
+            unsigned c0 = __float_as_uint(fabsf((float)term_coef<KID>(pa0[k], ph[k])));
+            unsigned c1 = NOUT == 2 ? __float_as_uint(fabsf((float)term_coef<KID>(pa1[k], ph[k]))) : 0u;
+            int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
+            int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
+            if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > kWideTiles) {
+                wide_list[atomicAdd(&ctr[cWideCursor], 1)] = (int)p;
+                atomicMax((unsigned*)&ctr[cWideMax0], c0);
+                if (NOUT == 2) atomicMax((unsigned*)&ctr[cWideMax1], c1);
+                continue;
             }
+            float4 r0 = make_float4(pu[k], pv[k], ph[k], pa0[k]);
+            float4 r1 = make_float4(pa1[k], 0.0f, 0.0f, 0.0f);
+            for (int tx = tx0; tx <= tx1; ++tx)
+                for (int ty = ty0; ty <= ty1; ++ty) {
+                    int t = tx * g.nty + ty;
+                    long long slot = tile_start[t] + atomicAdd(&cur[t], 1);
+                    atomicMax(&cm[t * NOUT], c0);
+                    if constexpr (NOUT == 2) {
+                        atomicMax(&cm[t * NOUT + 1], c1);
+                        recs[2 * slot] = r0;
+                        recs[2 * slot + 1] = r1;
+                    } else {
+                        recs[slot] = r0;
+                    }
+                }
+        }
+    }
+    __syncthreads();
+    unsigned* out = cmx + (long long)blockIdx.x * g.ntiles * NOUT;
+    for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kCountBlock) out[t] = cm[t];
+}
+
+// Power-of-two scale exponent so that n * cmax * 2^k <= 2^kScaleBits.
+__device__ __forceinline__ int scale_exp(long long n, float cmax) {
+    if (!(cmax > 0.0f) || n <= 0 || !__builtin_isfinite(cmax)) return 0;
+    int e;
+    frexp((double)n * (double)cmax, &e);  // n*cmax < 2^e
+    return kScaleBits - e;
+}
+
+// ----------------------------------------------------------------------------------
+// K3b: per tile, max over blocks of cmx -> fixed-point exponents tile_k[t] = {k0, k1}.
+// ----------------------------------------------------------------------------------
+template <int NOUT>
+__global__ __launch_bounds__(kBlock) void k_tilescale(const unsigned* __restrict__ cmx, int nblk,
+                                                      int ntiles,
+                                                      const int* __restrict__ tile_total,
+                                                      int2* __restrict__ tile_k) {
+    __shared__ unsigned part[4][64][NOUT];
+    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int t = blockIdx.x * 64 + lane;
+    int b0 = (int)((long long)nblk * w / 4), b1 = (int)((long long)nblk * (w + 1) / 4);
+    unsigned m[NOUT];
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) m[o] = 0u;
+    if (t < ntiles)
+        for (int b = b0; b < b1; ++b)
+#pragma unroll
+            for (int o = 0; o < NOUT; ++o)
+                m[o] = max(m[o], cmx[((long long)b * ntiles + t) * NOUT + o]);
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) part[w][lane][o] = m[o];
+    __syncthreads();
+    if (w == 0 && t < ntiles) {
+        int k[2] = {0, 0};
+#pragma unroll
+        for (int o = 0; o < NOUT; ++o) {
+            unsigned mm = max(max(part[0][lane][o], part[1][lane][o]),
+                              max(part[2][lane][o], part[3][lane][o]));
+            k[o] = scale_exp(tile_total[t], __uint_as_float(mm));
+        }
+        tile_k[t] = make_int2(k[0], k[1]);
     }
 }
 
 // ----------------------------------------------------------------------------------
-// Pair accumulation into the LDS tile
+// Pair accumulation into the LDS tile (int64 fixed point)
 // ----------------------------------------------------------------------------------
 template <int KID, int NOUT>
-__device__ __forceinline__ void accumulate(const Prep& P, float r2, float* acc0, float* acc1,
-                                           int k) {
+__device__ __forceinline__ void accumulate(const Prep& P, float r2, unsigned long long* acc0,
+                                           unsigned long long* acc1, int k) {
     float q = __builtin_sqrtf(r2) * P.hinv;
     float w = kernel_shape<KID>(q);
-    atomicAdd(&acc0[k], P.c0 * w);
-    if constexpr (NOUT == 2) atomicAdd(&acc1[k], P.c1 * w);
+    atomicAdd(&acc0[k], f2fix(P.s0 * w));
+    if constexpr (NOUT == 2) atomicAdd(&acc1[k], f2fix(P.s1 * w));
 }
 
 // One wave sweeps the (clipped) box of one wave-uniform record: lanes along y (the
-// contiguous image axis), so LDS atomics of a wave hit distinct consecutive words.
+// contiguous image axis), so the LDS atomics of a wave hit distinct consecutive words.
 template <int KID, int NOUT>
 __device__ __forceinline__ void sweep(const Grid& g, const Prep& P, int X0, int Y0,
-                                      const float* xt, const float* yt, float* acc0,
-                                      float* acc1, int lane) {
-    int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
+                                      const float* xt, const float* yt,
+                                      unsigned long long* acc0, unsigned long long* acc1,
+                                      int lane) {
+    int bh = P.b.y1 - P.b.y0 + 1;
     if (bh <= 64) {
         int rps = 64 / bh;
         int r = lane / bh, c = lane - r * bh;
@@ -269,7 +394,6 @@ __device__ __forceinline__ void sweep(const Grid& g, const Prep& P, int X0, int 
             }
         }
     }
-    (void)bw;
 }
 
 __device__ __forceinline__ Prep bcast_prep(const Prep& P, int l) {
@@ -280,8 +404,8 @@ __device__ __forceinline__ Prep bcast_prep(const Prep& P, int l) {
     Q.thr = bcast(P.thr, l);
     Q.band = bcast(P.band, l);
     Q.hinv = bcast(P.hinv, l);
-    Q.c0 = bcast(P.c0, l);
-    Q.c1 = bcast(P.c1, l);
+    Q.s0 = bcast(P.s0, l);
+    Q.s1 = bcast(P.s1, l);
     Q.b.x0 = bcast(P.b.x0, l);
     Q.b.x1 = bcast(P.b.x1, l);
     Q.b.y0 = bcast(P.b.y0, l);
@@ -310,12 +434,15 @@ __device__ __forceinline__ void load_rec(const float4* recs, long long i, float&
     }
 }
 
+constexpr int kTilePix = kTile * kTile;
+constexpr int kFlagAccumulate = 1;
+constexpr int kFlagRatio = 2;  // fused ratio: out0 <- map0 / map1
+
 // Tile prologue: zero accumulators, fp32 corner tables (exact fp64 corners rounded).
-template <int NOUT>
-__device__ __forceinline__ void tile_prologue(const Grid& g, int X0, int Y0, float* smem) {
-    for (int i = threadIdx.x; i < NOUT * kTile * kTile; i += kBlock) smem[i] = 0.0f;
-    float* xt = smem + NOUT * kTile * kTile;
-    float* yt = xt + kTile;
+template <int NOUT, int NT>
+__device__ __forceinline__ void tile_prologue(const Grid& g, int X0, int Y0,
+                                              unsigned long long* acc, float* xt, float* yt) {
+    for (int i = threadIdx.x; i < NOUT * kTilePix; i += NT) acc[i] = 0ull;
     if (threadIdx.x < kTile)
         xt[threadIdx.x] = (float)corner_x(g, X0 + threadIdx.x);
     else if (threadIdx.x < 2 * kTile)
@@ -323,52 +450,57 @@ __device__ __forceinline__ void tile_prologue(const Grid& g, int X0, int Y0, flo
     __syncthreads();
 }
 
+// Convert a pixel's fixed-point sums and write it (plain store: the tile has one owner).
 template <int NOUT>
-__device__ __forceinline__ void tile_epilogue(const Grid& g, int X0, int Y0, int TW, int TH,
-                                              const float* smem, float* out0, float* out1,
-                                              bool atomic) {
-    __syncthreads();
-    for (int k = threadIdx.x; k < kTile * kTile; k += kBlock) {
-        int lx = k >> kTileShift, ly = k & (kTile - 1);
-        if (lx >= TW || ly >= TH) continue;
-        long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
-        float a = smem[k];
-        if (atomic) {
-            if (a != 0.0f) atomicAdd(&out0[o], a);
-        } else {
-            out0[o] = a;
-        }
-        if constexpr (NOUT == 2) {
-            float b = smem[kTile * kTile + k];
-            if (atomic) {
-                if (b != 0.0f) atomicAdd(&out1[o], b);
-            } else {
-                out1[o] = b;
-            }
-        }
+__device__ __forceinline__ void emit_pixel(long long o, long long s0, long long s1, int k0,
+                                           int k1, float* out0, float* out1, int flags) {
+    float v0 = (float)ldexp((double)s0, -k0);
+    float v1 = NOUT == 2 ? (float)ldexp((double)s1, -k1) : 0.0f;
+    if (flags & kFlagAccumulate) {
+        v0 += out0[o];
+        if (NOUT == 2) v1 += out1[o];
+    }
+    if (NOUT == 2) {
+        out1[o] = v1;
+        out0[o] = (flags & kFlagRatio) ? (v1 != 0.0f ? v0 / v1 : 0.0f) : v0;
+    } else {
+        out0[o] = v0;
     }
 }
 
 // ----------------------------------------------------------------------------------
-// K4: deposit one work item (a run of records of one tile) into LDS, write the tile.
+// K4: deposit one work item (a run of records of one tile) into LDS, then write the
+// tile (single-item tiles) or its int64 partial slab (split tiles).
 // ----------------------------------------------------------------------------------
 template <int KID, int NOUT>
-__global__ __launch_bounds__(kBlock) void k_deposit(Grid g, const float4* __restrict__ recs,
-                                                    const Item* __restrict__ items,
-                                                    float* __restrict__ out0,
-                                                    float* __restrict__ out1, int accumulate_all) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* acc0 = smem;
-    float* acc1 = smem + kTile * kTile;
-    const float* xt = smem + NOUT * kTile * kTile;
-    const float* yt = xt + kTile;
+__global__ __launch_bounds__(kDepBlock) void k_deposit(
+    Grid g, const float4* __restrict__ recs, const Item* __restrict__ items,
+    const int2* __restrict__ tile_k, unsigned long long* __restrict__ slabs,
+    float* __restrict__ out0, float* __restrict__ out1, int flags) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];
+    unsigned long long* acc0 = acc;
+    unsigned long long* acc1 = acc + kTilePix;
+    float* xt = (float*)(acc + NOUT * kTilePix);
+    float* yt = xt + kTile;
     const Item it = items[blockIdx.x];
     int tx = it.tile / g.nty, ty = it.tile - (it.tile / g.nty) * g.nty;
     int X0 = tx * kTile, Y0 = ty * kTile;
     int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
-    tile_prologue<NOUT>(g, X0, Y0, smem);
+    if (it.count == 0) {  // empty tile: the map is 0 there
+        if (flags & kFlagAccumulate) return;
+        for (int k = threadIdx.x; k < kTilePix; k += kDepBlock) {
+            int lx = k >> kTileShift, ly = k & (kTile - 1);
+            if (lx >= TW || ly >= TH) continue;
+            long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
+            out0[o] = 0.0f;
+            if (NOUT == 2) out1[o] = 0.0f;
+        }
+        return;
+    }
+    tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
+    const int2 kk = tile_k[it.tile];
     int lane = threadIdx.x & 63;
-    for (int base = 0; base < it.count; base += kBlock) {
+    for (int base = 0; base < it.count; base += kDepBlock) {
         int i = base + threadIdx.x;
         Prep P;
         P.b = Box{0, -1, 0, -1};
@@ -376,7 +508,8 @@ __global__ __launch_bounds__(kBlock) void k_deposit(Grid g, const float4* __rest
         if (i < it.count) {
             float pu, pv, ph, pa0, pa1;
             load_rec<NOUT>(recs, it.start + i, pu, pv, ph, pa0, pa1);
-            live = prep_record<KID>(g, pu, pv, ph, pa0, pa1, P) && clip(P.b, X0, Y0, TW, TH);
+            live = prep_record<KID>(g, pu, pv, ph, pa0, pa1, kk.x, kk.y, P) &&
+                   clip(P.b, X0, Y0, TW, TH);
         }
         int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
         bool small = live && bw <= 4 && bh <= 4;
@@ -395,8 +528,7 @@ __global__ __launch_bounds__(kBlock) void k_deposit(Grid g, const float4* __rest
             for (int ii = 0; ii < 4; ++ii) {
                 if (ii < bw) {
                     int xi = P.b.x0 + ii;
-                    float X = xt[xi - X0];
-                    float dx = P.u - X;
+                    float dx = P.u - xt[xi - X0];
                     float dx2 = dx * dx;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
@@ -421,12 +553,53 @@ __global__ __launch_bounds__(kBlock) void k_deposit(Grid g, const float4* __rest
             sweep<KID, NOUT>(g, Q, X0, Y0, xt, yt, acc0, acc1, lane);
         }
     }
-    tile_epilogue<NOUT>(g, X0, Y0, TW, TH, smem, out0, out1, accumulate_all || it.multi);
+    __syncthreads();
+    if (it.slab >= 0) {  // split tile: exact partial sums, merged by K5
+        unsigned long long* dst = slabs + (long long)it.slab * NOUT * kTilePix;
+        for (int k = threadIdx.x; k < NOUT * kTilePix; k += kDepBlock) dst[k] = acc[k];
+        return;
+    }
+    for (int k = threadIdx.x; k < kTilePix; k += kDepBlock) {
+        int lx = k >> kTileShift, ly = k & (kTile - 1);
+        if (lx >= TW || ly >= TH) continue;
+        long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
+        emit_pixel<NOUT>(o, (long long)acc0[k], NOUT == 2 ? (long long)acc1[k] : 0, kk.x, kk.y,
+                         out0, out1, flags);
+    }
 }
 
 // ----------------------------------------------------------------------------------
-// K5: wide particles (footprint over > kWideTiles tiles).  One workgroup per tile,
-// each wave takes every 4th wide particle and sweeps its clipped box.
+// K5: split tiles -- exact int64 sum of the item slabs, convert, write.
+// ----------------------------------------------------------------------------------
+template <int NOUT>
+__global__ __launch_bounds__(kBlock) void k_merge(Grid g, const Merge* __restrict__ merges,
+                                                  const unsigned long long* __restrict__ slabs,
+                                                  const int2* __restrict__ tile_k,
+                                                  float* __restrict__ out0,
+                                                  float* __restrict__ out1, int flags) {
+    const Merge m = merges[blockIdx.x];
+    int tx = m.tile / g.nty, ty = m.tile - (m.tile / g.nty) * g.nty;
+    int X0 = tx * kTile, Y0 = ty * kTile;
+    int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
+    const int2 kk = tile_k[m.tile];
+    for (int k = threadIdx.x; k < kTilePix; k += kBlock) {
+        int lx = k >> kTileShift, ly = k & (kTile - 1);
+        if (lx >= TW || ly >= TH) continue;
+        unsigned long long s0 = 0, s1 = 0;
+        for (int j = 0; j < m.nslab; ++j) {
+            const unsigned long long* src = slabs + (long long)(m.slab0 + j) * NOUT * kTilePix;
+            s0 += src[k];
+            if (NOUT == 2) s1 += src[kTilePix + k];
+        }
+        long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
+        emit_pixel<NOUT>(o, (long long)s0, (long long)s1, kk.x, kk.y, out0, out1, flags);
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// K6: wide particles (footprint over > kWideTiles tiles).  One workgroup per tile, each
+// wave takes every 4th wide particle and sweeps its clipped box; fixed point with the
+// wide particles' own bound, added onto the tile (this workgroup is its only writer).
 // ----------------------------------------------------------------------------------
 template <int KID, int NOUT>
 __global__ __launch_bounds__(kBlock) void k_wide(Grid g, const float* __restrict__ u,
@@ -435,35 +608,45 @@ __global__ __launch_bounds__(kBlock) void k_wide(Grid g, const float* __restrict
                                                  const float* __restrict__ a0,
                                                  const float* __restrict__ a1,
                                                  const int* __restrict__ wide_list, int n_wide,
+                                                 const int* __restrict__ ctr,
                                                  float* __restrict__ out0,
                                                  float* __restrict__ out1) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* acc0 = smem;
-    float* acc1 = smem + kTile * kTile;
-    const float* xt = smem + NOUT * kTile * kTile;
-    const float* yt = xt + kTile;
+    extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];
+    unsigned long long* acc0 = acc;
+    unsigned long long* acc1 = acc + kTilePix;
+    float* xt = (float*)(acc + NOUT * kTilePix);
+    float* yt = xt + kTile;
+    int* any = (int*)(yt + kTile);
     int t = blockIdx.x;
     int tx = t / g.nty, ty = t - (t / g.nty) * g.nty;
     int X0 = tx * kTile, Y0 = ty * kTile;
     int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
-    tile_prologue<NOUT>(g, X0, Y0, smem);
-    int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int* any = (int*)(smem + NOUT * kTile * kTile + 2 * kTile);
     if (threadIdx.x == 0) *any = 0;
-    __syncthreads();
+    tile_prologue<NOUT, kBlock>(g, X0, Y0, acc, xt, yt);
+    int k0 = scale_exp(n_wide, __uint_as_float((unsigned)ctr[cWideMax0]));
+    int k1 = NOUT == 2 ? scale_exp(n_wide, __uint_as_float((unsigned)ctr[cWideMax1])) : 0;
+    int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int k = wv; k < n_wide; k += kBlock / 64) {
         int p = wide_list[k];
         Prep P;
-        if (!prep_record<KID>(g, u[p], v[p], h[p], a0[p], NOUT == 2 ? a1[p] : 0.0f, P)) continue;
+        if (!prep_record<KID>(g, u[p], v[p], h[p], a0[p], NOUT == 2 ? a1[p] : 0.0f, k0, k1, P))
+            continue;
         if (!clip(P.b, X0, Y0, TW, TH)) continue;
         if (lane == 0) *any = 1;
         sweep<KID, NOUT>(g, P, X0, Y0, xt, yt, acc0, acc1, lane);
     }
     __syncthreads();
-    if (*any) tile_epilogue<NOUT>(g, X0, Y0, TW, TH, smem, out0, out1, true);
+    if (!*any) return;
+    for (int k = threadIdx.x; k < kTilePix; k += kBlock) {
+        int lx = k >> kTileShift, ly = k & (kTile - 1);
+        if (lx >= TW || ly >= TH) continue;
+        long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
+        emit_pixel<NOUT>(o, (long long)acc0[k], NOUT == 2 ? (long long)acc1[k] : 0, k0, k1,
+                         out0, out1, kFlagAccumulate);
+    }
 }
 
-// K6: out0 <- out0 / out1 (0 where out1 == 0).
+// K7: out0 <- out0 / out1 (0 where out1 == 0).
 __global__ __launch_bounds__(kBlock) void k_ratio(float* __restrict__ out0,
                                                   const float* __restrict__ out1, long long m) {
     long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
@@ -537,7 +720,7 @@ __global__ __launch_bounds__(kBlock) void k_neighbours(Grid g, const float* __re
         bool in = false;
         if (p < n) {
             Prep P;
-            if (prep_record<2>(g, u[p], v[p], h[p], 0.0f, 0.0f, P) && xi >= P.b.x0 &&
+            if (prep_record<2>(g, u[p], v[p], h[p], 0.0f, 0.0f, 0, 0, P) && xi >= P.b.x0 &&
                 xi <= P.b.x1 && yi >= P.b.y0 && yi <= P.b.y1) {
                 float r2;
                 in = decide(g, P, xi, yi, X, Y, r2);
@@ -584,8 +767,11 @@ struct Buf {
     size_t cap = 0;
 };
 
-constexpr int kStages = 8;  // memset, count, colscan, tilescan, scatter, deposit, wide, ratio
-enum Stage { kSMemset = 0, kSCount, kSColscan, kSTilescan, kSScatter, kSDeposit, kSWide, kSRatio };
+constexpr int kStages = 10;
+enum Stage {
+    kSMemset = 0, kSCount, kSColscan, kSTilescan, kSScatter, kSScale, kSDeposit, kSMerge,
+    kSWide, kSRatio
+};
 
 struct Workspace {
     std::mutex mu;
@@ -596,7 +782,8 @@ struct Workspace {
     bool ev_live[kStages] = {};
     double stage_ms[kStages] = {};
     long long stage_n[kStages] = {};
-    Buf in[5], out[2], hist, tile_total, tile_start, items, counters, recs, wide, morton, aux[6];
+    Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
+        wide, slabs, morton, aux[6];
     int* h_counters = nullptr;  // pinned
     int morton_ntx = -1, morton_nty = -1;
     long long stats[8] = {0};
@@ -617,7 +804,7 @@ static int prof_fold(Workspace& ws) {
     return ASP_OK;
 }
 
-// RAII-free stage bracket: record start/stop events around a launch when profiling.
+// Stage bracket: record start/stop events around a launch when profiling.
 struct StageMark {
     Workspace& ws;
     int k;
@@ -657,10 +844,17 @@ static int ensure(Buf& b, size_t bytes) {
     return ASP_OK;
 }
 
-#define ASP_TRY(expr)             \
-    do {                          \
-        int rc_ = (expr);         \
+#define ASP_TRY(expr)                  \
+    do {                               \
+        int rc_ = (expr);              \
         if (rc_ != ASP_OK) return rc_; \
+    } while (0)
+
+#define ASP_LAUNCHED()                                                                    \
+    do {                                                                                  \
+        hipError_t e_ = hipGetLastError();                                                \
+        if (e_ != hipSuccess)                                                             \
+            return fail(ASP_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e_)); \
     } while (0)
 
 static uint32_t spread_bits(uint32_t x) {
@@ -702,6 +896,12 @@ static bool make_grid(double x_min, double x_max, double y_min, double y_max, in
     g.psx = (x_max - x_min) / nx;
     g.psy_pix = (y_max - y_min) / nx;
     g.psy_cull = (y_max - y_min) / ny;
+    if (!(g.psx > 0.0) || !(g.psy_pix > 0.0) || !(g.psy_cull > 0.0)) return false;
+    g.xminf = (float)x_min;
+    g.yminf = (float)y_min;
+    g.ipsx = (float)(1.0 / g.psx);
+    g.ipsy = (float)(1.0 / g.psy_pix);
+    if (!std::isfinite(g.ipsx) || !std::isfinite(g.ipsy)) return false;
     double mg = std::max({std::fabs(x_min), std::fabs(x_min + nx * g.psx), std::fabs(y_min),
                           std::fabs(y_min + ny * g.psy_pix)});
     g.mg = (float)(mg * (1.0 + 1e-6));
@@ -717,26 +917,74 @@ static bool make_grid(double x_min, double x_max, double y_min, double y_max, in
     return true;
 }
 
-constexpr int kMaxTiles = 16384;  // K1/K3 LDS histogram limit (64 KiB)
+constexpr int kMaxTiles = 4096;  // K3 LDS: cursor + per-tile max (12 B/tile at 2 maps)
 
+struct Plan {
+    long long n, nblk, per_block;
+    int n_items, n_merges, n_slabs, n_wide;
+    long long n_recs;
+};
+
+// K3..K7 for one kernel / map count.
 template <int KID, int NOUT>
-static int launch_deposit(const Grid& g, Workspace& ws, int n_items, const float* u,
-                          const float* v, const float* h, const float* a0, const float* a1,
-                          int n_wide, float* o0, float* o1, bool accumulate, hipStream_t st) {
-    size_t lds = (size_t)(NOUT * kTile * kTile + 2 * kTile + 4) * sizeof(float);
-    if (n_items > 0) {
-        StageMark m(ws, kSDeposit, st);
-        hipLaunchKernelGGL((k_deposit<KID, NOUT>), dim3(n_items), dim3(kBlock), lds, st, g,
-                           (const float4*)ws.recs.p, (const Item*)ws.items.p, o0, o1,
-                           accumulate ? 1 : 0);
-        ASP_HIP(hipGetLastError());
+static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u,
+                    const float* v, const float* h, const float* a0, const float* a1, float* o0,
+                    float* o1, int flags, hipStream_t st) {
+    int* dc = (int*)ws.counters.p;
+    const bool ratio = (flags & ASP_F_RATIO) != 0;
+    const bool fuse_ratio = ratio && pl.n_wide == 0;
+    int dflags = ((flags & ASP_F_ACCUMULATE) ? kFlagAccumulate : 0) | (fuse_ratio ? kFlagRatio : 0);
+    {
+        StageMark m(ws, kSScatter, st);
+        size_t lds = (size_t)g.ntiles * (1 + NOUT) * sizeof(int);
+        hipLaunchKernelGGL((k_scatter<KID, NOUT>), dim3((unsigned)pl.nblk), dim3(kCountBlock),
+                           lds, st, u, v, h, a0, a1, pl.n, pl.per_block, g, (const int*)ws.hist.p,
+                           (const long long*)ws.tile_start.p, (float4*)ws.recs.p,
+                           (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc);
+        ASP_LAUNCHED();
         m.done();
     }
-    if (n_wide > 0) {
+    {
+        StageMark m(ws, kSScale, st);
+        hipLaunchKernelGGL((k_tilescale<NOUT>), dim3((g.ntiles + 63) / 64), dim3(kBlock), 0, st,
+                           (const unsigned*)ws.cmx.p, (int)pl.nblk, g.ntiles,
+                           (const int*)ws.tile_total.p, (int2*)ws.tile_k.p);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    {
+        StageMark m(ws, kSDeposit, st);
+        size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4;
+        hipLaunchKernelGGL((k_deposit<KID, NOUT>), dim3(pl.n_items), dim3(kDepBlock), lds, st, g,
+                           (const float4*)ws.recs.p, (const Item*)ws.items.p,
+                           (const int2*)ws.tile_k.p, (unsigned long long*)ws.slabs.p, o0, o1,
+                           dflags);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    if (pl.n_merges > 0) {
+        StageMark m(ws, kSMerge, st);
+        hipLaunchKernelGGL((k_merge<NOUT>), dim3(pl.n_merges), dim3(kBlock), 0, st, g,
+                           (const Merge*)ws.merges.p, (const unsigned long long*)ws.slabs.p,
+                           (const int2*)ws.tile_k.p, o0, o1, dflags);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    if (pl.n_wide > 0) {
         StageMark m(ws, kSWide, st);
-        hipLaunchKernelGGL((k_wide<KID, NOUT>), dim3(g.ntiles), dim3(kBlock), lds, st, g, u, v,
-                           h, a0, a1, (const int*)ws.wide.p, n_wide, o0, o1);
-        ASP_HIP(hipGetLastError());
+        size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4 + 16;
+        hipLaunchKernelGGL((k_wide<KID, NOUT>), dim3(g.ntiles), dim3(kBlock), lds, st, g, u, v, h,
+                           a0, a1, (const int*)ws.wide.p, pl.n_wide, (const int*)dc, o0, o1);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    if (ratio && !fuse_ratio) {
+        long long npix = (long long)g.nx * g.ny;
+        long long blocks = std::min<long long>((npix + kBlock - 1) / kBlock, 8192);
+        StageMark m(ws, kSRatio, st);
+        hipLaunchKernelGGL(k_ratio, dim3((unsigned)std::max<long long>(1, blocks)), dim3(kBlock),
+                           0, st, o0, (const float*)o1, npix);
+        ASP_LAUNCHED();
         m.done();
     }
     return ASP_OK;
@@ -762,7 +1010,7 @@ static int project2d(const float* u, const float* v, const float* h, const float
                     "invalid grid: need nx, ny, chunk_size >= 1, finite x_max > x_min, "
                     "y_max > y_min");
     if (g.ntiles > kMaxTiles)
-        return fail(ASP_ERR_UNSUPPORTED, "grid too large (more than 16384 64x64 tiles)");
+        return fail(ASP_ERR_UNSUPPORTED, "grid too large (more than 4096 64x64 tiles)");
     if (device < 0 || device >= 64) return fail(ASP_ERR_INVALID, "bad device");
     int ndev = 0;
     ASP_HIP(hipGetDeviceCount(&ndev));
@@ -805,94 +1053,84 @@ static int project2d(const float* u, const float* v, const float* h, const float
                 ASP_HIP(hipMemcpyAsync(d1, out1, npix * sizeof(float), hipMemcpyHostToDevice, st));
         }
     }
-    const bool accumulate = flags & ASP_F_ACCUMULATE;
     if (ws.prof) ASP_TRY(prof_fold(ws));
-    if (!accumulate) {
-        StageMark m(ws, kSMemset, st);
-        ASP_HIP(hipMemsetAsync(d0, 0, npix * sizeof(float), st));
-        if (d1) ASP_HIP(hipMemsetAsync(d1, 0, npix * sizeof(float), st));
-        m.done();
-    }
 
-    int n_items = 0, n_wide = 0;
-    long long n_recs = 0;
-    if (n > 0) {
+    Plan pl{};
+    pl.n = n;
+    if (n == 0) {  // all-zero map(s)
+        if (!(flags & ASP_F_ACCUMULATE)) {
+            StageMark m(ws, kSMemset, st);
+            ASP_HIP(hipMemsetAsync(d0, 0, npix * sizeof(float), st));
+            if (d1) ASP_HIP(hipMemsetAsync(d1, 0, npix * sizeof(float), st));
+            m.done();
+        }
+    } else {
         ASP_TRY(ensure_morton(ws, g.ntx, g.nty, st));
-        long long nblk = std::min<long long>(1024, std::max<long long>(1, (n + 4095) / 4096));
-        long long per_block = (n + nblk - 1) / nblk;
-        nblk = (n + per_block - 1) / per_block;
-        ASP_TRY(ensure(ws.hist, (size_t)nblk * g.ntiles * sizeof(int)));
+        pl.nblk = std::min<long long>(1024, std::max<long long>(1, (n + 8191) / 8192));
+        pl.per_block = (n + pl.nblk - 1) / pl.nblk;
+        pl.nblk = (n + pl.per_block - 1) / pl.per_block;
+        ASP_TRY(ensure(ws.hist, (size_t)pl.nblk * g.ntiles * sizeof(int)));
+        ASP_TRY(ensure(ws.cmx, (size_t)pl.nblk * g.ntiles * nout * sizeof(unsigned)));
         ASP_TRY(ensure(ws.tile_total, (size_t)g.ntiles * sizeof(int)));
         ASP_TRY(ensure(ws.tile_start, (size_t)g.ntiles * sizeof(long long)));
+        ASP_TRY(ensure(ws.tile_k, (size_t)g.ntiles * sizeof(int2)));
         ASP_TRY(ensure(ws.items, (size_t)(g.ntiles + kTargetItems + 16) * sizeof(Item)));
-        ASP_TRY(ensure(ws.counters, 16 * sizeof(int)));
-        if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, 16 * sizeof(int)));
+        ASP_TRY(ensure(ws.merges, (size_t)(g.ntiles + 16) * sizeof(Merge)));
+        ASP_TRY(ensure(ws.counters, cNum * sizeof(int)));
+        if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, cNum * sizeof(int)));
         int* dc = (int*)ws.counters.p;
-        ASP_HIP(hipMemsetAsync(dc, 0, 16 * sizeof(int), st));
-        size_t lds_hist = (size_t)g.ntiles * sizeof(int);
+        ASP_HIP(hipMemsetAsync(dc, 0, cNum * sizeof(int), st));
         {
             StageMark m(ws, kSCount, st);
-            hipLaunchKernelGGL(k_count, dim3((unsigned)nblk), dim3(kBlock), lds_hist, st, du, dv,
-                               dh, n, per_block, g, (int*)ws.hist.p, dc + 2);
-            ASP_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_count, dim3((unsigned)pl.nblk), dim3(kCountBlock),
+                               (size_t)g.ntiles * sizeof(int), st, du, dv, dh, n, pl.per_block, g,
+                               (int*)ws.hist.p, dc);
+            ASP_LAUNCHED();
             m.done();
         }
         {
             StageMark m(ws, kSColscan, st);
             hipLaunchKernelGGL(k_colscan, dim3((g.ntiles + 63) / 64), dim3(kBlock), 0, st,
-                               (int*)ws.hist.p, (int)nblk, g.ntiles, (int*)ws.tile_total.p);
-            ASP_HIP(hipGetLastError());
+                               (int*)ws.hist.p, (int)pl.nblk, g.ntiles, (int*)ws.tile_total.p);
+            ASP_LAUNCHED();
             m.done();
         }
         {
             StageMark m(ws, kSTilescan, st);
             hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(kScanThreads), 0, st,
                                (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles,
-                               (long long*)ws.tile_start.p, (Item*)ws.items.p, dc);
-            ASP_HIP(hipGetLastError());
+                               (long long*)ws.tile_start.p, (Item*)ws.items.p,
+                               (Merge*)ws.merges.p, dc);
+            ASP_LAUNCHED();
             m.done();
         }
-        ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, 16 * sizeof(int), hipMemcpyDeviceToHost, st));
+        // One small read-back sizes the record / slab buffers.
+        ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, cNum * sizeof(int), hipMemcpyDeviceToHost, st));
         ASP_HIP(hipStreamSynchronize(st));
-        n_items = ws.h_counters[0];
-        n_recs = ws.h_counters[1];
-        n_wide = ws.h_counters[2];
-        if (n_recs >= 0x7fffffffLL)
+        pl.n_items = ws.h_counters[cItems];
+        pl.n_recs = ws.h_counters[cRecs];
+        pl.n_wide = ws.h_counters[cWideCount];
+        pl.n_slabs = ws.h_counters[cSlabs];
+        pl.n_merges = ws.h_counters[cMerges];
+        if (pl.n_recs >= 0x7fffffffLL)
             return fail(ASP_ERR_UNSUPPORTED, "more than 2^31 particle-tile records");
-        ASP_TRY(ensure(ws.recs, (size_t)n_recs * nout * sizeof(float4)));
-        ASP_TRY(ensure(ws.wide, (size_t)n_wide * sizeof(int)));
-        StageMark ms(ws, kSScatter, st);
-        if (nout == 1)
-            hipLaunchKernelGGL((k_scatter<1>), dim3((unsigned)nblk), dim3(kBlock), lds_hist, st,
-                               du, dv, dh, da0, da1, n, per_block, g, (const int*)ws.hist.p,
-                               (const long long*)ws.tile_start.p, (float4*)ws.recs.p,
-                               (int*)ws.wide.p, dc + 4);
-        else
-            hipLaunchKernelGGL((k_scatter<2>), dim3((unsigned)nblk), dim3(kBlock), lds_hist, st,
-                               du, dv, dh, da0, da1, n, per_block, g, (const int*)ws.hist.p,
-                               (const long long*)ws.tile_start.p, (float4*)ws.recs.p,
-                               (int*)ws.wide.p, dc + 4);
-        ASP_HIP(hipGetLastError());
-        ms.done();
+        ASP_TRY(ensure(ws.recs, (size_t)pl.n_recs * nout * sizeof(float4)));
+        ASP_TRY(ensure(ws.wide, (size_t)pl.n_wide * sizeof(int)));
+        ASP_TRY(ensure(ws.slabs, (size_t)pl.n_slabs * nout * kTilePix * sizeof(long long)));
         int rc;
-#define ASP_DEP(K, N) \
-    launch_deposit<K, N>(g, ws, n_items, du, dv, dh, da0, da1, n_wide, d0, d1, accumulate, st)
+#define ASP_TAIL(K, N) \
+    run_tail<K, N>(g, ws, pl, du, dv, dh, da0, da1, d0, d1, flags, st)
         if (kid == 0)
-            rc = nout == 1 ? ASP_DEP(0, 1) : ASP_DEP(0, 2);
+            rc = nout == 1 ? ASP_TAIL(0, 1) : ASP_TAIL(0, 2);
         else if (kid == 1)
-            rc = nout == 1 ? ASP_DEP(1, 1) : ASP_DEP(1, 2);
+            rc = nout == 1 ? ASP_TAIL(1, 1) : ASP_TAIL(1, 2);
         else
-            rc = nout == 1 ? ASP_DEP(2, 1) : ASP_DEP(2, 2);
-#undef ASP_DEP
+            rc = nout == 1 ? ASP_TAIL(2, 1) : ASP_TAIL(2, 2);
+#undef ASP_TAIL
         if (rc != ASP_OK) return rc;
     }
-    if (flags & ASP_F_RATIO) {
-        long long blocks = std::min<long long>((npix + kBlock - 1) / kBlock, 8192);
-        StageMark m(ws, kSRatio, st);
-        hipLaunchKernelGGL(k_ratio, dim3((unsigned)std::max<long long>(1, blocks)), dim3(kBlock),
-                           0, st, d0, (const float*)d1, npix);
-        ASP_HIP(hipGetLastError());
-        m.done();
+    if (n == 0 && (flags & ASP_F_RATIO)) {
+        // 0 / 0 -> 0: the memset already wrote the ratio map
     }
     if (!dev) {
         ASP_HIP(hipMemcpyAsync(out0, d0, npix * sizeof(float), hipMemcpyDeviceToHost, st));
@@ -900,12 +1138,14 @@ static int project2d(const float* u, const float* v, const float* h, const float
             ASP_HIP(hipMemcpyAsync(out1, d1, npix * sizeof(float), hipMemcpyDeviceToHost, st));
         ASP_HIP(hipStreamSynchronize(st));
     }
-    ws.stats[0] = n_recs;
-    ws.stats[1] = n_items;
-    ws.stats[2] = n_wide;
+    ws.stats[0] = pl.n_recs;
+    ws.stats[1] = pl.n_items;
+    ws.stats[2] = pl.n_wide;
     ws.stats[3] = kTile;
     ws.stats[4] = g.ntiles;
-    ws.stats[5] = n > 0 && ws.h_counters ? ws.h_counters[3] : 0;
+    ws.stats[5] = n > 0 ? ws.h_counters[cChunk] : 0;
+    ws.stats[6] = pl.n_merges;
+    ws.stats[7] = pl.n_slabs;
     return ASP_OK;
 }
 
@@ -1150,9 +1390,10 @@ int asp_release(int32_t device) {
         std::lock_guard<std::mutex> lock(ws.mu);
         if (hipSetDevice(d) != hipSuccess) continue;
         Buf* all[] = {&ws.in[0], &ws.in[1], &ws.in[2], &ws.in[3], &ws.in[4], &ws.out[0],
-                      &ws.out[1], &ws.hist, &ws.tile_total, &ws.tile_start, &ws.items,
-                      &ws.counters, &ws.recs, &ws.wide, &ws.morton, &ws.aux[0], &ws.aux[1],
-                      &ws.aux[2], &ws.aux[3], &ws.aux[4], &ws.aux[5]};
+                      &ws.out[1], &ws.hist, &ws.cmx, &ws.tile_total, &ws.tile_start,
+                      &ws.tile_k, &ws.items, &ws.merges, &ws.counters, &ws.recs, &ws.wide,
+                      &ws.slabs, &ws.morton, &ws.aux[0], &ws.aux[1], &ws.aux[2], &ws.aux[3],
+                      &ws.aux[4], &ws.aux[5]};
         for (Buf* b : all) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;

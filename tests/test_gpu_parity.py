@@ -320,3 +320,20 @@ def test_device_api_ratio_accumulate(gpu, oracle):
     with np.errstate(divide="ignore", invalid="ignore"):
         want = np.where(o1n != 0, o0n / o1n, 0.0)
     np.testing.assert_allclose(r.cpu().numpy(), want, rtol=1e-6)
+
+
+def test_bitwise_deterministic_and_permutation_invariant(gpu):
+    """Fixed-point (int64) accumulation: repeated runs AND permuted inputs give
+    bit-identical maps (the reference itself varies by summation order, S11)."""
+    from asp_amd.tools.projections import create_image, create_weighted_image
+    p = plummer_f32(300_000, seed=12, h_law="physical")
+    ext = (-4.0, 4.0, -4.0, 4.0)
+    a = create_image(p["pos"], p["h"], p["m"], (512, 512), 64, 2, *ext)
+    b = create_image(p["pos"], p["h"], p["m"], (512, 512), 64, 2, *ext)
+    perm = np.random.default_rng(1).permutation(p["h"].size)
+    c = create_image(p["pos"][perm], p["h"][perm], p["m"][perm], (512, 512), 64, 2, *ext)
+    assert np.array_equal(a, b) and np.array_equal(a, c)
+    w1 = create_weighted_image(p["pos"], p["h"], p["m"], p["T"], (512, 512), 64, 2, *ext)
+    w2 = create_weighted_image(p["pos"][perm], p["h"][perm], p["m"][perm], p["T"][perm],
+                               (512, 512), 64, 2, *ext)
+    assert np.array_equal(w1, w2)
