@@ -20,6 +20,7 @@ ASP_KERNEL_INDICATOR = 2
 ASP_F_DEVICE_PTRS = 0x1
 ASP_F_RATIO = 0x2
 ASP_F_ACCUMULATE = 0x4
+ASP_F_DETERMINISTIC = 0x8
 
 ASP_OK = 0
 ASP_ERR_INVALID = -1

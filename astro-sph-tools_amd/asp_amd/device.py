@@ -35,7 +35,7 @@ def _check(t, name, n=None, device=None):
 
 def project2d(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
               kernel="cubic", ratio: bool = False, accumulate: bool = False, out0=None,
-              out1=None, stream=None):
+              out1=None, stream=None, deterministic: bool = False):
     """Project device-resident particles; returns ``(out0, out1)`` (out1 None for one map).
 
     ``extent = (u_min, u_max, v_min, v_max)``; images are (nx, ny) float32 tensors on the
@@ -62,6 +62,8 @@ def project2d(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
         flags |= _lib.ASP_F_RATIO
     if accumulate:
         flags |= _lib.ASP_F_ACCUMULATE
+    if deterministic:
+        flags |= _lib.ASP_F_DETERMINISTIC
     if stream is None:
         stream = torch.cuda.current_stream(dev).cuda_stream
     P = _lib.ptr

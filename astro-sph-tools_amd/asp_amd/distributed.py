@@ -42,7 +42,8 @@ def zslab_bounds(z, world_size: int, sample: int = 1 << 20, seed: int = 0):
 
 def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
                       kernel="cubic", ratio: bool = False, op: str = "reduce", dst: int = 0,
-                      group=None, out0=None, out1=None, projector=None):
+                      group=None, out0=None, out1=None, projector=None,
+                      deterministic: bool = False):
     """Project this rank's particles, then combine the grids over ``group``.
 
     Returns ``(out0, out1)``: the full map(s) on ``dst`` (``op="reduce"``), on every rank
@@ -54,8 +55,9 @@ def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
     import torch
     import torch.distributed as dist
     proj = project2d if projector is None else projector
+    kw = {"deterministic": True} if deterministic else {}
     o0, o1 = proj(u, v, h, a0, a1, image_size=image_size, extent=extent,
-                  chunk_size=chunk_size, kernel=kernel, ratio=False, out0=out0, out1=out1)
+                  chunk_size=chunk_size, kernel=kernel, ratio=False, out0=out0, out1=out1, **kw)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     outs = [o0] if o1 is None else [o0, o1]

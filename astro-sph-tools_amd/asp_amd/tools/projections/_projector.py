@@ -71,15 +71,18 @@ def create_image(positions: np.ndarray, smoothing_lengths: np.ndarray,
                  particle_properties: np.ndarray, image_size: tuple, chunk_size: int,
                  projection_axis, x_min: float, x_max: float, y_min: float, y_max: float,
                  kernel_func=quartic_spline_kernel, *, device: int = 0,
-                 dtype=np.float64) -> np.ndarray:
+                 dtype=np.float64, deterministic: bool = False) -> np.ndarray:
     """Project particle property A onto an (Nx, Ny) pixel grid (reference semantics).
 
-    ``device`` selects the GPU; ``dtype=np.float32`` skips the host upcast (opt-in).
+    ``device`` selects the GPU; ``dtype=np.float32`` skips the host upcast (opt-in);
+    ``deterministic=True`` selects int64 fixed-point accumulation (bitwise reproducible,
+    input-order independent; see ASP_F_DETERMINISTIC in include/asp.h).
     """
     cs = _check_chunk_size(chunk_size)
     kid = kernel_id_of(kernel_func)
     u, v, h, A = _soa(positions, smoothing_lengths, particle_properties, projection_axis)
-    img, _ = _run(u, v, h, A, None, image_size, cs, (x_min, x_max, y_min, y_max), kid, 0,
+    flags = _lib.ASP_F_DETERMINISTIC if deterministic else 0
+    img, _ = _run(u, v, h, A, None, image_size, cs, (x_min, x_max, y_min, y_max), kid, flags,
                   device)
     return img.astype(dtype, copy=False)
 
@@ -87,7 +90,8 @@ def create_image(positions: np.ndarray, smoothing_lengths: np.ndarray,
 def create_weighted_image(positions, smoothing_lengths, weights, values, image_size,
                           chunk_size, projection_axis, x_min, x_max, y_min, y_max,
                           kernel_func=quartic_spline_kernel, *, device: int = 0,
-                          return_components: bool = False, dtype=np.float64):
+                          return_components: bool = False, dtype=np.float64,
+                          deterministic: bool = False):
     """Weighted-average map, e.g. mass-weighted temperature.
 
     ``sum(w v W) / sum(w W)`` per pixel over the same neighbour sets as
@@ -103,12 +107,13 @@ def create_weighted_image(positions, smoothing_lengths, weights, values, image_s
     if vals.shape[0] != u.shape[0]:
         raise ValueError("values and positions differ in length")
     wv = np.ascontiguousarray(np.asarray(weights, np.float64).reshape(-1) * vals, dtype=np.float32)
+    det = _lib.ASP_F_DETERMINISTIC if deterministic else 0
     if return_components:
-        s0, s1 = _run(u, v, h, wv, w, image_size, cs, (x_min, x_max, y_min, y_max), kid, 0,
+        s0, s1 = _run(u, v, h, wv, w, image_size, cs, (x_min, x_max, y_min, y_max), kid, det,
                       device)
         with np.errstate(divide="ignore", invalid="ignore"):
             ratio = np.where(s1 != 0, s0.astype(np.float64) / s1, 0.0)
         return ratio.astype(dtype, copy=False), s0.astype(dtype), s1.astype(dtype)
     r, _ = _run(u, v, h, wv, w, image_size, cs, (x_min, x_max, y_min, y_max), kid,
-                _lib.ASP_F_RATIO, device)
+                _lib.ASP_F_RATIO | det, device)
     return r.astype(dtype, copy=False)

@@ -12,10 +12,13 @@
 // re-decided by the reference's own fp64 arithmetic, including the chunk cull.  See
 // DESIGN.md §3 for the bound.
 //
-// Accumulation is fixed point: every term A*W is scaled by a per-tile power of two and
-// rounded to an int64 that is added with ds_add_u64 (LDS fp32 atomics run ~10x slower
-// than integer ones on gfx950: tools/microbench_lds.hip).  Integer sums are associative,
-// so maps are bitwise reproducible regardless of scheduling.
+// Accumulation.  LDS fp32 atomics run ~8x slower than fp64 or integer
+// ones on gfx950 (tools/microbench_lds.hip), so tiles accumulate either
+//  * kAccF64 (default): fp32 terms A*W added in fp64 with ds_add_f64 -- more precise than
+//    the fp32 map it produces; or
+//  * kAccFix (ASP_F_DETERMINISTIC): terms scaled by a per-tile power of two, rounded to
+//    int64 and added with ds_add_u64.  Integer sums are associative, so maps are bitwise
+//    reproducible regardless of scheduling and input order.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -29,6 +32,8 @@ constexpr int kTile = 64;          // GPU tile edge in pixels
 constexpr int kTileShift = 6;
 constexpr int kWideTiles = 64;     // particles overlapping more GPU tiles take the wide path
 constexpr int kScaleBits = 61;     // per-tile bound n_t * max|c| maps to <= 2^61
+constexpr int kAccF64 = 0;         // LDS fp64 accumulation
+constexpr int kAccFix = 1;         // LDS int64 fixed point (deterministic)
 
 struct Grid {
     double x_min, y_min;
@@ -54,7 +59,7 @@ struct Prep {
     float thr;   // (2h)^2 in fp32
     float band;  // |r2_32 - thr_32| <= band  ->  decide in fp64
     float hinv;  // 1/h
-    float s0, s1;  // a * norm(h) * 2^k_tile: fixed-point term = s * shape(q)
+    float s0, s1;  // a * norm(h) (kAccF64) or a * norm(h) * 2^k_tile (kAccFix)
     Box b;
 };
 
@@ -189,7 +194,7 @@ __device__ __forceinline__ float kernel_shape(float q) {
     }
 }
 
-template <int KID>
+template <int KID, int ACC = kAccF64>
 __device__ __forceinline__ bool prep_record(const Grid& g, float u, float v, float h, float a0,
                                             float a1, int k0, int k1, Prep& P) {
     if (!footprint(g, u, v, h, P.b)) return false;
@@ -204,8 +209,13 @@ __device__ __forceinline__ bool prep_record(const Grid& g, float u, float v, flo
     // Negative h narrows the chunk cull below the disc: decide every pair in fp64.
     P.band = (h < 0.0f || !__builtin_isfinite(band)) ? __builtin_inff() : band;
     P.hinv = 1.0f / h;
-    P.s0 = (float)ldexp(term_coef<KID>(a0, h), k0);
-    P.s1 = (float)ldexp(term_coef<KID>(a1, h), k1);
+    if constexpr (ACC == kAccFix) {
+        P.s0 = (float)ldexp(term_coef<KID>(a0, h), k0);
+        P.s1 = (float)ldexp(term_coef<KID>(a1, h), k1);
+    } else {
+        P.s0 = (float)term_coef<KID>(a0, h);
+        P.s1 = (float)term_coef<KID>(a1, h);
+    }
     return true;
 }
 
@@ -243,6 +253,33 @@ __device__ __forceinline__ unsigned long long f2fix(float f) {
     unsigned long long m =
         ((unsigned long long)(unsigned int)hi << 32) | (unsigned long long)(unsigned int)lo;
     return f < 0.0f ? 0ull - m : m;
+}
+
+// Add one term to an LDS tile accumulator word.
+template <int ACC>
+__device__ __forceinline__ void acc_add(unsigned long long* a, float t) {
+    if constexpr (ACC == kAccFix)
+        atomicAdd(a, f2fix(t));
+    else
+        atomicAdd((double*)a, (double)t);
+}
+
+// Accumulator word -> map value.
+template <int ACC>
+__device__ __forceinline__ float acc_value(unsigned long long s, int k) {
+    if constexpr (ACC == kAccFix)
+        return (float)ldexp((double)(long long)s, -k);
+    else
+        return (float)__longlong_as_double((long long)s);
+}
+
+template <int ACC>
+__device__ __forceinline__ unsigned long long acc_sum(unsigned long long a, unsigned long long b) {
+    if constexpr (ACC == kAccFix)
+        return a + b;
+    else
+        return (unsigned long long)__double_as_longlong(__longlong_as_double((long long)a) +
+                                                        __longlong_as_double((long long)b));
 }
 
 __device__ __forceinline__ float bcast(float x, int lane) {

@@ -241,20 +241,22 @@ __global__ __launch_bounds__(kScanThreads) void k_tilescan(const int* __restrict
 // {u, v, h, a0}, {a1, 0, 0, 0}.  Also the per-(block, tile) max |c| (fp32 bits) of the
 // records it inserted, the fixed-point bound of K3b.
 // ----------------------------------------------------------------------------------
-template <int KID, int NOUT>
+template <int KID, int NOUT, int ACC>
 __global__ __launch_bounds__(kCountBlock) void k_scatter(
     const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
     const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long per_block,
     Grid g, const int* __restrict__ hist, const long long* __restrict__ tile_start,
     float4* __restrict__ recs, unsigned* __restrict__ cmx, int* __restrict__ wide_list,
     int* __restrict__ ctr) {
-    extern __shared__ __attribute__((aligned(16))) int cur[];
-    unsigned* cm = (unsigned*)(cur + g.ntiles);  // [ntiles][NOUT]
+    extern __shared__ __attribute__((aligned(16))) int cur[];  // absolute record cursors
+    unsigned* cm = (unsigned*)(cur + g.ntiles);  // [ntiles][NOUT] (kAccFix only)
     const int* row = hist + (long long)blockIdx.x * g.ntiles;
     for (int t = threadIdx.x; t < g.ntiles; t += kCountBlock) {
-        cur[t] = row[t];
+        cur[t] = (int)tile_start[t] + row[t];  // n_recs < 2^31 (checked on the host)
+        if constexpr (ACC == kAccFix) {
 #pragma unroll
-        for (int o = 0; o < NOUT; ++o) cm[t * NOUT + o] = 0u;
+            for (int o = 0; o < NOUT; ++o) cm[t * NOUT + o] = 0u;
+        }
     }
     __syncthreads();
     long long p0 = (long long)blockIdx.x * per_block;
@@ -276,14 +278,19 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
             long long p = base + threadIdx.x + (long long)k * kCountBlock;
             Box b;
             if (!footprint(g, pu[k], pv[k], ph[k], b)) continue;
-            unsigned c0 = __float_as_uint(fabsf((float)term_coef<KID>(pa0[k], ph[k])));
-            unsigned c1 = NOUT == 2 ? __float_as_uint(fabsf((float)term_coef<KID>(pa1[k], ph[k]))) : 0u;
+            unsigned c0 = 0u, c1 = 0u;
+            if constexpr (ACC == kAccFix) {
+                c0 = __float_as_uint(fabsf((float)term_coef<KID>(pa0[k], ph[k])));
+                if (NOUT == 2) c1 = __float_as_uint(fabsf((float)term_coef<KID>(pa1[k], ph[k])));
+            }
             int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
             int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
             if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > kWideTiles) {
                 wide_list[atomicAdd(&ctr[cWideCursor], 1)] = (int)p;
-                atomicMax((unsigned*)&ctr[cWideMax0], c0);
-                if (NOUT == 2) atomicMax((unsigned*)&ctr[cWideMax1], c1);
+                if constexpr (ACC == kAccFix) {
+                    atomicMax((unsigned*)&ctr[cWideMax0], c0);
+                    if (NOUT == 2) atomicMax((unsigned*)&ctr[cWideMax1], c1);
+                }
                 continue;
             }
             float4 r0 = make_float4(pu[k], pv[k], ph[k], pa0[k]);
@@ -291,10 +298,12 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
             for (int tx = tx0; tx <= tx1; ++tx)
                 for (int ty = ty0; ty <= ty1; ++ty) {
                     int t = tx * g.nty + ty;
-                    long long slot = tile_start[t] + atomicAdd(&cur[t], 1);
-                    atomicMax(&cm[t * NOUT], c0);
+                    long long slot = (long long)atomicAdd(&cur[t], 1);
+                    if constexpr (ACC == kAccFix) {
+                        atomicMax(&cm[t * NOUT], c0);
+                        if (NOUT == 2) atomicMax(&cm[t * NOUT + 1], c1);
+                    }
                     if constexpr (NOUT == 2) {
-                        atomicMax(&cm[t * NOUT + 1], c1);
                         recs[2 * slot] = r0;
                         recs[2 * slot + 1] = r1;
                     } else {
@@ -303,9 +312,11 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
                 }
         }
     }
-    __syncthreads();
-    unsigned* out = cmx + (long long)blockIdx.x * g.ntiles * NOUT;
-    for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kCountBlock) out[t] = cm[t];
+    if constexpr (ACC == kAccFix) {
+        __syncthreads();
+        unsigned* out = cmx + (long long)blockIdx.x * g.ntiles * NOUT;
+        for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kCountBlock) out[t] = cm[t];
+    }
 }
 
 // Power-of-two scale exponent so that n * cmax * 2^k <= 2^kScaleBits.
@@ -354,18 +365,18 @@ __global__ __launch_bounds__(kBlock) void k_tilescale(const unsigned* __restrict
 // ----------------------------------------------------------------------------------
 // Pair accumulation into the LDS tile (int64 fixed point)
 // ----------------------------------------------------------------------------------
-template <int KID, int NOUT>
+template <int KID, int NOUT, int ACC>
 __device__ __forceinline__ void accumulate(const Prep& P, float r2, unsigned long long* acc0,
                                            unsigned long long* acc1, int k) {
     float q = __builtin_sqrtf(r2) * P.hinv;
     float w = kernel_shape<KID>(q);
-    atomicAdd(&acc0[k], f2fix(P.s0 * w));
-    if constexpr (NOUT == 2) atomicAdd(&acc1[k], f2fix(P.s1 * w));
+    acc_add<ACC>(&acc0[k], P.s0 * w);
+    if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k], P.s1 * w);
 }
 
 // One wave sweeps the (clipped) box of one wave-uniform record: lanes along y (the
 // contiguous image axis), so the LDS atomics of a wave hit distinct consecutive words.
-template <int KID, int NOUT>
+template <int KID, int NOUT, int ACC>
 __device__ __forceinline__ void sweep(const Grid& g, const Prep& P, int X0, int Y0,
                                       const float* xt, const float* yt,
                                       unsigned long long* acc0, unsigned long long* acc1,
@@ -380,7 +391,7 @@ __device__ __forceinline__ void sweep(const Grid& g, const Prep& P, int X0, int 
             for (int xi = P.b.x0 + r; xi <= P.b.x1; xi += rps) {
                 float r2;
                 if (decide(g, P, xi, yi, xt[xi - X0], Y, r2))
-                    accumulate<KID, NOUT>(P, r2, acc0, acc1, (xi - X0) * kTile + (yi - Y0));
+                    accumulate<KID, NOUT, ACC>(P, r2, acc0, acc1, (xi - X0) * kTile + (yi - Y0));
             }
         }
     } else {
@@ -390,7 +401,7 @@ __device__ __forceinline__ void sweep(const Grid& g, const Prep& P, int X0, int 
                 int yi = P.b.y0 + c;
                 float r2;
                 if (decide(g, P, xi, yi, X, yt[yi - Y0], r2))
-                    accumulate<KID, NOUT>(P, r2, acc0, acc1, (xi - X0) * kTile + (yi - Y0));
+                    accumulate<KID, NOUT, ACC>(P, r2, acc0, acc1, (xi - X0) * kTile + (yi - Y0));
             }
         }
     }
@@ -451,11 +462,12 @@ __device__ __forceinline__ void tile_prologue(const Grid& g, int X0, int Y0,
 }
 
 // Convert a pixel's fixed-point sums and write it (plain store: the tile has one owner).
-template <int NOUT>
-__device__ __forceinline__ void emit_pixel(long long o, long long s0, long long s1, int k0,
-                                           int k1, float* out0, float* out1, int flags) {
-    float v0 = (float)ldexp((double)s0, -k0);
-    float v1 = NOUT == 2 ? (float)ldexp((double)s1, -k1) : 0.0f;
+template <int NOUT, int ACC>
+__device__ __forceinline__ void emit_pixel(long long o, unsigned long long s0,
+                                           unsigned long long s1, int k0, int k1, float* out0,
+                                           float* out1, int flags) {
+    float v0 = acc_value<ACC>(s0, k0);
+    float v1 = NOUT == 2 ? acc_value<ACC>(s1, k1) : 0.0f;
     if (flags & kFlagAccumulate) {
         v0 += out0[o];
         if (NOUT == 2) v1 += out1[o];
@@ -472,7 +484,7 @@ __device__ __forceinline__ void emit_pixel(long long o, long long s0, long long 
 // K4: deposit one work item (a run of records of one tile) into LDS, then write the
 // tile (single-item tiles) or its int64 partial slab (split tiles).
 // ----------------------------------------------------------------------------------
-template <int KID, int NOUT>
+template <int KID, int NOUT, int ACC>
 __global__ __launch_bounds__(kDepBlock) void k_deposit(
     Grid g, const float4* __restrict__ recs, const Item* __restrict__ items,
     const int2* __restrict__ tile_k, unsigned long long* __restrict__ slabs,
@@ -498,7 +510,7 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
         return;
     }
     tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
-    const int2 kk = tile_k[it.tile];
+    const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
     int lane = threadIdx.x & 63;
     for (int base = 0; base < it.count; base += kDepBlock) {
         int i = base + threadIdx.x;
@@ -508,7 +520,7 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
         if (i < it.count) {
             float pu, pv, ph, pa0, pa1;
             load_rec<NOUT>(recs, it.start + i, pu, pv, ph, pa0, pa1);
-            live = prep_record<KID>(g, pu, pv, ph, pa0, pa1, kk.x, kk.y, P) &&
+            live = prep_record<KID, ACC>(g, pu, pv, ph, pa0, pa1, kk.x, kk.y, P) &&
                    clip(P.b, X0, Y0, TW, TH);
         }
         int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
@@ -538,7 +550,7 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
                             if (fabsf(r2 - P.thr) <= P.band)
                                 in = exact_pair(g, P.u, P.v, P.h, xi, yc[j]);
                             if (in)
-                                accumulate<KID, NOUT>(P, r2, acc0, acc1,
+                                accumulate<KID, NOUT, ACC>(P, r2, acc0, acc1,
                                                       (xi - X0) * kTile + (yc[j] - Y0));
                         }
                     }
@@ -550,7 +562,7 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
             int l = __builtin_ctzll(big);
             big &= big - 1;
             Prep Q = bcast_prep(P, l);
-            sweep<KID, NOUT>(g, Q, X0, Y0, xt, yt, acc0, acc1, lane);
+            sweep<KID, NOUT, ACC>(g, Q, X0, Y0, xt, yt, acc0, acc1, lane);
         }
     }
     __syncthreads();
@@ -563,15 +575,15 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
         int lx = k >> kTileShift, ly = k & (kTile - 1);
         if (lx >= TW || ly >= TH) continue;
         long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
-        emit_pixel<NOUT>(o, (long long)acc0[k], NOUT == 2 ? (long long)acc1[k] : 0, kk.x, kk.y,
-                         out0, out1, flags);
+        emit_pixel<NOUT, ACC>(o, acc0[k], NOUT == 2 ? acc1[k] : 0ull, kk.x, kk.y, out0, out1,
+                              flags);
     }
 }
 
 // ----------------------------------------------------------------------------------
 // K5: split tiles -- exact int64 sum of the item slabs, convert, write.
 // ----------------------------------------------------------------------------------
-template <int NOUT>
+template <int NOUT, int ACC>
 __global__ __launch_bounds__(kBlock) void k_merge(Grid g, const Merge* __restrict__ merges,
                                                   const unsigned long long* __restrict__ slabs,
                                                   const int2* __restrict__ tile_k,
@@ -581,18 +593,18 @@ __global__ __launch_bounds__(kBlock) void k_merge(Grid g, const Merge* __restric
     int tx = m.tile / g.nty, ty = m.tile - (m.tile / g.nty) * g.nty;
     int X0 = tx * kTile, Y0 = ty * kTile;
     int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
-    const int2 kk = tile_k[m.tile];
+    const int2 kk = ACC == kAccFix ? tile_k[m.tile] : make_int2(0, 0);
     for (int k = threadIdx.x; k < kTilePix; k += kBlock) {
         int lx = k >> kTileShift, ly = k & (kTile - 1);
         if (lx >= TW || ly >= TH) continue;
-        unsigned long long s0 = 0, s1 = 0;
-        for (int j = 0; j < m.nslab; ++j) {
+        unsigned long long s0 = 0, s1 = 0;  // +0.0 in fp64 as well
+        for (int j = 0; j < m.nslab; ++j) {  // fixed slab order: deterministic
             const unsigned long long* src = slabs + (long long)(m.slab0 + j) * NOUT * kTilePix;
-            s0 += src[k];
-            if (NOUT == 2) s1 += src[kTilePix + k];
+            s0 = acc_sum<ACC>(s0, src[k]);
+            if (NOUT == 2) s1 = acc_sum<ACC>(s1, src[kTilePix + k]);
         }
         long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
-        emit_pixel<NOUT>(o, (long long)s0, (long long)s1, kk.x, kk.y, out0, out1, flags);
+        emit_pixel<NOUT, ACC>(o, s0, s1, kk.x, kk.y, out0, out1, flags);
     }
 }
 
@@ -601,7 +613,7 @@ __global__ __launch_bounds__(kBlock) void k_merge(Grid g, const Merge* __restric
 // wave takes every 4th wide particle and sweeps its clipped box; fixed point with the
 // wide particles' own bound, added onto the tile (this workgroup is its only writer).
 // ----------------------------------------------------------------------------------
-template <int KID, int NOUT>
+template <int KID, int NOUT, int ACC>
 __global__ __launch_bounds__(kBlock) void k_wide(Grid g, const float* __restrict__ u,
                                                  const float* __restrict__ v,
                                                  const float* __restrict__ h,
@@ -623,17 +635,19 @@ __global__ __launch_bounds__(kBlock) void k_wide(Grid g, const float* __restrict
     int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
     if (threadIdx.x == 0) *any = 0;
     tile_prologue<NOUT, kBlock>(g, X0, Y0, acc, xt, yt);
-    int k0 = scale_exp(n_wide, __uint_as_float((unsigned)ctr[cWideMax0]));
-    int k1 = NOUT == 2 ? scale_exp(n_wide, __uint_as_float((unsigned)ctr[cWideMax1])) : 0;
+    int k0 = ACC == kAccFix ? scale_exp(n_wide, __uint_as_float((unsigned)ctr[cWideMax0])) : 0;
+    int k1 = (ACC == kAccFix && NOUT == 2)
+                 ? scale_exp(n_wide, __uint_as_float((unsigned)ctr[cWideMax1])) : 0;
     int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int k = wv; k < n_wide; k += kBlock / 64) {
         int p = wide_list[k];
         Prep P;
-        if (!prep_record<KID>(g, u[p], v[p], h[p], a0[p], NOUT == 2 ? a1[p] : 0.0f, k0, k1, P))
+        if (!prep_record<KID, ACC>(g, u[p], v[p], h[p], a0[p], NOUT == 2 ? a1[p] : 0.0f, k0, k1,
+                                   P))
             continue;
         if (!clip(P.b, X0, Y0, TW, TH)) continue;
         if (lane == 0) *any = 1;
-        sweep<KID, NOUT>(g, P, X0, Y0, xt, yt, acc0, acc1, lane);
+        sweep<KID, NOUT, ACC>(g, P, X0, Y0, xt, yt, acc0, acc1, lane);
     }
     __syncthreads();
     if (!*any) return;
@@ -641,8 +655,8 @@ __global__ __launch_bounds__(kBlock) void k_wide(Grid g, const float* __restrict
         int lx = k >> kTileShift, ly = k & (kTile - 1);
         if (lx >= TW || ly >= TH) continue;
         long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
-        emit_pixel<NOUT>(o, (long long)acc0[k], NOUT == 2 ? (long long)acc1[k] : 0, k0, k1,
-                         out0, out1, kFlagAccumulate);
+        emit_pixel<NOUT, ACC>(o, acc0[k], NOUT == 2 ? acc1[k] : 0ull, k0, k1, out0, out1,
+                              kFlagAccumulate);
     }
 }
 
@@ -926,7 +940,7 @@ struct Plan {
 };
 
 // K3..K7 for one kernel / map count.
-template <int KID, int NOUT>
+template <int KID, int NOUT, int ACC>
 static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u,
                     const float* v, const float* h, const float* a0, const float* a1, float* o0,
                     float* o1, int flags, hipStream_t st) {
@@ -936,15 +950,15 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     int dflags = ((flags & ASP_F_ACCUMULATE) ? kFlagAccumulate : 0) | (fuse_ratio ? kFlagRatio : 0);
     {
         StageMark m(ws, kSScatter, st);
-        size_t lds = (size_t)g.ntiles * (1 + NOUT) * sizeof(int);
-        hipLaunchKernelGGL((k_scatter<KID, NOUT>), dim3((unsigned)pl.nblk), dim3(kCountBlock),
+        size_t lds = (size_t)g.ntiles * (1 + (ACC == kAccFix ? NOUT : 0)) * sizeof(int);
+        hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC>), dim3((unsigned)pl.nblk), dim3(kCountBlock),
                            lds, st, u, v, h, a0, a1, pl.n, pl.per_block, g, (const int*)ws.hist.p,
                            (const long long*)ws.tile_start.p, (float4*)ws.recs.p,
                            (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc);
         ASP_LAUNCHED();
         m.done();
     }
-    {
+    if (ACC == kAccFix) {
         StageMark m(ws, kSScale, st);
         hipLaunchKernelGGL((k_tilescale<NOUT>), dim3((g.ntiles + 63) / 64), dim3(kBlock), 0, st,
                            (const unsigned*)ws.cmx.p, (int)pl.nblk, g.ntiles,
@@ -955,7 +969,7 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     {
         StageMark m(ws, kSDeposit, st);
         size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4;
-        hipLaunchKernelGGL((k_deposit<KID, NOUT>), dim3(pl.n_items), dim3(kDepBlock), lds, st, g,
+        hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(pl.n_items), dim3(kDepBlock), lds, st, g,
                            (const float4*)ws.recs.p, (const Item*)ws.items.p,
                            (const int2*)ws.tile_k.p, (unsigned long long*)ws.slabs.p, o0, o1,
                            dflags);
@@ -964,7 +978,7 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     }
     if (pl.n_merges > 0) {
         StageMark m(ws, kSMerge, st);
-        hipLaunchKernelGGL((k_merge<NOUT>), dim3(pl.n_merges), dim3(kBlock), 0, st, g,
+        hipLaunchKernelGGL((k_merge<NOUT, ACC>), dim3(pl.n_merges), dim3(kBlock), 0, st, g,
                            (const Merge*)ws.merges.p, (const unsigned long long*)ws.slabs.p,
                            (const int2*)ws.tile_k.p, o0, o1, dflags);
         ASP_LAUNCHED();
@@ -973,7 +987,7 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     if (pl.n_wide > 0) {
         StageMark m(ws, kSWide, st);
         size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4 + 16;
-        hipLaunchKernelGGL((k_wide<KID, NOUT>), dim3(g.ntiles), dim3(kBlock), lds, st, g, u, v, h,
+        hipLaunchKernelGGL((k_wide<KID, NOUT, ACC>), dim3(g.ntiles), dim3(kBlock), lds, st, g, u, v, h,
                            a0, a1, (const int*)ws.wide.p, pl.n_wide, (const int*)dc, o0, o1);
         ASP_LAUNCHED();
         m.done();
@@ -1070,7 +1084,8 @@ static int project2d(const float* u, const float* v, const float* h, const float
         pl.per_block = (n + pl.nblk - 1) / pl.nblk;
         pl.nblk = (n + pl.per_block - 1) / pl.per_block;
         ASP_TRY(ensure(ws.hist, (size_t)pl.nblk * g.ntiles * sizeof(int)));
-        ASP_TRY(ensure(ws.cmx, (size_t)pl.nblk * g.ntiles * nout * sizeof(unsigned)));
+        const bool det = (flags & ASP_F_DETERMINISTIC) != 0;
+        if (det) ASP_TRY(ensure(ws.cmx, (size_t)pl.nblk * g.ntiles * nout * sizeof(unsigned)));
         ASP_TRY(ensure(ws.tile_total, (size_t)g.ntiles * sizeof(int)));
         ASP_TRY(ensure(ws.tile_start, (size_t)g.ntiles * sizeof(long long)));
         ASP_TRY(ensure(ws.tile_k, (size_t)g.ntiles * sizeof(int2)));
@@ -1118,14 +1133,13 @@ static int project2d(const float* u, const float* v, const float* h, const float
         ASP_TRY(ensure(ws.wide, (size_t)pl.n_wide * sizeof(int)));
         ASP_TRY(ensure(ws.slabs, (size_t)pl.n_slabs * nout * kTilePix * sizeof(long long)));
         int rc;
-#define ASP_TAIL(K, N) \
-    run_tail<K, N>(g, ws, pl, du, dv, dh, da0, da1, d0, d1, flags, st)
-        if (kid == 0)
-            rc = nout == 1 ? ASP_TAIL(0, 1) : ASP_TAIL(0, 2);
-        else if (kid == 1)
-            rc = nout == 1 ? ASP_TAIL(1, 1) : ASP_TAIL(1, 2);
-        else
-            rc = nout == 1 ? ASP_TAIL(2, 1) : ASP_TAIL(2, 2);
+#define ASP_TAIL(K, N, A) \
+    run_tail<K, N, A>(g, ws, pl, du, dv, dh, da0, da1, d0, d1, flags, st)
+#define ASP_TAIL2(K, A) (nout == 1 ? ASP_TAIL(K, 1, A) : ASP_TAIL(K, 2, A))
+#define ASP_TAIL3(A) (kid == 0 ? ASP_TAIL2(0, A) : kid == 1 ? ASP_TAIL2(1, A) : ASP_TAIL2(2, A))
+        rc = det ? ASP_TAIL3(kAccFix) : ASP_TAIL3(kAccF64);
+#undef ASP_TAIL3
+#undef ASP_TAIL2
 #undef ASP_TAIL
         if (rc != ASP_OK) return rc;
     }

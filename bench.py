@@ -45,6 +45,8 @@ def parse():
                     help="budget for the bounded CPU-baseline sample")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_latest.json"),
                     help="PMC summary (tools/pmc_summary.py) for roofline.traffic")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="int64 fixed-point accumulation (bitwise reproducible maps)")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args()
 
@@ -138,9 +140,9 @@ def main():
         if world > 1:
             return project2d_sharded(u, v, h, a0, a1, image_size=(G, G), extent=ext,
                                      kernel=args.kernel, ratio=ratio, op=args.op, out0=out0,
-                                     out1=out1)
+                                     out1=out1, deterministic=args.deterministic)
         return project2d(u, v, h, a0, a1, image_size=(G, G), extent=ext, kernel=args.kernel,
-                         ratio=ratio, out0=out0, out1=out1)
+                         ratio=ratio, out0=out0, out1=out1, deterministic=args.deterministic)
 
     for _ in range(args.warmup):
         step()
@@ -202,7 +204,8 @@ def main():
                                f"map, {args.kernel}, {args.h_law}-scale h, fp32"
                                + (f", Z-slab x{world} + RCCL {args.op}" if world > 1 else ""),
                    "particles": args.n, "grid": G, "kernel": args.kernel, "h_law": args.h_law,
-                   "map": args.map, "parallelism": f"zslab{world}" if world > 1 else "single"},
+                   "map": args.map, "parallelism": f"zslab{world}" if world > 1 else "single",
+                   "accumulation": "int64 fixed point" if args.deterministic else "fp64"},
         "particles_per_s": pps,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

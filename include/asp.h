@@ -43,6 +43,10 @@ extern "C" {
 #define ASP_F_DEVICE_PTRS 0x1 /* inputs/outputs are device pointers on `device`            */
 #define ASP_F_RATIO 0x2       /* two outputs: out0 <- out0 / out1 (0 where out1 == 0)      */
 #define ASP_F_ACCUMULATE 0x4  /* add into out0/out1 instead of overwriting                 */
+#define ASP_F_DETERMINISTIC 0x8 /* int64 fixed-point accumulation: bitwise reproducible and
+                                 * input-order independent maps; relative precision degrades
+                                 * for pixels below ~2^-37 n_t max|A W| of their 64x64 tile
+                                 * (DESIGN.md §4).  Default: fp64 accumulation.            */
 
 /* errors */
 #define ASP_OK 0

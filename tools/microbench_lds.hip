@@ -21,19 +21,21 @@ __global__ __launch_bounds__(256) void k(float* out, int span) {
     __syncthreads();
     uint32_t s = hash(blockIdx.x * 256 + threadIdx.x);
     float val = 1.0f + (threadIdx.x & 7);
+    unsigned mask = (unsigned)span - 1u;  // span is a power of two
     for (int it = 0; it < ITERS; ++it) {
-        s = hash(s + it);
-        int a = (int)(s % (uint32_t)span);
+        s = s * 1664525u + 1013904223u;   // LCG: 2 VALU ops
+        int a = (int)((s >> 7) & mask);
         if constexpr (MODE == 0) atomicAdd(&lds[a], val);                      // ds_add_f32
         else if constexpr (MODE == 1) atomicAdd((unsigned*)&lds[a], (unsigned)val);  // ds_add_u32
         else if constexpr (MODE == 2) lds[a] = val;                            // ds_write_b32
         else if constexpr (MODE == 3) atomicAdd(&lds64[a >> 1], (unsigned long long)val);  // ds_add_u64
         else if constexpr (MODE == 4) { float t = lds[a]; lds[a] = t + val; }  // racy RMW
-        else if constexpr (MODE == 5) {  // contiguous per wave (lanes consecutive)
-            int b = ((s >> 6) % (uint32_t)(span / 64)) * 64 + (threadIdx.x & 63);
-            b = __builtin_amdgcn_readfirstlane(b - (threadIdx.x & 63)) + (threadIdx.x & 63);
-            atomicAdd(&lds[b], val);
+        else if constexpr (MODE == 5) {  // ds_add_rtn_u32 (cursor-style, result used)
+            unsigned r = atomicAdd((unsigned*)&lds[a], 1u);
+            val += (float)(r & 1u);
         }
+        else if constexpr (MODE == 6) atomicAdd((double*)&lds64[a >> 1], (double)val);  // ds_add_f64
+        else if constexpr (MODE == 7) atomicMax((unsigned*)&lds[a], (unsigned)val);    // ds_max_u32
     }
     __syncthreads();
     float acc = 0.f;
@@ -57,13 +59,15 @@ float run(float* d, int blocks, int span) {
 int main() {
     int blocks = 256 * 8;
     float* d; hipMalloc(&d, blocks * 256 * sizeof(float));
-    const char* names[] = {"ds_add_f32", "ds_add_u32", "ds_write_b32", "ds_add_u64", "racy_rmw", "ds_add_f32 contiguous"};
-    for (int span : {8192, 4096, 256}) {
-        float t[6];
+    const char* names[] = {"ds_add_f32", "ds_add_u32", "ds_write_b32", "ds_add_u64", "racy_rmw",
+                           "ds_add_rtn_u32", "ds_add_f64", "ds_max_u32"};
+    for (int span : {8192, 256}) {
+        float t[8];
         t[0] = run<0>(d, blocks, span); t[1] = run<1>(d, blocks, span); t[2] = run<2>(d, blocks, span);
         t[3] = run<3>(d, blocks, span); t[4] = run<4>(d, blocks, span); t[5] = run<5>(d, blocks, span);
+        t[6] = run<6>(d, blocks, span); t[7] = run<7>(d, blocks, span);
         double ops = (double)blocks * 256 * ITERS;
-        for (int m = 0; m < 6; ++m)
+        for (int m = 0; m < 8; ++m)
             printf("span %5d %-24s %8.3f ms  %7.2f G lane-ops/s  %6.2f lane-ops/clk/CU@2.4GHz\n", span, names[m], t[m],
                    ops / t[m] / 1e6, ops / (t[m] * 1e-3) / 256 / 2.4e9);
     }

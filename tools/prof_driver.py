@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--kernel", default="wendland_c2")
     ap.add_argument("--map", default="weighted")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--deterministic", action="store_true")
     a = ap.parse_args()
     import torch
     from asp_amd.device import project2d, stats
@@ -35,7 +36,7 @@ def main():
     out1 = torch.empty((G, G), device="cuda:0") if a1 is not None else None
     for _ in range(a.iters):
         project2d(u, v, h, a0, a1, image_size=(G, G), extent=(-4, 4, -4, 4), kernel=a.kernel,
-                  ratio=a1 is not None, out0=out0, out1=out1)
+                  ratio=a1 is not None, out0=out0, out1=out1, deterministic=a.deterministic)
     torch.cuda.synchronize()
     print("stats", stats(0), file=sys.stderr)
 
