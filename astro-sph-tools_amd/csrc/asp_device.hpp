@@ -177,18 +177,20 @@ __device__ __forceinline__ double term_coef(float a, float h) {
 }
 
 // Kernel shape f(q), W = norm(h) * f(q); max f = f(0) = 1 for all three kernels.
+// Explicit FMAs: the value path is held to the fp32 tolerance, not to bit-exactness
+// (only the neighbour decision is, and it never reaches here).
 template <int KID>
 __device__ __forceinline__ float kernel_shape(float q) {
     if constexpr (KID == 0) {  // M4 cubic spline (_kernels.pyx:14-19)
         float q2 = q * q;
-        float a = 1.0f - 1.5f * q2 + 0.75f * (q2 * q);
+        float a = fmaf(q2, fmaf(0.75f, q, -1.5f), 1.0f);  // 1 - 1.5 q^2 + 0.75 q^3
         float t = 2.0f - q;
         float b = 0.25f * (t * t * t);
         return q < 1.0f ? a : (q < 2.0f ? b : 0.0f);
     } else if constexpr (KID == 1) {  // Wendland C2, support 2h
-        float t = fmaxf(1.0f - 0.5f * q, 0.0f);
+        float t = fmaxf(fmaf(-0.5f, q, 1.0f), 0.0f);
         float t2 = t * t;
-        return (t2 * t2) * (1.0f + 2.0f * q);
+        return (t2 * t2) * fmaf(2.0f, q, 1.0f);
     } else {
         return 1.0f;
     }

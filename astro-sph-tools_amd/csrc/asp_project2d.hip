@@ -57,6 +57,22 @@ enum Ctr {
 constexpr int kCountBlock = 512;  // count / scatter workgroup
 constexpr int kUnroll = 2;        // particles in flight per thread in count / scatter
 
+// Load kUnroll particles (lane-strided by the block size); h = 0 past the end, which has
+// no footprint.
+__device__ __forceinline__ void load_batch(const float* __restrict__ u,
+                                           const float* __restrict__ v,
+                                           const float* __restrict__ h, long long base,
+                                           long long p1, float* pu, float* pv, float* ph) {
+#pragma unroll
+    for (int k = 0; k < kUnroll; ++k) {
+        long long p = base + threadIdx.x + (long long)k * kCountBlock;
+        bool in = p < p1;
+        pu[k] = in ? u[p] : 0.0f;
+        pv[k] = in ? v[p] : 0.0f;
+        ph[k] = in ? h[p] : 0.0f;
+    }
+}
+
 // ----------------------------------------------------------------------------------
 // K1: count insertions per (block, tile)
 // ----------------------------------------------------------------------------------
@@ -72,16 +88,13 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
     long long p0 = (long long)blockIdx.x * per_block;
     long long p1 = min(n, p0 + per_block);
     int nwide = 0;
-    for (long long base = p0; base < p1; base += (long long)kCountBlock * kUnroll) {
-        float pu[kUnroll], pv[kUnroll], ph[kUnroll];
-#pragma unroll
-        for (int k = 0; k < kUnroll; ++k) {
-            long long p = base + threadIdx.x + (long long)k * kCountBlock;
-            bool in = p < p1;
-            pu[k] = in ? u[p] : 0.0f;
-            pv[k] = in ? v[p] : 0.0f;
-            ph[k] = in ? h[p] : 0.0f;  // h = 0: no footprint
-        }
+    constexpr long long kStep = (long long)kCountBlock * kUnroll;
+    // Software pipeline: the next batch's loads are in flight while this batch is binned.
+    float pu[kUnroll], pv[kUnroll], ph[kUnroll];
+    load_batch(u, v, h, p0, p1, pu, pv, ph);
+    for (long long base = p0; base < p1; base += kStep) {
+        float nu[kUnroll], nv[kUnroll], nh[kUnroll];
+        load_batch(u, v, h, base + kStep, p1, nu, nv, nh);
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
             Box b;
@@ -94,6 +107,12 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
             }
             for (int tx = tx0; tx <= tx1; ++tx)
                 for (int ty = ty0; ty <= ty1; ++ty) atomicAdd(&lh[tx * g.nty + ty], 1);
+        }
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k) {
+            pu[k] = nu[k];
+            pv[k] = nv[k];
+            ph[k] = nh[k];
         }
     }
     if (nwide) atomicAdd(&ctr[cWideCount], nwide);
@@ -235,6 +254,19 @@ __global__ __launch_bounds__(kScanThreads) void k_tilescan(const int* __restrict
     }
 }
 
+template <int NOUT>
+__device__ __forceinline__ void load_props(const float* __restrict__ a0,
+                                           const float* __restrict__ a1, long long base,
+                                           long long p1, float* pa0, float* pa1) {
+#pragma unroll
+    for (int k = 0; k < kUnroll; ++k) {
+        long long p = base + threadIdx.x + (long long)k * kCountBlock;
+        bool in = p < p1;
+        pa0[k] = in ? a0[p] : 0.0f;
+        pa1[k] = (in && NOUT == 2) ? a1[p] : 0.0f;
+    }
+}
+
 // ----------------------------------------------------------------------------------
 // K3: scatter records into their tiles' runs.  Same particle partition as K1.
 // Record layout: NOUT == 1 -> float4 {u, v, h, a0};  NOUT == 2 -> 2 x float4
@@ -249,7 +281,9 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
     float4* __restrict__ recs, unsigned* __restrict__ cmx, int* __restrict__ wide_list,
     int* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) int cur[];  // absolute record cursors
-    unsigned* cm = (unsigned*)(cur + g.ntiles);  // [ntiles][NOUT] (kAccFix only)
+    // per-wave staging for the paired record stores (NOUT == 2): 64 records x 32 B
+    float4* stage = (float4*)(cur + ((g.ntiles + 3) & ~3));
+    unsigned* cm = (unsigned*)(stage + (NOUT == 2 ? (kCountBlock / 64) * 128 : 0));
     const int* row = hist + (long long)blockIdx.x * g.ntiles;
     for (int t = threadIdx.x; t < g.ntiles; t += kCountBlock) {
         cur[t] = (int)tile_start[t] + row[t];  // n_recs < 2^31 (checked on the host)
@@ -261,18 +295,20 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
     __syncthreads();
     long long p0 = (long long)blockIdx.x * per_block;
     long long p1 = min(n, p0 + per_block);
-    for (long long base = p0; base < p1; base += (long long)kCountBlock * kUnroll) {
-        float pu[kUnroll], pv[kUnroll], ph[kUnroll], pa0[kUnroll], pa1[kUnroll];
+    constexpr long long kStep = (long long)kCountBlock * kUnroll;
+    // Software pipeline: issue the next batch's loads BEFORE this batch's record stores,
+    // so waiting for them (vmcnt counts loads and stores in issue order) never waits on
+    // the scattered stores.
+    float pu[kUnroll], pv[kUnroll], ph[kUnroll], pa0[kUnroll], pa1[kUnroll];
+    int first_slot[kUnroll];
 #pragma unroll
-        for (int k = 0; k < kUnroll; ++k) {
-            long long p = base + threadIdx.x + (long long)k * kCountBlock;
-            bool in = p < p1;
-            pu[k] = in ? u[p] : 0.0f;
-            pv[k] = in ? v[p] : 0.0f;
-            ph[k] = in ? h[p] : 0.0f;
-            pa0[k] = in ? a0[p] : 0.0f;
-            pa1[k] = (in && NOUT == 2) ? a1[p] : 0.0f;
-        }
+    for (int k = 0; k < kUnroll; ++k) first_slot[k] = -1;
+    load_batch(u, v, h, p0, p1, pu, pv, ph);
+    load_props<NOUT>(a0, a1, p0, p1, pa0, pa1);
+    for (long long base = p0; base < p1; base += kStep) {
+        float nu[kUnroll], nv[kUnroll], nh[kUnroll], na0[kUnroll], na1[kUnroll];
+        load_batch(u, v, h, base + kStep, p1, nu, nv, nh);
+        load_props<NOUT>(a0, a1, base + kStep, p1, na0, na1);
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
             long long p = base + threadIdx.x + (long long)k * kCountBlock;
@@ -298,18 +334,54 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
             for (int tx = tx0; tx <= tx1; ++tx)
                 for (int ty = ty0; ty <= ty1; ++ty) {
                     int t = tx * g.nty + ty;
-                    long long slot = (long long)atomicAdd(&cur[t], 1);
+                    int slot = atomicAdd(&cur[t], 1);
                     if constexpr (ACC == kAccFix) {
                         atomicMax(&cm[t * NOUT], c0);
                         if (NOUT == 2) atomicMax(&cm[t * NOUT + 1], c1);
                     }
                     if constexpr (NOUT == 2) {
-                        recs[2 * slot] = r0;
-                        recs[2 * slot + 1] = r1;
+                        if (tx == tx0 && ty == ty0) {
+                            first_slot[k] = slot;  // written by the paired store below
+                        } else {
+                            recs[2 * (long long)slot] = r0;
+                            recs[2 * (long long)slot + 1] = r1;
+                        }
                     } else {
                         recs[slot] = r0;
                     }
                 }
+        }
+        if constexpr (NOUT == 2) {
+            // Paired store of every particle's first record: lanes 2j and 2j+1 write the
+            // two 16-B halves of record j, so one store instruction covers 32 whole
+            // 32-B records (32 lines) instead of 64 half records (64 lines).
+            float4* st = stage + (threadIdx.x >> 6) * 128;
+            int lane = threadIdx.x & 63;
+#pragma unroll
+            for (int k = 0; k < kUnroll; ++k) {
+                st[2 * lane] = make_float4(pu[k], pv[k], ph[k], pa0[k]);
+                st[2 * lane + 1] = make_float4(pa1[k], 0.0f, 0.0f, 0.0f);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int half = 0; half < 2; ++half) {
+                    int src = half * 32 + (lane >> 1);
+                    int slot = __shfl(first_slot[k], src);
+                    float4 val = st[2 * src + (lane & 1)];
+                    if (slot >= 0) recs[2 * (long long)slot + (lane & 1)] = val;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                first_slot[k] = -1;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k) {
+            pu[k] = nu[k];
+            pv[k] = nv[k];
+            ph[k] = nh[k];
+            pa0[k] = na0[k];
+            pa1[k] = na1[k];
         }
     }
     if constexpr (ACC == kAccFix) {
@@ -365,13 +437,23 @@ __global__ __launch_bounds__(kBlock) void k_tilescale(const unsigned* __restrict
 // ----------------------------------------------------------------------------------
 // Pair accumulation into the LDS tile (int64 fixed point)
 // ----------------------------------------------------------------------------------
+#ifndef ASP_ABLATE
+#define ASP_ABLATE 0  // diagnostic builds only (tools/ablate.sh): 1 = no LDS atomics,
+                      // 2 = no pair loop, 3 = no record prep
+#endif
+
 template <int KID, int NOUT, int ACC>
 __device__ __forceinline__ void accumulate(const Prep& P, float r2, unsigned long long* acc0,
                                            unsigned long long* acc1, int k) {
-    float q = __builtin_sqrtf(r2) * P.hinv;
+    float q = __builtin_amdgcn_sqrtf(r2) * P.hinv;  // v_sqrt_f32, 1 ulp
     float w = kernel_shape<KID>(q);
+#if ASP_ABLATE == 1
+    float t0 = P.s0 * w, t1 = P.s1 * w;
+    asm volatile("" ::"v"(t0), "v"(t1), "v"(k));
+#else
     acc_add<ACC>(&acc0[k], P.s0 * w);
     if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k], P.s1 * w);
+#endif
 }
 
 // One wave sweeps the (clipped) box of one wave-uniform record: lanes along y (the
@@ -445,6 +527,17 @@ __device__ __forceinline__ void load_rec(const float4* recs, long long i, float&
     }
 }
 
+template <int NOUT>
+__device__ __forceinline__ void load_rec4(const float4* recs, long long i, float4& r0,
+                                          float4& r1) {
+    if constexpr (NOUT == 1) {
+        r0 = recs[i];
+    } else {
+        r0 = recs[2 * i];
+        r1 = recs[2 * i + 1];
+    }
+}
+
 constexpr int kTilePix = kTile * kTile;
 constexpr int kFlagAccumulate = 1;
 constexpr int kFlagRatio = 2;  // fused ratio: out0 <- map0 / map1
@@ -512,17 +605,32 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
     tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
     const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
     int lane = threadIdx.x & 63;
+    // Software pipeline: the next batch's records load while this batch deposits.
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
+    if ((int)threadIdx.x < it.count) load_rec4<NOUT>(recs, it.start + threadIdx.x, r0, r1);
     for (int base = 0; base < it.count; base += kDepBlock) {
         int i = base + threadIdx.x;
+        float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0;
+        if (i + kDepBlock < it.count) load_rec4<NOUT>(recs, it.start + i + kDepBlock, n0, n1);
         Prep P;
         P.b = Box{0, -1, 0, -1};
         bool live = false;
-        if (i < it.count) {
-            float pu, pv, ph, pa0, pa1;
-            load_rec<NOUT>(recs, it.start + i, pu, pv, ph, pa0, pa1);
-            live = prep_record<KID, ACC>(g, pu, pv, ph, pa0, pa1, kk.x, kk.y, P) &&
+#if ASP_ABLATE == 3
+        asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x));
+        r0 = n0;
+        r1 = n1;
+        continue;
+#endif
+        if (i < it.count)
+            live = prep_record<KID, ACC>(g, r0.x, r0.y, r0.z, r0.w, r1.x, kk.x, kk.y, P) &&
                    clip(P.b, X0, Y0, TW, TH);
-        }
+        r0 = n0;
+        r1 = n1;
+#if ASP_ABLATE == 2
+        asm volatile("" ::"v"(P.u), "v"(P.v), "v"(P.thr), "v"(P.band), "v"(P.s0), "v"(P.s1),
+                     "v"(P.b.x0), "v"(P.b.y1), "v"(live ? 1 : 0));
+        continue;
+#endif
         int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
         bool small = live && bw <= 4 && bh <= 4;
         if (small) {
@@ -536,6 +644,10 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
                 float dy = P.v - yt[yi - Y0];
                 dy2[j] = dy * dy;
             }
+            // Unrolled 4x4 pass decides every pair whose fp32 r2 is outside the error band
+            // and accumulates it; band pairs (~0.1 %) only set a bit, resolved below in
+            // fp64 -- keeping the rare slow path out of the unrolled body.
+            unsigned amb = 0u;
 #pragma unroll
             for (int ii = 0; ii < 4; ++ii) {
                 if (ii < bw) {
@@ -547,13 +659,23 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
                         if (j < bh) {
                             float r2 = dx2 + dy2[j];
                             bool in = r2 < P.thr;
-                            if (fabsf(r2 - P.thr) <= P.band)
-                                in = exact_pair(g, P.u, P.v, P.h, xi, yc[j]);
-                            if (in)
+                            bool a = fabsf(r2 - P.thr) <= P.band;
+                            amb |= a ? (1u << (ii * 4 + j)) : 0u;
+                            if (in && !a)
                                 accumulate<KID, NOUT, ACC>(P, r2, acc0, acc1,
-                                                      (xi - X0) * kTile + (yc[j] - Y0));
+                                                           (xi - X0) * kTile + (yc[j] - Y0));
                         }
                     }
+                }
+            }
+            while (amb) {
+                int bit = __builtin_ctz(amb);
+                amb &= amb - 1u;
+                int xi = P.b.x0 + (bit >> 2), yi = yc[bit & 3];
+                if (exact_pair(g, P.u, P.v, P.h, xi, yi)) {
+                    float dx = P.u - xt[xi - X0], dy = P.v - yt[yi - Y0];
+                    accumulate<KID, NOUT, ACC>(P, dx * dx + dy * dy, acc0, acc1,
+                                               (xi - X0) * kTile + (yi - Y0));
                 }
             }
         }
@@ -950,7 +1072,9 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     int dflags = ((flags & ASP_F_ACCUMULATE) ? kFlagAccumulate : 0) | (fuse_ratio ? kFlagRatio : 0);
     {
         StageMark m(ws, kSScatter, st);
-        size_t lds = (size_t)g.ntiles * (1 + (ACC == kAccFix ? NOUT : 0)) * sizeof(int);
+        size_t lds = (size_t)((g.ntiles + 3) & ~3) * sizeof(int) +
+                     (NOUT == 2 ? (size_t)(kCountBlock / 64) * 128 * sizeof(float4) : 0) +
+                     (ACC == kAccFix ? (size_t)g.ntiles * NOUT * sizeof(unsigned) : 0);
         hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC>), dim3((unsigned)pl.nblk), dim3(kCountBlock),
                            lds, st, u, v, h, a0, a1, pl.n, pl.per_block, g, (const int*)ws.hist.p,
                            (const long long*)ws.tile_start.p, (float4*)ws.recs.p,
