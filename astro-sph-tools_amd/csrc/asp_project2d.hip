@@ -605,27 +605,32 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
     tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
     const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
     int lane = threadIdx.x & 63;
-    // Software pipeline: the next batch's records load while this batch deposits.
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
+    // Software pipeline, two batches deep: batches i+1 and i+2 load while batch i deposits
+    // (16 waves/CU x 64 lanes x 32 B x 2 in flight per CU).
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, q0 = r0, q1 = r0;
     if ((int)threadIdx.x < it.count) load_rec4<NOUT>(recs, it.start + threadIdx.x, r0, r1);
+    if ((int)threadIdx.x + kDepBlock < it.count)
+        load_rec4<NOUT>(recs, it.start + threadIdx.x + kDepBlock, q0, q1);
     for (int base = 0; base < it.count; base += kDepBlock) {
         int i = base + threadIdx.x;
         float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0;
-        if (i + kDepBlock < it.count) load_rec4<NOUT>(recs, it.start + i + kDepBlock, n0, n1);
+        if (i + 2 * kDepBlock < it.count)
+            load_rec4<NOUT>(recs, it.start + i + 2 * kDepBlock, n0, n1);
         Prep P;
         P.b = Box{0, -1, 0, -1};
         bool live = false;
 #if ASP_ABLATE == 3
         asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x));
-        r0 = n0;
-        r1 = n1;
+        r0 = q0; r1 = q1; q0 = n0; q1 = n1;
         continue;
 #endif
         if (i < it.count)
             live = prep_record<KID, ACC>(g, r0.x, r0.y, r0.z, r0.w, r1.x, kk.x, kk.y, P) &&
                    clip(P.b, X0, Y0, TW, TH);
-        r0 = n0;
-        r1 = n1;
+        r0 = q0;
+        r1 = q1;
+        q0 = n0;
+        q1 = n1;
 #if ASP_ABLATE == 2
         asm volatile("" ::"v"(P.u), "v"(P.v), "v"(P.thr), "v"(P.band), "v"(P.s0), "v"(P.s1),
                      "v"(P.b.x0), "v"(P.b.y1), "v"(live ? 1 : 0));
