@@ -33,7 +33,7 @@ EXPORTS = ("asp_version", "asp_last_error", "asp_device_count", "asp_project2d",
            "asp_kernel_eval", "asp_chunk_ranges", "asp_pixel_neighbours", "asp_ratio",
            "asp_profile", "asp_profile_read", "asp_last_stats", "asp_release")
 
-STAGES = ("memset", "count", "colscan", "tilescan", "bin1", "bin2", "deposit", "merge",
+STAGES = ("memset", "count", "colscan", "tilescan", "scatter", "scale", "deposit", "merge",
           "wide", "ratio")
 
 _lib = None
@@ -130,7 +130,7 @@ def last_stats(device: int = 0):
     s = (C.c_int64 * 8)()
     check(lib().asp_last_stats(device, s, 8))
     return {"records": s[0], "items": s[1], "wide": s[2], "tile": s[3], "tiles": s[4],
-            "records_per_item": s[5], "merges": s[6], "coarse_records": s[7]}
+            "records_per_item": s[5], "merges": s[6], "slabs": s[7]}
 
 
 def profile(device: int = 0, enable: bool = True):

@@ -46,7 +46,6 @@ struct Grid {
     int nx, ny, cs;
     int ncx, ncy;     // reference chunks per axis
     int ntx, nty, ntiles;  // GPU tiles
-    int nctx, ncty, ncoarse;  // coarse bins of 8 x 8 GPU tiles (binning pass 1)
     int nonsquare;    // nx != ny: the y chunk cull is not implied by the r2 test
 };
 

@@ -5,25 +5,25 @@
 // _projector.py:13-120, _pixel_calculations.pyx:9-36, _kernels.pyx:9-20) with a
 // scatter formulation built for CDNA4:
 //
-//   K1 count     streaming pass over (u, v, h): per-workgroup LDS histograms of
-//                (particle, GPU tile) and (particle, coarse bin) insertions
-//   K2a colscan  per column, exclusive prefix over workgroups + totals (both histograms)
-//   K2b tilescan one workgroup: tile / coarse-bin start offsets (tiles in Morton order),
-//                deposit work items (runs of <= CH records of one tile; empty tiles get a
-//                zero item), split-tile merge list, pass-2 binning items
-//   K3 bin1      particles -> coarse bins (512 x 512 px): LDS counting sort per batch,
-//                one contiguous run per (batch, bin): coalesced record stores
-//   K4 bin2      coarse bin -> its 64 GPU tiles, same scheme (runs reserved by atomics)
-//   K5 deposit   one workgroup per work item: records -> fp64 (or int64 fixed-point) LDS
-//                tile accumulators; small footprints lane-per-record, large ones swept
-//                by a whole wave; the tile is written once, or (split tiles) stored as a
-//                partial slab
-//   K6 merge     split tiles: sum their slabs in slab order, convert, write
-//   K7 wide      particles overlapping > kWideTiles tiles, per tile, wave sweeps
-//   K8 ratio     out0 / out1 (mass-weighted maps) when not fused into K5/K6
+//   K1 count     one streaming pass over (u, v, h): per-workgroup LDS histogram of
+//                (particle, GPU tile) insertions -> hist[block][tile]
+//   K2a colscan  per tile, exclusive prefix over blocks (in place) + tile totals
+//   K2b tilescan one workgroup: tile start offsets in Morton order of the tiles, the
+//                deposit work list (runs of <= CH records of one tile; empty tiles get
+//                a zero item) and the merge list of tiles split over several items
+//   K3 scatter   second streaming pass: each insertion written as a 16/32-byte record
+//                into its tile's run (LDS cursors) + per-(block, tile) max|A W_norm|
+//   K3b scale    per tile: max over blocks -> power-of-two fixed-point scale
+//   K4 deposit   one workgroup per work item: records -> int64 LDS tile accumulators
+//                (ds_add_u64), small footprints lane-per-record, large ones swept by a
+//                whole wave; the tile is converted and written once, or (split tiles)
+//                stored as an int64 partial slab
+//   K5 merge     split tiles: exact int64 sum of their slabs, convert, write
+//   K6 wide      particles overlapping > kWideTiles tiles, per tile, wave sweeps
+//   K7 ratio     out0 / out1 (mass-weighted maps) when not fused into K4/K5
 //
-// No MFMA: this is gather/scatter work; the bounds are HBM bytes and VALU/LDS issue
-// (DESIGN.md §4).
+// No MFMA: this is gather/scatter work; the bounds are HBM bytes and VALU/LDS-atomic
+// issue.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -42,26 +42,20 @@ namespace asp {
 
 // Counter words (int) shared by the pipeline stages.
 enum Ctr {
-    cItems = 0,      // deposit work items (K2b)
-    cRecs = 1,       // fine records (K2b)
-    cWideCount = 2,  // wide particles (K1)
-    cChunk = 3,      // records per deposit item (K2b)
-    cWideCursor = 4, // wide list fill (K3)
-    cSlabs = 5,      // partial slabs (K2b)
-    cMerges = 6,     // split tiles (K2b)
-    cWideMax0 = 7,   // max |c0| over wide particles, fp32 bits (K3, kAccFix)
-    cWideMax1 = 8,   // max |c1| over wide particles, fp32 bits (K3, kAccFix)
-    cItems2 = 9,     // pass-2 binning items (K2b)
-    cRecsCoarse = 10,// coarse records (K2b)
+    cItems = 0,     // work items (K2b)
+    cRecs = 1,      // records (K2b)
+    cWideCount = 2, // wide particles (K1)
+    cChunk = 3,     // records per item (K2b)
+    cWideCursor = 4,// wide list fill (K3)
+    cSlabs = 5,     // int64 partial slabs (K2b)
+    cMerges = 6,    // split tiles (K2b)
+    cWideMax0 = 7,  // max |c0| over wide particles, fp32 bits (K3)
+    cWideMax1 = 8,  // max |c1| over wide particles, fp32 bits (K3)
     cNum = 16
 };
 
-constexpr int kCountBlock = 512;  // count / binning workgroup (8 waves)
-constexpr int kUnroll = 2;        // particles (records) per thread per batch
-constexpr int kBatch = kCountBlock * kUnroll;
-constexpr int kCoarseShift = 3;   // coarse bin = 8 x 8 GPU tiles = 512 x 512 pixels
-constexpr int kCoarse = 1 << kCoarseShift;
-constexpr int kMaxCoarse = 512;   // <= kCountBlock: one scan entry per thread
+constexpr int kCountBlock = 512;  // count / scatter workgroup
+constexpr int kUnroll = 2;        // particles in flight per thread in count / scatter
 
 // Load kUnroll particles (lane-strided by the block size); h = 0 past the end, which has
 // no footprint.
@@ -79,91 +73,40 @@ __device__ __forceinline__ void load_batch(const float* __restrict__ u,
     }
 }
 
-template <int NOUT>
-__device__ __forceinline__ void load_props(const float* __restrict__ a0,
-                                           const float* __restrict__ a1, long long base,
-                                           long long p1, float* pa0, float* pa1) {
-#pragma unroll
-    for (int k = 0; k < kUnroll; ++k) {
-        long long p = base + threadIdx.x + (long long)k * kCountBlock;
-        bool in = p < p1;
-        pa0[k] = in ? a0[p] : 0.0f;
-        pa1[k] = (in && NOUT == 2) ? a1[p] : 0.0f;
-    }
-}
-
-// Exclusive scan of cnt[0..n) (n <= kCountBlock) into base[] by a kCountBlock-thread
-// block; returns the total.  Wave scans by DPP shuffles, then the 8 wave totals.
-__device__ __forceinline__ int block_excl_scan(const int* cnt, int* base, int n, int* wtot) {
-    int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    int x = t < n ? cnt[t] : 0;
-    int incl = x;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
-    if (lane == 63) wtot[w] = incl;
-    __syncthreads();
-    int off = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < kCountBlock / 64; ++k) {
-        int y = wtot[k];
-        off += k < w ? y : 0;
-        tot += y;
-    }
-    if (t < n) base[t] = off + incl - x;
-    __syncthreads();
-    return tot;
-}
-
-__device__ __forceinline__ bool tile_range(const Box& b, int& tx0, int& tx1, int& ty0,
-                                           int& ty1) {
-    tx0 = b.x0 >> kTileShift;
-    tx1 = b.x1 >> kTileShift;
-    ty0 = b.y0 >> kTileShift;
-    ty1 = b.y1 >> kTileShift;
-    return (tx1 - tx0 + 1) * (ty1 - ty0 + 1) <= kWideTiles;  // false: wide particle
-}
-
 // ----------------------------------------------------------------------------------
-// K1: count (particle, GPU tile) insertions per (block, tile) and (particle, coarse bin)
-// insertions per (block, coarse bin).
+// K1: count insertions per (block, tile)
 // ----------------------------------------------------------------------------------
 __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__ u,
                                                        const float* __restrict__ v,
                                                        const float* __restrict__ h,
                                                        long long n, long long per_block, Grid g,
                                                        int* __restrict__ hist,
-                                                       int* __restrict__ chist,
                                                        int* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) int lh[];
-    int* lc = lh + g.ntiles;
-    for (int t = threadIdx.x; t < g.ntiles + g.ncoarse; t += kCountBlock) lh[t] = 0;
+    for (int t = threadIdx.x; t < g.ntiles; t += kCountBlock) lh[t] = 0;
     __syncthreads();
     long long p0 = (long long)blockIdx.x * per_block;
     long long p1 = min(n, p0 + per_block);
     int nwide = 0;
+    constexpr long long kStep = (long long)kCountBlock * kUnroll;
     // Software pipeline: the next batch's loads are in flight while this batch is binned.
     float pu[kUnroll], pv[kUnroll], ph[kUnroll];
     load_batch(u, v, h, p0, p1, pu, pv, ph);
-    for (long long base = p0; base < p1; base += kBatch) {
+    for (long long base = p0; base < p1; base += kStep) {
         float nu[kUnroll], nv[kUnroll], nh[kUnroll];
-        load_batch(u, v, h, base + kBatch, p1, nu, nv, nh);
+        load_batch(u, v, h, base + kStep, p1, nu, nv, nh);
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
             Box b;
             if (!footprint(g, pu[k], pv[k], ph[k], b)) continue;
-            int tx0, tx1, ty0, ty1;
-            if (!tile_range(b, tx0, tx1, ty0, ty1)) {
+            int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
+            int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
+            if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > kWideTiles) {
                 ++nwide;
                 continue;
             }
             for (int tx = tx0; tx <= tx1; ++tx)
                 for (int ty = ty0; ty <= ty1; ++ty) atomicAdd(&lh[tx * g.nty + ty], 1);
-            for (int cx = tx0 >> kCoarseShift; cx <= (tx1 >> kCoarseShift); ++cx)
-                for (int cy = ty0 >> kCoarseShift; cy <= (ty1 >> kCoarseShift); ++cy)
-                    atomicAdd(&lc[cx * g.ncty + cy], 1);
         }
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
@@ -176,14 +119,11 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
     __syncthreads();
     int* row = hist + (long long)blockIdx.x * g.ntiles;
     for (int t = threadIdx.x; t < g.ntiles; t += kCountBlock) row[t] = lh[t];
-    int* crow = chist + (long long)blockIdx.x * g.ncoarse;
-    for (int c = threadIdx.x; c < g.ncoarse; c += kCountBlock) crow[c] = lc[c];
 }
 
 // ----------------------------------------------------------------------------------
-// K2a: per column, exclusive prefix of a [nblk][ncol] count matrix over blocks (in
-// place) and the column totals.  64 columns per workgroup (one per lane), the 4 waves
-// split the block range.
+// K2a: per tile, exclusive prefix of hist over blocks (in place); tile totals.
+// 64 tiles per workgroup (one per lane), the 4 waves split the block range.
 // ----------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_colscan(int* __restrict__ hist, int nblk, int ntiles,
                                                     int* __restrict__ tile_total) {
@@ -221,32 +161,14 @@ __global__ __launch_bounds__(kBlock) void k_colscan(int* __restrict__ hist, int 
     }
 }
 
-// Column totals of a [nblk][ncol] count matrix (left unchanged).
-__global__ __launch_bounds__(kBlock) void k_coltotal(const int* __restrict__ hist, int nblk,
-                                                     int ncol, int* __restrict__ total) {
-    __shared__ int part[4][64];
-    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int t = blockIdx.x * 64 + lane;
-    int s = 0;
-    if (t < ncol)
-        for (int b = w; b < nblk; b += 4) s += hist[(long long)b * ncol + t];
-    part[w][lane] = s;
-    __syncthreads();
-    if (w == 0 && t < ncol) total[t] = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
-}
-
 // ----------------------------------------------------------------------------------
-// K2b: single workgroup.
-//  * GPU tiles in Morton order: start offsets (spatially adjacent tiles' records are
-//    adjacent in HBM), fine cursors, deposit work items (every tile >= 1 item, empty
-//    tiles a zero item) and the merge list of tiles split over several items;
-//  * coarse bins: start offsets and the pass-2 binning items.
+// K2b: single workgroup.  Tile start offsets in Morton order of the tiles (spatially
+// adjacent tiles' records are adjacent in HBM), the deposit work list (also Morton
+// order: every tile gets >= 1 item, empty tiles a zero item) and the merge list.
 // ----------------------------------------------------------------------------------
 constexpr int kScanThreads = 1024;
 constexpr int kTargetItems = 2048;
 constexpr int kMinItemRecords = 2048;
-constexpr int kTargetItems2 = 4096;
-constexpr int kMinItem2Records = 8192;
 
 __device__ __forceinline__ void block_scan_ll(long long* s, int tid) {
     for (int o = 1; o < kScanThreads; o <<= 1) {
@@ -257,12 +179,13 @@ __device__ __forceinline__ void block_scan_ll(long long* s, int tid) {
     }
 }
 
-__global__ __launch_bounds__(kScanThreads) void k_tilescan(
-    const int* __restrict__ tile_total, const int* __restrict__ morton, int ntiles,
-    const int* __restrict__ coarse_total, int ncoarse, const int* __restrict__ chist,
-    int nblk, long long* __restrict__ tile_start, int* __restrict__ fcur,
-    Item* __restrict__ items, Merge* __restrict__ merges, Item* __restrict__ items2,
-    int* __restrict__ ctr) {
+__global__ __launch_bounds__(kScanThreads) void k_tilescan(const int* __restrict__ tile_total,
+                                                           const int* __restrict__ morton,
+                                                           int ntiles,
+                                                           long long* __restrict__ tile_start,
+                                                           Item* __restrict__ items,
+                                                           Merge* __restrict__ merges,
+                                                           int* __restrict__ ctr) {
     __shared__ long long s_rec[kScanThreads], s_item[kScanThreads], s_slab[kScanThreads],
         s_merge[kScanThreads];
     int tid = threadIdx.x;
@@ -271,58 +194,9 @@ __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     long long loc = 0;
     for (int r = r0; r < r1; ++r) loc += tile_total[morton[r]];
     s_rec[tid] = loc;
-    long long cl = tid < ncoarse ? coarse_total[tid] : 0;
-    s_item[tid] = cl;
     __syncthreads();
     block_scan_ll(s_rec, tid);
-    block_scan_ll(s_item, tid);
     long long total = s_rec[kScanThreads - 1];
-    long long ctot = s_item[kScanThreads - 1];
-    // Pass-2 items: one coarse bin per thread; consecutive block runs (b, c) grouped into
-    // items of >= ch2 records (Item.start = first block, .count = block count,
-    // .slab = records).
-    int ch2 = (int)max((long long)kMinItem2Records, (ctot + kTargetItems2 - 1) / kTargetItems2);
-    long long nit2 = 0;
-    if (tid < ncoarse) {
-        long long acc = 0;
-        for (int b = 0; b < nblk; ++b) {
-            acc += chist[(long long)b * ncoarse + tid];
-            if (acc >= ch2) {
-                ++nit2;
-                acc = 0;
-            }
-        }
-        if (acc > 0) ++nit2;
-    }
-    __syncthreads();
-    s_slab[tid] = nit2;
-    __syncthreads();
-    block_scan_ll(s_slab, tid);
-    long long ib2 = s_slab[tid] - nit2;
-    if (tid < ncoarse) {
-        long long acc = 0;
-        int b0 = 0;
-        for (int b = 0; b < nblk; ++b) {
-            acc += chist[(long long)b * ncoarse + tid];
-            if (acc >= ch2 || (b == nblk - 1 && acc > 0)) {
-                Item it;
-                it.start = b0;
-                it.tile = tid;
-                it.count = b + 1 - b0;
-                it.slab = (int)acc;
-                it.pad = 0;
-                items2[ib2++] = it;
-                acc = 0;
-                b0 = b + 1;
-            }
-        }
-    }
-    if (tid == kScanThreads - 1) {
-        ctr[cItems2] = (int)s_slab[kScanThreads - 1];
-        ctr[cRecsCoarse] = (int)min(ctot, (long long)0x7fffffff);
-    }
-    __syncthreads();
-    // GPU tiles
     long long base = s_rec[tid] - loc;
     int ch = (int)max((long long)kMinItemRecords, (total + kTargetItems - 1) / kTargetItems);
     long long nit = 0, nsl = 0, nmg = 0;
@@ -330,7 +204,6 @@ __global__ __launch_bounds__(kScanThreads) void k_tilescan(
         int t = morton[r];
         int c = tile_total[t];
         tile_start[t] = base;
-        fcur[t] = (int)base;
         base += c;
         int k = c > 0 ? (c + ch - 1) / ch : 1;
         nit += k;
@@ -381,80 +254,126 @@ __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     }
 }
 
-// Block-major run starts of the coarse records: run (b, c) begins at the exclusive
-// prefix of chist in row-major (block, bin) order.  One workgroup.
-__global__ __launch_bounds__(kScanThreads) void k_runscan(const int* __restrict__ chist,
-                                                          long long m,
-                                                          long long* __restrict__ rstart) {
-    __shared__ long long s[kScanThreads];
-    int tid = threadIdx.x;
-    long long per = (m + kScanThreads - 1) / kScanThreads;
-    long long i0 = min(m, tid * per), i1 = min(m, i0 + per);
-    long long loc = 0;
-    for (long long i = i0; i < i1; ++i) loc += chist[i];
-    s[tid] = loc;
-    __syncthreads();
-    block_scan_ll(s, tid);
-    long long run = s[tid] - loc;
-    for (long long i = i0; i < i1; ++i) {
-        rstart[i] = run;
-        run += chist[i];
+template <int NOUT>
+__device__ __forceinline__ void load_props(const float* __restrict__ a0,
+                                           const float* __restrict__ a1, long long base,
+                                           long long p1, float* pa0, float* pa1) {
+#pragma unroll
+    for (int k = 0; k < kUnroll; ++k) {
+        long long p = base + threadIdx.x + (long long)k * kCountBlock;
+        bool in = p < p1;
+        pa0[k] = in ? a0[p] : 0.0f;
+        pa1[k] = (in && NOUT == 2) ? a1[p] : 0.0f;
     }
 }
 
-// Record (structure of arrays): rec4 = {u, v, h, a0}, rec1 = a1 (two-map runs only).
-
 // ----------------------------------------------------------------------------------
-// K3 (binning pass 1): particles -> coarse bins (512 x 512 px).  Block b writes its
-// records for bin c into its own run (b, c) (block-major layout, k_runscan), through LDS
-// cursors.  A block has only ncoarse (<= 64 for a square grid) runs open at a time, so
-// the XCD's L2 completes each line before it is evicted: the scattered 16-B / 4-B stores
-// reach HBM as full lines, without a staging buffer or block barriers in the loop.
+// K3: scatter records into their tiles' runs.  Same particle partition as K1.
+// Record layout: NOUT == 1 -> float4 {u, v, h, a0};  NOUT == 2 -> 2 x float4
+// {u, v, h, a0}, {a1, 0, 0, 0}.  Also the per-(block, tile) max |c| (fp32 bits) of the
+// records it inserted, the fixed-point bound of K3b.
 // ----------------------------------------------------------------------------------
 template <int KID, int NOUT, int ACC>
-__global__ __launch_bounds__(kCountBlock) void k_bin1(
+__global__ __launch_bounds__(kCountBlock) void k_scatter(
     const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
     const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long per_block,
-    Grid g, const long long* __restrict__ rstart, float4* __restrict__ c4, float* __restrict__ c1,
-    int* __restrict__ wide_list, int* __restrict__ ctr) {
-    extern __shared__ __attribute__((aligned(16))) int cur[];  // [ncoarse] absolute cursors
-    const int nc = g.ncoarse;
-    const long long* rrow = rstart + (long long)blockIdx.x * nc;
-    for (int c = threadIdx.x; c < nc; c += kCountBlock) cur[c] = (int)rrow[c];
+    Grid g, const int* __restrict__ hist, const long long* __restrict__ tile_start,
+    float4* __restrict__ recs, unsigned* __restrict__ cmx, int* __restrict__ wide_list,
+    int* __restrict__ ctr) {
+    extern __shared__ __attribute__((aligned(16))) int cur[];  // absolute record cursors
+    // per-wave staging for the paired record stores (NOUT == 2): 64 records x 32 B
+    float4* stage = (float4*)(cur + ((g.ntiles + 3) & ~3));
+    unsigned* cm = (unsigned*)(stage + (NOUT == 2 ? (kCountBlock / 64) * 128 : 0));
+    const int* row = hist + (long long)blockIdx.x * g.ntiles;
+    for (int t = threadIdx.x; t < g.ntiles; t += kCountBlock) {
+        cur[t] = (int)tile_start[t] + row[t];  // n_recs < 2^31 (checked on the host)
+        if constexpr (ACC == kAccFix) {
+#pragma unroll
+            for (int o = 0; o < NOUT; ++o) cm[t * NOUT + o] = 0u;
+        }
+    }
     __syncthreads();
     long long p0 = (long long)blockIdx.x * per_block;
     long long p1 = min(n, p0 + per_block);
+    constexpr long long kStep = (long long)kCountBlock * kUnroll;
+    // Software pipeline: issue the next batch's loads BEFORE this batch's record stores,
+    // so waiting for them (vmcnt counts loads and stores in issue order) never waits on
+    // the scattered stores.
     float pu[kUnroll], pv[kUnroll], ph[kUnroll], pa0[kUnroll], pa1[kUnroll];
+    int first_slot[kUnroll];
+#pragma unroll
+    for (int k = 0; k < kUnroll; ++k) first_slot[k] = -1;
     load_batch(u, v, h, p0, p1, pu, pv, ph);
     load_props<NOUT>(a0, a1, p0, p1, pa0, pa1);
-    for (long long base = p0; base < p1; base += kBatch) {
+    for (long long base = p0; base < p1; base += kStep) {
         float nu[kUnroll], nv[kUnroll], nh[kUnroll], na0[kUnroll], na1[kUnroll];
-        load_batch(u, v, h, base + kBatch, p1, nu, nv, nh);
-        load_props<NOUT>(a0, a1, base + kBatch, p1, na0, na1);
+        load_batch(u, v, h, base + kStep, p1, nu, nv, nh);
+        load_props<NOUT>(a0, a1, base + kStep, p1, na0, na1);
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
+            long long p = base + threadIdx.x + (long long)k * kCountBlock;
             Box b;
             if (!footprint(g, pu[k], pv[k], ph[k], b)) continue;
-            int tx0, tx1, ty0, ty1;
-            if (!tile_range(b, tx0, tx1, ty0, ty1)) {
-                long long p = base + threadIdx.x + (long long)k * kCountBlock;
+            unsigned c0 = 0u, c1 = 0u;
+            if constexpr (ACC == kAccFix) {
+                c0 = __float_as_uint(fabsf((float)term_coef<KID>(pa0[k], ph[k])));
+                if (NOUT == 2) c1 = __float_as_uint(fabsf((float)term_coef<KID>(pa1[k], ph[k])));
+            }
+            int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
+            int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
+            if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > kWideTiles) {
                 wide_list[atomicAdd(&ctr[cWideCursor], 1)] = (int)p;
                 if constexpr (ACC == kAccFix) {
-                    atomicMax((unsigned*)&ctr[cWideMax0],
-                              __float_as_uint(fabsf((float)term_coef<KID>(pa0[k], ph[k]))));
-                    if (NOUT == 2)
-                        atomicMax((unsigned*)&ctr[cWideMax1],
-                                  __float_as_uint(fabsf((float)term_coef<KID>(pa1[k], ph[k]))));
+                    atomicMax((unsigned*)&ctr[cWideMax0], c0);
+                    if (NOUT == 2) atomicMax((unsigned*)&ctr[cWideMax1], c1);
                 }
                 continue;
             }
-            float4 r = make_float4(pu[k], pv[k], ph[k], pa0[k]);
-            for (int cx = tx0 >> kCoarseShift; cx <= (tx1 >> kCoarseShift); ++cx)
-                for (int cy = ty0 >> kCoarseShift; cy <= (ty1 >> kCoarseShift); ++cy) {
-                    int dst = atomicAdd(&cur[cx * g.ncty + cy], 1);
-                    c4[dst] = r;
-                    if (NOUT == 2) c1[dst] = pa1[k];
+            float4 r0 = make_float4(pu[k], pv[k], ph[k], pa0[k]);
+            float4 r1 = make_float4(pa1[k], 0.0f, 0.0f, 0.0f);
+            for (int tx = tx0; tx <= tx1; ++tx)
+                for (int ty = ty0; ty <= ty1; ++ty) {
+                    int t = tx * g.nty + ty;
+                    int slot = atomicAdd(&cur[t], 1);
+                    if constexpr (ACC == kAccFix) {
+                        atomicMax(&cm[t * NOUT], c0);
+                        if (NOUT == 2) atomicMax(&cm[t * NOUT + 1], c1);
+                    }
+                    if constexpr (NOUT == 2) {
+                        if (tx == tx0 && ty == ty0) {
+                            first_slot[k] = slot;  // written by the paired store below
+                        } else {
+                            recs[2 * (long long)slot] = r0;
+                            recs[2 * (long long)slot + 1] = r1;
+                        }
+                    } else {
+                        recs[slot] = r0;
+                    }
                 }
+        }
+        if constexpr (NOUT == 2) {
+            // Paired store of every particle's first record: lanes 2j and 2j+1 write the
+            // two 16-B halves of record j, so one store instruction covers 32 whole
+            // 32-B records (32 lines) instead of 64 half records (64 lines).
+            float4* st = stage + (threadIdx.x >> 6) * 128;
+            int lane = threadIdx.x & 63;
+#pragma unroll
+            for (int k = 0; k < kUnroll; ++k) {
+                st[2 * lane] = make_float4(pu[k], pv[k], ph[k], pa0[k]);
+                st[2 * lane + 1] = make_float4(pa1[k], 0.0f, 0.0f, 0.0f);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int half = 0; half < 2; ++half) {
+                    int src = half * 32 + (lane >> 1);
+                    int slot = __shfl(first_slot[k], src);
+                    float4 val = st[2 * src + (lane & 1)];
+                    if (slot >= 0) recs[2 * (long long)slot + (lane & 1)] = val;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                first_slot[k] = -1;
+            }
         }
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
@@ -465,88 +384,10 @@ __global__ __launch_bounds__(kCountBlock) void k_bin1(
             pa1[k] = na1[k];
         }
     }
-}
-
-// ----------------------------------------------------------------------------------
-// K4 (binning pass 2): item = coarse bin c, block runs (b, c) for b in [b0, b0 + nb).
-// Phase A counts the item's insertions per tile of the bin (LDS), one atomic per tile
-// reserves the item's run in the tile's segment, phase B re-reads the item (L2 / MALL)
-// and stores each record through an LDS cursor: 64 open runs per block, L2-combined.
-// kAccFix: per-tile max |c| for the fixed-point scale.
-// ----------------------------------------------------------------------------------
-template <int KID, int NOUT, int ACC>
-__global__ __launch_bounds__(kCountBlock) void k_bin2(
-    Grid g, const Item* __restrict__ items2, const int* __restrict__ chist,
-    const long long* __restrict__ rstart, const float4* __restrict__ c4,
-    const float* __restrict__ c1, int* __restrict__ fcur, float4* __restrict__ f4,
-    float* __restrict__ f1, unsigned* __restrict__ tile_cmax) {
-    constexpr int kLoc = kCoarse * kCoarse;  // 64 tiles per coarse bin
-    __shared__ int lcnt[kLoc], lcur[kLoc];
-    __shared__ unsigned cm[2 * kLoc];
-    const Item it = items2[blockIdx.x];
-    const int c = it.tile, nc = g.ncoarse;
-    const int ccx = c / g.ncty, ccy = c - (c / g.ncty) * g.ncty;
-    const int tbx = ccx * kCoarse, tby = ccy * kCoarse;  // first tile of the coarse bin
-    if (threadIdx.x < kLoc) lcnt[threadIdx.x] = 0;
-    if (ACC == kAccFix && threadIdx.x < 2 * kLoc) cm[threadIdx.x] = 0u;
-    __syncthreads();
-    // local tile range of a record inside this coarse bin
-    auto local = [&](const float4& r, int& lx0, int& lx1, int& ly0, int& ly1) -> bool {
-        Box b;
-        if (!footprint(g, r.x, r.y, r.z, b)) return false;
-        int tx0, tx1, ty0, ty1;
-        tile_range(b, tx0, tx1, ty0, ty1);
-        lx0 = max(tx0, tbx) - tbx;
-        ly0 = max(ty0, tby) - tby;
-        lx1 = min(tx1, tbx + kCoarse - 1) - tbx;
-        ly1 = min(ty1, tby + kCoarse - 1) - tby;
-        return lx0 <= lx1 && ly0 <= ly1;
-    };
-    for (int pass = 0; pass < 2; ++pass) {
-        for (int bb = 0; bb < it.count; ++bb) {
-            long long b = it.start + bb;
-            long long s0 = rstart[b * nc + c];
-            int cnt = chist[b * nc + c];
-            for (int i = threadIdx.x; i < cnt; i += kCountBlock) {
-                float4 r = c4[s0 + i];
-                float r1 = NOUT == 2 ? c1[s0 + i] : 0.0f;
-                int lx0, lx1, ly0, ly1;
-                if (!local(r, lx0, lx1, ly0, ly1)) continue;
-                unsigned cc0 = 0u, cc1 = 0u;
-                if (ACC == kAccFix && pass == 0) {
-                    cc0 = __float_as_uint(fabsf((float)term_coef<KID>(r.w, r.z)));
-                    if (NOUT == 2) cc1 = __float_as_uint(fabsf((float)term_coef<KID>(r1, r.z)));
-                }
-                for (int lx = lx0; lx <= lx1; ++lx)
-                    for (int ly = ly0; ly <= ly1; ++ly) {
-                        int lt = lx * kCoarse + ly;
-                        if (pass == 0) {
-                            atomicAdd(&lcnt[lt], 1);
-                            if constexpr (ACC == kAccFix) {
-                                atomicMax(&cm[2 * lt], cc0);
-                                if (NOUT == 2) atomicMax(&cm[2 * lt + 1], cc1);
-                            }
-                        } else {
-                            int dst = atomicAdd(&lcur[lt], 1);
-                            f4[dst] = r;
-                            if (NOUT == 2) f1[dst] = r1;
-                        }
-                    }
-            }
-        }
+    if constexpr (ACC == kAccFix) {
         __syncthreads();
-        if (pass == 0 && threadIdx.x < kLoc) {
-            int lt = threadIdx.x;
-            int tx = tbx + (lt >> kCoarseShift), ty = tby + (lt & (kCoarse - 1));
-            int t = tx * g.nty + ty;
-            int n_lt = lcnt[lt];
-            lcur[lt] = n_lt > 0 ? atomicAdd(&fcur[t], n_lt) : 0;
-            if constexpr (ACC == kAccFix) {
-                for (int o = 0; o < NOUT; ++o)
-                    if (cm[2 * lt + o]) atomicMax(&tile_cmax[2 * t + o], cm[2 * lt + o]);
-            }
-        }
-        __syncthreads();
+        unsigned* out = cmx + (long long)blockIdx.x * g.ntiles * NOUT;
+        for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kCountBlock) out[t] = cm[t];
     }
 }
 
@@ -558,14 +399,44 @@ __device__ __forceinline__ int scale_exp(long long n, float cmax) {
     return kScaleBits - e;
 }
 
-// Fixed-point exponents of a tile (kAccFix): from its record count and max |c|.
-__device__ __forceinline__ int2 tile_scale(const int* tile_total, const unsigned* tile_cmax,
-                                           int t) {
-    int n = tile_total[t];
-    return make_int2(scale_exp(n, __uint_as_float(tile_cmax[2 * t])),
-                     scale_exp(n, __uint_as_float(tile_cmax[2 * t + 1])));
+// ----------------------------------------------------------------------------------
+// K3b: per tile, max over blocks of cmx -> fixed-point exponents tile_k[t] = {k0, k1}.
+// ----------------------------------------------------------------------------------
+template <int NOUT>
+__global__ __launch_bounds__(kBlock) void k_tilescale(const unsigned* __restrict__ cmx, int nblk,
+                                                      int ntiles,
+                                                      const int* __restrict__ tile_total,
+                                                      int2* __restrict__ tile_k) {
+    __shared__ unsigned part[4][64][NOUT];
+    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int t = blockIdx.x * 64 + lane;
+    int b0 = (int)((long long)nblk * w / 4), b1 = (int)((long long)nblk * (w + 1) / 4);
+    unsigned m[NOUT];
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) m[o] = 0u;
+    if (t < ntiles)
+        for (int b = b0; b < b1; ++b)
+#pragma unroll
+            for (int o = 0; o < NOUT; ++o)
+                m[o] = max(m[o], cmx[((long long)b * ntiles + t) * NOUT + o]);
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) part[w][lane][o] = m[o];
+    __syncthreads();
+    if (w == 0 && t < ntiles) {
+        int k[2] = {0, 0};
+#pragma unroll
+        for (int o = 0; o < NOUT; ++o) {
+            unsigned mm = max(max(part[0][lane][o], part[1][lane][o]),
+                              max(part[2][lane][o], part[3][lane][o]));
+            k[o] = scale_exp(tile_total[t], __uint_as_float(mm));
+        }
+        tile_k[t] = make_int2(k[0], k[1]);
+    }
 }
 
+// ----------------------------------------------------------------------------------
+// Pair accumulation into the LDS tile (int64 fixed point)
+// ----------------------------------------------------------------------------------
 #ifndef ASP_ABLATE
 #define ASP_ABLATE 0  // diagnostic builds only (tools/ablate.sh): 1 = no LDS atomics,
                       // 2 = no pair loop, 3 = no record prep
@@ -644,10 +515,27 @@ __device__ __forceinline__ bool clip(Box& b, int X0, int Y0, int TW, int TH) {
 }
 
 template <int NOUT>
-__device__ __forceinline__ void load_rec4(const float4* f4, const float* f1, long long i,
-                                          float4& r0, float& r1) {
-    r0 = f4[i];
-    if constexpr (NOUT == 2) r1 = f1[i];
+__device__ __forceinline__ void load_rec(const float4* recs, long long i, float& u, float& v,
+                                         float& h, float& a0, float& a1) {
+    if constexpr (NOUT == 1) {
+        float4 r = recs[i];
+        u = r.x; v = r.y; h = r.z; a0 = r.w; a1 = 0.0f;
+    } else {
+        float4 r = recs[2 * i];
+        float4 s = recs[2 * i + 1];
+        u = r.x; v = r.y; h = r.z; a0 = r.w; a1 = s.x;
+    }
+}
+
+template <int NOUT>
+__device__ __forceinline__ void load_rec4(const float4* recs, long long i, float4& r0,
+                                          float4& r1) {
+    if constexpr (NOUT == 1) {
+        r0 = recs[i];
+    } else {
+        r0 = recs[2 * i];
+        r1 = recs[2 * i + 1];
+    }
 }
 
 constexpr int kTilePix = kTile * kTile;
@@ -691,9 +579,8 @@ __device__ __forceinline__ void emit_pixel(long long o, unsigned long long s0,
 // ----------------------------------------------------------------------------------
 template <int KID, int NOUT, int ACC>
 __global__ __launch_bounds__(kDepBlock) void k_deposit(
-    Grid g, const float4* __restrict__ f4, const float* __restrict__ f1,
-    const Item* __restrict__ items, const int* __restrict__ tile_total,
-    const unsigned* __restrict__ tile_cmax, unsigned long long* __restrict__ slabs,
+    Grid g, const float4* __restrict__ recs, const Item* __restrict__ items,
+    const int2* __restrict__ tile_k, unsigned long long* __restrict__ slabs,
     float* __restrict__ out0, float* __restrict__ out1, int flags) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];
     unsigned long long* acc0 = acc;
@@ -716,30 +603,29 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
         return;
     }
     tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
-    const int2 kk = ACC == kAccFix ? tile_scale(tile_total, tile_cmax, it.tile) : make_int2(0, 0);
+    const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
     int lane = threadIdx.x & 63;
-    // Software pipeline, two batches deep: batches i+1 and i+2 load while batch i deposits.
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), q0 = r0;
-    float r1 = 0.f, q1 = 0.f;
-    if ((int)threadIdx.x < it.count) load_rec4<NOUT>(f4, f1, it.start + threadIdx.x, r0, r1);
+    // Software pipeline, two batches deep: batches i+1 and i+2 load while batch i deposits
+    // (16 waves/CU x 64 lanes x 32 B x 2 in flight per CU).
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, q0 = r0, q1 = r0;
+    if ((int)threadIdx.x < it.count) load_rec4<NOUT>(recs, it.start + threadIdx.x, r0, r1);
     if ((int)threadIdx.x + kDepBlock < it.count)
-        load_rec4<NOUT>(f4, f1, it.start + threadIdx.x + kDepBlock, q0, q1);
+        load_rec4<NOUT>(recs, it.start + threadIdx.x + kDepBlock, q0, q1);
     for (int base = 0; base < it.count; base += kDepBlock) {
         int i = base + threadIdx.x;
-        float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f);
-        float n1 = 0.f;
+        float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0;
         if (i + 2 * kDepBlock < it.count)
-            load_rec4<NOUT>(f4, f1, it.start + i + 2 * kDepBlock, n0, n1);
+            load_rec4<NOUT>(recs, it.start + i + 2 * kDepBlock, n0, n1);
         Prep P;
         P.b = Box{0, -1, 0, -1};
         bool live = false;
 #if ASP_ABLATE == 3
-        asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1));
+        asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x));
         r0 = q0; r1 = q1; q0 = n0; q1 = n1;
         continue;
 #endif
         if (i < it.count)
-            live = prep_record<KID, ACC>(g, r0.x, r0.y, r0.z, r0.w, r1, kk.x, kk.y, P) &&
+            live = prep_record<KID, ACC>(g, r0.x, r0.y, r0.z, r0.w, r1.x, kk.x, kk.y, P) &&
                    clip(P.b, X0, Y0, TW, TH);
         r0 = q0;
         r1 = q1;
@@ -827,15 +713,14 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
 template <int NOUT, int ACC>
 __global__ __launch_bounds__(kBlock) void k_merge(Grid g, const Merge* __restrict__ merges,
                                                   const unsigned long long* __restrict__ slabs,
-                                                  const int* __restrict__ tile_total,
-                                                  const unsigned* __restrict__ tile_cmax,
+                                                  const int2* __restrict__ tile_k,
                                                   float* __restrict__ out0,
                                                   float* __restrict__ out1, int flags) {
     const Merge m = merges[blockIdx.x];
     int tx = m.tile / g.nty, ty = m.tile - (m.tile / g.nty) * g.nty;
     int X0 = tx * kTile, Y0 = ty * kTile;
     int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
-    const int2 kk = ACC == kAccFix ? tile_scale(tile_total, tile_cmax, m.tile) : make_int2(0, 0);
+    const int2 kk = ACC == kAccFix ? tile_k[m.tile] : make_int2(0, 0);
     for (int k = threadIdx.x; k < kTilePix; k += kBlock) {
         int lx = k >> kTileShift, ly = k & (kTile - 1);
         if (lx >= TW || ly >= TH) continue;
@@ -1025,8 +910,8 @@ struct Buf {
 
 constexpr int kStages = 10;
 enum Stage {
-    kSMemset = 0, kSCount, kSColscan, kSTilescan, kSBin1, kSBin2, kSDeposit, kSMerge, kSWide,
-    kSRatio
+    kSMemset = 0, kSCount, kSColscan, kSTilescan, kSScatter, kSScale, kSDeposit, kSMerge,
+    kSWide, kSRatio
 };
 
 struct Workspace {
@@ -1038,8 +923,8 @@ struct Workspace {
     bool ev_live[kStages] = {};
     double stage_ms[kStages] = {};
     long long stage_n[kStages] = {};
-    Buf in[5], out[2], hist, chist, tile_total, coarse_total, tile_start, coarse_start, fcur,
-        tile_cmax, items, items2, merges, counters, c4, c1, f4, f1, wide, slabs, morton, aux[6];
+    Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
+        wide, slabs, morton, aux[6];
     int* h_counters = nullptr;  // pinned
     int morton_ntx = -1, morton_nty = -1;
     long long stats[8] = {0};
@@ -1169,22 +1054,19 @@ static bool make_grid(double x_min, double x_max, double y_min, double y_max, in
     g.ntx = (nx + kTile - 1) / kTile;
     g.nty = (ny + kTile - 1) / kTile;
     g.ntiles = g.ntx * g.nty;
-    g.nctx = (g.ntx + kCoarse - 1) / kCoarse;
-    g.ncty = (g.nty + kCoarse - 1) / kCoarse;
-    g.ncoarse = g.nctx * g.ncty;
     g.nonsquare = nx != ny;
     return true;
 }
 
-constexpr int kMaxTiles = 16384;  // K1 LDS histogram (64 KiB)
+constexpr int kMaxTiles = 4096;  // K3 LDS: cursor + per-tile max (12 B/tile at 2 maps)
 
 struct Plan {
     long long n, nblk, per_block;
-    int n_items, n_merges, n_slabs, n_wide, n_items2;
-    long long n_recs, n_recs_coarse;
+    int n_items, n_merges, n_slabs, n_wide;
+    long long n_recs;
 };
 
-// Binning passes, deposit, merge, wide, ratio for one kernel / map count / accumulator.
+// K3..K7 for one kernel / map count.
 template <int KID, int NOUT, int ACC>
 static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u,
                     const float* v, const float* h, const float* a0, const float* a1, float* o0,
@@ -1194,22 +1076,22 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     const bool fuse_ratio = ratio && pl.n_wide == 0;
     int dflags = ((flags & ASP_F_ACCUMULATE) ? kFlagAccumulate : 0) | (fuse_ratio ? kFlagRatio : 0);
     {
-        StageMark m(ws, kSBin1, st);
-        size_t lds = (size_t)g.ncoarse * sizeof(int);
-        hipLaunchKernelGGL((k_bin1<KID, NOUT, ACC>), dim3((unsigned)pl.nblk), dim3(kCountBlock),
-                           lds, st, u, v, h, a0, a1, pl.n, pl.per_block, g,
-                           (const long long*)ws.coarse_start.p, (float4*)ws.c4.p,
-                           (float*)ws.c1.p, (int*)ws.wide.p, dc);
+        StageMark m(ws, kSScatter, st);
+        size_t lds = (size_t)((g.ntiles + 3) & ~3) * sizeof(int) +
+                     (NOUT == 2 ? (size_t)(kCountBlock / 64) * 128 * sizeof(float4) : 0) +
+                     (ACC == kAccFix ? (size_t)g.ntiles * NOUT * sizeof(unsigned) : 0);
+        hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC>), dim3((unsigned)pl.nblk), dim3(kCountBlock),
+                           lds, st, u, v, h, a0, a1, pl.n, pl.per_block, g, (const int*)ws.hist.p,
+                           (const long long*)ws.tile_start.p, (float4*)ws.recs.p,
+                           (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc);
         ASP_LAUNCHED();
         m.done();
     }
-    if (pl.n_items2 > 0) {
-        StageMark m(ws, kSBin2, st);
-        hipLaunchKernelGGL((k_bin2<KID, NOUT, ACC>), dim3(pl.n_items2), dim3(kCountBlock), 0, st,
-                           g, (const Item*)ws.items2.p, (const int*)ws.chist.p,
-                           (const long long*)ws.coarse_start.p, (const float4*)ws.c4.p,
-                           (const float*)ws.c1.p, (int*)ws.fcur.p, (float4*)ws.f4.p,
-                           (float*)ws.f1.p, (unsigned*)ws.tile_cmax.p);
+    if (ACC == kAccFix) {
+        StageMark m(ws, kSScale, st);
+        hipLaunchKernelGGL((k_tilescale<NOUT>), dim3((g.ntiles + 63) / 64), dim3(kBlock), 0, st,
+                           (const unsigned*)ws.cmx.p, (int)pl.nblk, g.ntiles,
+                           (const int*)ws.tile_total.p, (int2*)ws.tile_k.p);
         ASP_LAUNCHED();
         m.done();
     }
@@ -1217,9 +1099,9 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
         StageMark m(ws, kSDeposit, st);
         size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4;
         hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(pl.n_items), dim3(kDepBlock), lds, st, g,
-                           (const float4*)ws.f4.p, (const float*)ws.f1.p, (const Item*)ws.items.p,
-                           (const int*)ws.tile_total.p, (const unsigned*)ws.tile_cmax.p,
-                           (unsigned long long*)ws.slabs.p, o0, o1, dflags);
+                           (const float4*)ws.recs.p, (const Item*)ws.items.p,
+                           (const int2*)ws.tile_k.p, (unsigned long long*)ws.slabs.p, o0, o1,
+                           dflags);
         ASP_LAUNCHED();
         m.done();
     }
@@ -1227,8 +1109,7 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
         StageMark m(ws, kSMerge, st);
         hipLaunchKernelGGL((k_merge<NOUT, ACC>), dim3(pl.n_merges), dim3(kBlock), 0, st, g,
                            (const Merge*)ws.merges.p, (const unsigned long long*)ws.slabs.p,
-                           (const int*)ws.tile_total.p, (const unsigned*)ws.tile_cmax.p, o0, o1,
-                           dflags);
+                           (const int2*)ws.tile_k.p, o0, o1, dflags);
         ASP_LAUNCHED();
         m.done();
     }
@@ -1271,9 +1152,8 @@ static int project2d(const float* u, const float* v, const float* h, const float
         return fail(ASP_ERR_INVALID,
                     "invalid grid: need nx, ny, chunk_size >= 1, finite x_max > x_min, "
                     "y_max > y_min");
-    if (g.ntiles > kMaxTiles || g.ncoarse > kMaxCoarse)
-        return fail(ASP_ERR_UNSUPPORTED,
-                    "grid too large (more than 16384 64x64 tiles or 512 coarse bins)");
+    if (g.ntiles > kMaxTiles)
+        return fail(ASP_ERR_UNSUPPORTED, "grid too large (more than 4096 64x64 tiles)");
     if (device < 0 || device >= 64) return fail(ASP_ERR_INVALID, "bad device");
     int ndev = 0;
     ASP_HIP(hipGetDeviceCount(&ndev));
@@ -1332,34 +1212,23 @@ static int project2d(const float* u, const float* v, const float* h, const float
         pl.nblk = std::min<long long>(1024, std::max<long long>(1, (n + 8191) / 8192));
         pl.per_block = (n + pl.nblk - 1) / pl.nblk;
         pl.nblk = (n + pl.per_block - 1) / pl.per_block;
-        const bool det = (flags & ASP_F_DETERMINISTIC) != 0;
         ASP_TRY(ensure(ws.hist, (size_t)pl.nblk * g.ntiles * sizeof(int)));
-        ASP_TRY(ensure(ws.chist, (size_t)pl.nblk * g.ncoarse * sizeof(int)));
+        const bool det = (flags & ASP_F_DETERMINISTIC) != 0;
+        if (det) ASP_TRY(ensure(ws.cmx, (size_t)pl.nblk * g.ntiles * nout * sizeof(unsigned)));
         ASP_TRY(ensure(ws.tile_total, (size_t)g.ntiles * sizeof(int)));
-        ASP_TRY(ensure(ws.coarse_total, (size_t)g.ncoarse * sizeof(int)));
         ASP_TRY(ensure(ws.tile_start, (size_t)g.ntiles * sizeof(long long)));
-        ASP_TRY(ensure(ws.coarse_start, (size_t)pl.nblk * g.ncoarse * sizeof(long long)));
-        ASP_TRY(ensure(ws.fcur, (size_t)g.ntiles * sizeof(int)));
-        ASP_TRY(ensure(ws.tile_cmax, (size_t)g.ntiles * 2 * sizeof(unsigned)));
+        ASP_TRY(ensure(ws.tile_k, (size_t)g.ntiles * sizeof(int2)));
         ASP_TRY(ensure(ws.items, (size_t)(g.ntiles + kTargetItems + 16) * sizeof(Item)));
-        ASP_TRY(ensure(ws.items2, (size_t)(g.ncoarse + kTargetItems2 + 16) * sizeof(Item)));
         ASP_TRY(ensure(ws.merges, (size_t)(g.ntiles + 16) * sizeof(Merge)));
         ASP_TRY(ensure(ws.counters, cNum * sizeof(int)));
         if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, cNum * sizeof(int)));
         int* dc = (int*)ws.counters.p;
         ASP_HIP(hipMemsetAsync(dc, 0, cNum * sizeof(int), st));
-        if (det) ASP_HIP(hipMemsetAsync(ws.tile_cmax.p, 0, (size_t)g.ntiles * 2 * sizeof(unsigned), st));
-        static bool lds_attr = false;  // K1 needs (ntiles + ncoarse) ints of LDS (< 66 KiB)
-        if (!lds_attr) {
-            ASP_HIP(hipFuncSetAttribute((const void*)k_count,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
-            lds_attr = true;
-        }
         {
             StageMark m(ws, kSCount, st);
             hipLaunchKernelGGL(k_count, dim3((unsigned)pl.nblk), dim3(kCountBlock),
-                               (size_t)(g.ntiles + g.ncoarse) * sizeof(int), st, du, dv, dh, n,
-                               pl.per_block, g, (int*)ws.hist.p, (int*)ws.chist.p, dc);
+                               (size_t)g.ntiles * sizeof(int), st, du, dv, dh, n, pl.per_block, g,
+                               (int*)ws.hist.p, dc);
             ASP_LAUNCHED();
             m.done();
         }
@@ -1368,23 +1237,14 @@ static int project2d(const float* u, const float* v, const float* h, const float
             hipLaunchKernelGGL(k_colscan, dim3((g.ntiles + 63) / 64), dim3(kBlock), 0, st,
                                (int*)ws.hist.p, (int)pl.nblk, g.ntiles, (int*)ws.tile_total.p);
             ASP_LAUNCHED();
-            hipLaunchKernelGGL(k_coltotal, dim3((g.ncoarse + 63) / 64), dim3(kBlock), 0, st,
-                               (const int*)ws.chist.p, (int)pl.nblk, g.ncoarse,
-                               (int*)ws.coarse_total.p);
-            ASP_LAUNCHED();
             m.done();
         }
         {
             StageMark m(ws, kSTilescan, st);
             hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(kScanThreads), 0, st,
                                (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles,
-                               (const int*)ws.coarse_total.p, g.ncoarse, (const int*)ws.chist.p,
-                               (int)pl.nblk, (long long*)ws.tile_start.p, (int*)ws.fcur.p,
-                               (Item*)ws.items.p, (Merge*)ws.merges.p, (Item*)ws.items2.p, dc);
-            ASP_LAUNCHED();
-            hipLaunchKernelGGL(k_runscan, dim3(1), dim3(kScanThreads), 0, st,
-                               (const int*)ws.chist.p, (long long)pl.nblk * g.ncoarse,
-                               (long long*)ws.coarse_start.p);
+                               (long long*)ws.tile_start.p, (Item*)ws.items.p,
+                               (Merge*)ws.merges.p, dc);
             ASP_LAUNCHED();
             m.done();
         }
@@ -1396,16 +1256,9 @@ static int project2d(const float* u, const float* v, const float* h, const float
         pl.n_wide = ws.h_counters[cWideCount];
         pl.n_slabs = ws.h_counters[cSlabs];
         pl.n_merges = ws.h_counters[cMerges];
-        pl.n_items2 = ws.h_counters[cItems2];
-        pl.n_recs_coarse = ws.h_counters[cRecsCoarse];
-        if (pl.n_recs >= 0x7fffffffLL || pl.n_recs_coarse >= 0x7fffffffLL)
+        if (pl.n_recs >= 0x7fffffffLL)
             return fail(ASP_ERR_UNSUPPORTED, "more than 2^31 particle-tile records");
-        ASP_TRY(ensure(ws.c4, (size_t)pl.n_recs_coarse * sizeof(float4)));
-        ASP_TRY(ensure(ws.f4, (size_t)pl.n_recs * sizeof(float4)));
-        if (nout == 2) {
-            ASP_TRY(ensure(ws.c1, (size_t)pl.n_recs_coarse * sizeof(float)));
-            ASP_TRY(ensure(ws.f1, (size_t)pl.n_recs * sizeof(float)));
-        }
+        ASP_TRY(ensure(ws.recs, (size_t)pl.n_recs * nout * sizeof(float4)));
         ASP_TRY(ensure(ws.wide, (size_t)pl.n_wide * sizeof(int)));
         ASP_TRY(ensure(ws.slabs, (size_t)pl.n_slabs * nout * kTilePix * sizeof(long long)));
         int rc;
@@ -1435,7 +1288,7 @@ static int project2d(const float* u, const float* v, const float* h, const float
     ws.stats[4] = g.ntiles;
     ws.stats[5] = n > 0 ? ws.h_counters[cChunk] : 0;
     ws.stats[6] = pl.n_merges;
-    ws.stats[7] = pl.n_recs_coarse;
+    ws.stats[7] = pl.n_slabs;
     return ASP_OK;
 }
 
@@ -1680,11 +1533,10 @@ int asp_release(int32_t device) {
         std::lock_guard<std::mutex> lock(ws.mu);
         if (hipSetDevice(d) != hipSuccess) continue;
         Buf* all[] = {&ws.in[0], &ws.in[1], &ws.in[2], &ws.in[3], &ws.in[4], &ws.out[0],
-                      &ws.out[1], &ws.hist, &ws.chist, &ws.tile_total, &ws.coarse_total,
-                      &ws.tile_start, &ws.coarse_start, &ws.fcur, &ws.tile_cmax, &ws.items,
-                      &ws.items2, &ws.merges, &ws.counters, &ws.c4, &ws.c1, &ws.f4, &ws.f1,
-                      &ws.wide, &ws.slabs, &ws.morton, &ws.aux[0], &ws.aux[1], &ws.aux[2],
-                      &ws.aux[3], &ws.aux[4], &ws.aux[5]};
+                      &ws.out[1], &ws.hist, &ws.cmx, &ws.tile_total, &ws.tile_start,
+                      &ws.tile_k, &ws.items, &ws.merges, &ws.counters, &ws.recs, &ws.wide,
+                      &ws.slabs, &ws.morton, &ws.aux[0], &ws.aux[1], &ws.aux[2], &ws.aux[3],
+                      &ws.aux[4], &ws.aux[5]};
         for (Buf* b : all) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;

@@ -132,7 +132,7 @@ int asp_ratio(float *out0, const float *out1, int64_t n, int32_t device, void *s
  * Statistics of the last asp_project2d call on `device` (inspection / roofline):
  * stats[0] = records binned (particle x GPU-tile insertions), stats[1] = work items,
  * stats[2] = wide particles, stats[3] = GPU tile edge (pixels), stats[4] = GPU tiles,
- * stats[5] = records per work item, stats[6] = split tiles, stats[7] = coarse records.
+ * stats[5] = records per work item, stats[6] = split tiles, stats[7] = partial slabs.
  */
 int asp_last_stats(int32_t device, int64_t *stats, int32_t nstats);
 
@@ -140,8 +140,8 @@ int asp_last_stats(int32_t device, int64_t *stats, int32_t nstats);
  * Stage timing with HIP events recorded on the call's stream around every launch
  * (enable != 0 starts and resets, 0 stops).  asp_profile_read returns, per stage, the
  * summed milliseconds and the number of launches since the last reset.  Stages:
- * 0 memset, 1 count, 2 colscan, 3 tilescan, 4 bin1 (particles -> coarse bins),
- * 5 bin2 (coarse bins -> GPU tiles), 6 deposit, 7 merge, 8 wide, 9 ratio.
+ * 0 memset, 1 count, 2 colscan, 3 tilescan, 4 scatter, 5 scale, 6 deposit, 7 merge,
+ * 8 wide, 9 ratio.
  */
 int asp_profile(int32_t device, int32_t enable);
 int asp_profile_read(int32_t device, double *ms_sum, int64_t *launches, int32_t nstages);
