@@ -104,10 +104,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    local = local % max(1, torch.cuda.device_count())  # 1-GPU rehearsal of N ranks
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("ASP_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:  # rehearsal only (several ranks sharing one GPU cannot use RCCL)
+            dist.init_process_group(backend)
     from asp_amd import _lib
     from asp_amd.device import project2d, stats
     from asp_amd.distributed import project2d_sharded, zslab_bounds
