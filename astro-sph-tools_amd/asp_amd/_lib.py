@@ -30,11 +30,12 @@ ASP_ERR_UNSUPPORTED = -4
 
 # Every symbol include/asp.h declares (tests check the library exports all of them).
 EXPORTS = ("asp_version", "asp_last_error", "asp_device_count", "asp_project2d",
-           "asp_kernel_eval", "asp_chunk_ranges", "asp_pixel_neighbours", "asp_ratio",
+           "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges", "asp_pixel_neighbours", "asp_ratio",
            "asp_profile", "asp_profile_read", "asp_last_stats", "asp_release")
 
 STAGES = ("memset", "count", "colscan", "tilescan", "scatter", "scale", "deposit", "merge",
-          "wide", "ratio")
+          "wide", "ratio", "cube_count", "cube_colscan", "cube_tilescan", "cube_scatter",
+          "cube_deposit", "cube_merge")
 
 _lib = None
 
@@ -74,6 +75,8 @@ def lib():
     L.asp_project2d.argtypes = [_f, _f, _f, _f, _f, C.c_int64, C.c_double, C.c_double,
                                 C.c_double, C.c_double, C.c_int32, C.c_int32, C.c_int32,
                                 C.c_int32, C.c_int32, _f, _f, C.c_int32, C.c_void_p]
+    L.asp_project3d.argtypes = ([_f] * 5 + [C.c_int64] + [C.c_double] * 6 + [C.c_int32] * 7
+                                + [_f, C.c_int32, C.c_void_p])
     L.asp_kernel_eval.argtypes = [C.c_int32, _d, _d, _d, C.c_int64, C.c_int32, C.c_int32,
                                   C.c_void_p]
     L.asp_chunk_ranges.argtypes = [_f, _f, _f, C.c_int64, C.c_double, C.c_double, C.c_double,
@@ -87,8 +90,8 @@ def lib():
     L.asp_profile_read.argtypes = [C.c_int32, _d, _i64, C.c_int32]
     L.asp_last_stats.argtypes = [C.c_int32, _i64, C.c_int32]
     L.asp_release.argtypes = [C.c_int32]
-    for name in ("asp_project2d", "asp_kernel_eval", "asp_chunk_ranges", "asp_pixel_neighbours",
-                 "asp_ratio", "asp_profile", "asp_profile_read", "asp_last_stats",
+    for name in ("asp_project2d", "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges",
+                 "asp_pixel_neighbours", "asp_ratio", "asp_profile", "asp_profile_read", "asp_last_stats",
                  "asp_release"):
         getattr(L, name).restype = C.c_int
     _lib = L

@@ -74,6 +74,38 @@ def project2d(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
     return out0, (out1 if a1 is not None else None)
 
 
+def project3d(x, y, z, h, a, *, cube_size, extent, kernel="cubic", planes=None,
+              accumulate: bool = False, out=None, stream=None):
+    """Deposit device-resident particles into a voxel cube (asp_project3d).
+
+    ``extent = (x_min, x_max, y_min, y_max, z_min, z_max)``; ``planes = (k_lo, k_hi)``
+    restricts the output to those z planes (default: all).  Returns the
+    (nx, ny, k_hi - k_lo) float32 tensor on the particles' device.
+    """
+    import torch
+    dev = x.device
+    n = x.shape[0]
+    for t, name in ((x, "x"), (y, "y"), (z, "z"), (h, "h"), (a, "a")):
+        _check(t, name, n, dev)
+    nx, ny, nz = (int(c) for c in cube_size)
+    k_lo, k_hi = (0, nz) if planes is None else (int(planes[0]), int(planes[1]))
+    shape = (nx, ny, max(0, k_hi - k_lo))
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=dev)
+    if (out.dtype != torch.float32 or out.device != dev or not out.is_contiguous()
+            or out.numel() != shape[0] * shape[1] * shape[2]):
+        raise ValueError("out must be a contiguous float32 (nx, ny, k_hi - k_lo) tensor on the device")
+    flags = _lib.ASP_F_DEVICE_PTRS | (_lib.ASP_F_ACCUMULATE if accumulate else 0)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    P = _lib.ptr
+    e = [float(v) for v in extent]
+    _lib.check(_lib.lib().asp_project3d(P(x), P(y), P(z), P(h), P(a), n, *e, nx, ny, nz, k_lo,
+                                        k_hi, kernel_id(kernel), flags, P(out), dev.index or 0,
+                                        stream))
+    return out
+
+
 def stats(device: int = 0):
     """Counters of the last projection on ``device`` (records, work items, wide, ...)."""
     return _lib.last_stats(device)

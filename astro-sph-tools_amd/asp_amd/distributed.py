@@ -89,3 +89,93 @@ def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
                                             outs[0].numel(), dev.index or 0,
                                             torch.cuda.current_stream(dev).cuda_stream))
     return outs[0], (outs[1] if len(outs) > 1 else None)
+
+
+# ---------------------------------------------------------------------------------------
+# 3-D cube: voxel Z-slab ownership with footprint-halo duplication
+# ---------------------------------------------------------------------------------------
+def plane_slabs(nz: int, world_size: int):
+    """Equal split of the nz voxel planes: rank r owns planes [K[r], K[r+1])."""
+    return [(nz * r) // world_size for r in range(world_size + 1)]
+
+
+def route_particles(z, h, z_extent, nz: int, world_size: int):
+    """Owner-rank range [r0, r1] of every particle's plane footprint (r0 > r1: none).
+
+    The plane range is a superset (one plane of slack each side) of the planes whose
+    corners can lie within 2|h| of z; the device deposit decides every voxel exactly,
+    so duplicates only cost bandwidth.
+    """
+    import torch
+    z_min, z_max = (float(e) for e in z_extent)
+    pz = (z_max - z_min) / nz
+    zd, rad = z.double(), (2.0 * h.double()).abs()
+    k0 = torch.floor((zd - rad - z_min) / pz) - 1
+    k1 = torch.ceil((zd + rad - z_min) / pz) + 1
+    ok = (rad > 0) & torch.isfinite(zd) & torch.isfinite(rad) & (k1 >= 0) & (k0 <= nz - 1)
+    k0 = k0.clamp(0, nz - 1).long()
+    k1 = k1.clamp(0, nz - 1).long()
+    K = torch.tensor(plane_slabs(nz, world_size)[1:-1], device=z.device, dtype=torch.long)
+    r0 = torch.searchsorted(K, k0, right=True)
+    r1 = torch.searchsorted(K, k1, right=True)
+    r0 = torch.where(ok, r0, torch.full_like(r0, world_size))
+    r1 = torch.where(ok, r1, torch.full_like(r1, -1))
+    return r0, r1
+
+
+def exchange_halo(x, y, z, h, a, *, z_extent, nz: int, group=None):
+    """All-to-all exchange: every rank receives every particle (from any rank) whose
+    footprint reaches its plane slab.  Returns the received (x, y, z, h, a)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    r0, r1 = route_particles(z, h, z_extent, nz, world)
+    packed = torch.stack([x, y, z, h, a], dim=1)
+    parts, counts = [], []
+    for d in range(world):
+        sel = packed[(r0 <= d) & (r1 >= d)]
+        parts.append(sel)
+        counts.append(sel.shape[0])
+    send = torch.cat(parts, dim=0).contiguous()
+    scount = torch.tensor(counts, dtype=torch.int64, device=x.device)
+    rcount = torch.empty_like(scount)
+    dist.all_to_all_single(rcount, scount, group=group)
+    rc = rcount.tolist()
+    recv = torch.empty((sum(rc), 5), dtype=send.dtype, device=send.device)
+    dist.all_to_all_single(recv.view(-1), send.view(-1), [c * 5 for c in rc],
+                           [c * 5 for c in counts], group=group)
+    return tuple(recv[:, c].contiguous() for c in range(5))
+
+
+def project3d_sharded(x, y, z, h, a, *, cube_size, extent, kernel="cubic",
+                      gather: str = "none", group=None, projector=None):
+    """Cube on W ranks: rank r owns voxel planes [K[r], K[r+1]) of ``plane_slabs``.
+
+    Any input split works (each rank passes ITS particles): one all-to-all moves each
+    particle to every rank whose slab its footprint reaches (halo duplication), then each
+    rank deposits its slab locally -- no reduction of the 512 MiB cube.  ``gather="none"``
+    returns this rank's (nx, ny, K[r+1]-K[r]) slab; ``"all"`` all-gathers the full cube
+    on every rank.  ``projector`` replaces the local deposit (CPU tests); default HIP.
+    """
+    import torch
+    import torch.distributed as dist
+    from .device import project3d
+    proj = project3d if projector is None else projector
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    nx, ny, nz = (int(c) for c in cube_size)
+    K = plane_slabs(nz, world)
+    if world > 1:
+        x, y, z, h, a = exchange_halo(x, y, z, h, a, z_extent=extent[4:6], nz=nz, group=group)
+    local = proj(x, y, z, h, a, cube_size=cube_size, extent=extent, kernel=kernel,
+                 planes=(K[rank], K[rank + 1]))
+    if gather == "none" or world == 1:
+        return local
+    if gather != "all":
+        raise ValueError(f"unknown gather {gather!r}")
+    zmax = max(K[r + 1] - K[r] for r in range(world))
+    pad = torch.zeros((nx, ny, zmax), dtype=local.dtype, device=local.device)
+    pad[:, :, :local.shape[2]] = local
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    return torch.cat([bufs[r][:, :, :K[r + 1] - K[r]] for r in range(world)], dim=2)

@@ -1,0 +1,130 @@
+// asp_host.hpp -- host runtime shared by the 2-D and 3-D projectors: errors, the
+// per-device workspace cache (HBM buffers reused across calls), HIP-event stage timing.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/asp.h"
+
+namespace asp {
+
+inline thread_local std::string t_err;
+
+inline int fail(int code, const std::string& msg) {
+    t_err = msg;
+    return code;
+}
+
+#define ASP_HIP(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail(ASP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+constexpr int kStages = 16;
+enum Stage {
+    kSMemset = 0, kSCount, kSColscan, kSTilescan, kSScatter, kSScale, kSDeposit, kSMerge,
+    kSWide, kSRatio,
+    // 3-D cube (asp_project3d)
+    kS3Count = 10, kS3Colscan, kS3Tilescan, kS3Scatter, kS3Deposit, kS3Merge
+};
+
+struct Workspace {
+    std::mutex mu;
+    // HIP-event profiling (asp_profile): per-stage start/stop events of the last call,
+    // folded into the running sums at the next call or at asp_profile_read.
+    bool prof = false;
+    hipEvent_t ev[2 * kStages] = {};
+    bool ev_live[kStages] = {};
+    double stage_ms[kStages] = {};
+    long long stage_n[kStages] = {};
+    Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
+        wide, slabs, morton, aux[6];
+    int* h_counters = nullptr;  // pinned
+    int morton_ntx = -1, morton_nty = -1;
+    Buf morton3;  // brick order of the 3-D cube
+    int morton3_key[3] = {-1, -1, -1};
+    long long stats[8] = {0};
+};
+
+inline Workspace g_ws[64];
+
+inline int prof_fold(Workspace& ws) {
+    for (int k = 0; k < kStages; ++k) {
+        if (!ws.ev_live[k]) continue;
+        ASP_HIP(hipEventSynchronize(ws.ev[2 * k + 1]));
+        float ms = 0.0f;
+        ASP_HIP(hipEventElapsedTime(&ms, ws.ev[2 * k], ws.ev[2 * k + 1]));
+        ws.stage_ms[k] += ms;
+        ws.stage_n[k] += 1;
+        ws.ev_live[k] = false;
+    }
+    return ASP_OK;
+}
+
+// Stage bracket: record start/stop events around a launch when profiling.
+struct StageMark {
+    Workspace& ws;
+    int k;
+    hipStream_t st;
+    StageMark(Workspace& w, int stage, hipStream_t s) : ws(w), k(stage), st(s) {
+        if (ws.prof) (void)hipEventRecord(ws.ev[2 * k], st);
+    }
+    void done() {
+        if (ws.prof) {
+            (void)hipEventRecord(ws.ev[2 * k + 1], st);
+            ws.ev_live[k] = true;
+        }
+    }
+};
+
+inline int ensure(Buf& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return ASP_OK;
+    if (b.p) {
+        hipError_t e = hipFree(b.p);
+        (void)e;
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    size_t want = bytes + bytes / 4;
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) {
+        e = hipMalloc(&b.p, bytes);
+        want = bytes;
+    }
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        return fail(ASP_ERR_NOMEM, "hipMalloc(" + std::to_string(bytes) + ") failed: " +
+                                       hipGetErrorString(e));
+    }
+    b.cap = want;
+    return ASP_OK;
+}
+
+#define ASP_TRY(expr)                  \
+    do {                               \
+        int rc_ = (expr);              \
+        if (rc_ != ASP_OK) return rc_; \
+    } while (0)
+
+#define ASP_LAUNCHED()                                                                    \
+    do {                                                                                  \
+        hipError_t e_ = hipGetLastError();                                                \
+        if (e_ != hipSuccess)                                                             \
+            return fail(ASP_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+
+}  // namespace asp

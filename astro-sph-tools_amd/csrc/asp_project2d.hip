@@ -36,23 +36,11 @@
 #include <vector>
 
 #include "../../include/asp.h"
+#include "asp_binning.hpp"
 #include "asp_device.hpp"
+#include "asp_host.hpp"
 
 namespace asp {
-
-// Counter words (int) shared by the pipeline stages.
-enum Ctr {
-    cItems = 0,     // work items (K2b)
-    cRecs = 1,      // records (K2b)
-    cWideCount = 2, // wide particles (K1)
-    cChunk = 3,     // records per item (K2b)
-    cWideCursor = 4,// wide list fill (K3)
-    cSlabs = 5,     // int64 partial slabs (K2b)
-    cMerges = 6,    // split tiles (K2b)
-    cWideMax0 = 7,  // max |c0| over wide particles, fp32 bits (K3)
-    cWideMax1 = 8,  // max |c1| over wide particles, fp32 bits (K3)
-    cNum = 16
-};
 
 constexpr int kCountBlock = 512;  // count / scatter workgroup
 constexpr int kUnroll = 2;        // particles in flight per thread in count / scatter
@@ -119,139 +107,6 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
     __syncthreads();
     int* row = hist + (long long)blockIdx.x * g.ntiles;
     for (int t = threadIdx.x; t < g.ntiles; t += kCountBlock) row[t] = lh[t];
-}
-
-// ----------------------------------------------------------------------------------
-// K2a: per tile, exclusive prefix of hist over blocks (in place); tile totals.
-// 64 tiles per workgroup (one per lane), the 4 waves split the block range.
-// ----------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_colscan(int* __restrict__ hist, int nblk, int ntiles,
-                                                    int* __restrict__ tile_total) {
-    __shared__ int part[4][64];
-    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int t = blockIdx.x * 64 + lane;
-    int b0 = (int)((long long)nblk * w / 4), b1 = (int)((long long)nblk * (w + 1) / 4);
-    int s = 0;
-    if (t < ntiles) {
-        int b = b0;
-        for (; b + 8 <= b1; b += 8) {
-            int c[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) c[k] = hist[(long long)(b + k) * ntiles + t];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                hist[(long long)(b + k) * ntiles + t] = s;
-                s += c[k];
-            }
-        }
-        for (; b < b1; ++b) {
-            int c = hist[(long long)b * ntiles + t];
-            hist[(long long)b * ntiles + t] = s;
-            s += c;
-        }
-    }
-    part[w][lane] = s;
-    __syncthreads();
-    int off = 0;
-    for (int k = 0; k < w; ++k) off += part[k][lane];
-    if (t < ntiles) {
-        if (off)
-            for (int b = b0; b < b1; ++b) hist[(long long)b * ntiles + t] += off;
-        if (w == 3) tile_total[t] = off + s;
-    }
-}
-
-// ----------------------------------------------------------------------------------
-// K2b: single workgroup.  Tile start offsets in Morton order of the tiles (spatially
-// adjacent tiles' records are adjacent in HBM), the deposit work list (also Morton
-// order: every tile gets >= 1 item, empty tiles a zero item) and the merge list.
-// ----------------------------------------------------------------------------------
-constexpr int kScanThreads = 1024;
-constexpr int kTargetItems = 2048;
-constexpr int kMinItemRecords = 2048;
-
-__device__ __forceinline__ void block_scan_ll(long long* s, int tid) {
-    for (int o = 1; o < kScanThreads; o <<= 1) {
-        long long x = tid >= o ? s[tid - o] : 0;
-        __syncthreads();
-        s[tid] += x;
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(kScanThreads) void k_tilescan(const int* __restrict__ tile_total,
-                                                           const int* __restrict__ morton,
-                                                           int ntiles,
-                                                           long long* __restrict__ tile_start,
-                                                           Item* __restrict__ items,
-                                                           Merge* __restrict__ merges,
-                                                           int* __restrict__ ctr) {
-    __shared__ long long s_rec[kScanThreads], s_item[kScanThreads], s_slab[kScanThreads],
-        s_merge[kScanThreads];
-    int tid = threadIdx.x;
-    int per = (ntiles + kScanThreads - 1) / kScanThreads;
-    int r0 = min(ntiles, tid * per), r1 = min(ntiles, r0 + per);
-    long long loc = 0;
-    for (int r = r0; r < r1; ++r) loc += tile_total[morton[r]];
-    s_rec[tid] = loc;
-    __syncthreads();
-    block_scan_ll(s_rec, tid);
-    long long total = s_rec[kScanThreads - 1];
-    long long base = s_rec[tid] - loc;
-    int ch = (int)max((long long)kMinItemRecords, (total + kTargetItems - 1) / kTargetItems);
-    long long nit = 0, nsl = 0, nmg = 0;
-    for (int r = r0; r < r1; ++r) {
-        int t = morton[r];
-        int c = tile_total[t];
-        tile_start[t] = base;
-        base += c;
-        int k = c > 0 ? (c + ch - 1) / ch : 1;
-        nit += k;
-        if (k > 1) {
-            nsl += k;
-            nmg += 1;
-        }
-    }
-    s_item[tid] = nit;
-    s_slab[tid] = nsl;
-    s_merge[tid] = nmg;
-    __syncthreads();
-    block_scan_ll(s_item, tid);
-    block_scan_ll(s_slab, tid);
-    block_scan_ll(s_merge, tid);
-    long long ib = s_item[tid] - nit, sb = s_slab[tid] - nsl, mb = s_merge[tid] - nmg;
-    for (int r = r0; r < r1; ++r) {
-        int t = morton[r];
-        int c = tile_total[t];
-        int k = c > 0 ? (c + ch - 1) / ch : 1;
-        long long s0 = tile_start[t];
-        for (int j = 0; j < k; ++j) {
-            Item it;
-            it.start = s0 + (long long)j * ch;
-            it.tile = t;
-            it.count = c > 0 ? min(ch, c - j * ch) : 0;
-            it.slab = k > 1 ? (int)(sb + j) : -1;
-            it.pad = 0;
-            items[ib + j] = it;
-        }
-        ib += k;
-        if (k > 1) {
-            Merge m;
-            m.tile = t;
-            m.slab0 = (int)sb;
-            m.nslab = k;
-            m.pad = 0;
-            merges[mb++] = m;
-            sb += k;
-        }
-    }
-    if (tid == kScanThreads - 1) {
-        ctr[cItems] = (int)s_item[kScanThreads - 1];
-        ctr[cRecs] = (int)min(total, (long long)0x7fffffff);
-        ctr[cChunk] = ch;
-        ctr[cSlabs] = (int)s_slab[kScanThreads - 1];
-        ctr[cMerges] = (int)s_merge[kScanThreads - 1];
-    }
 }
 
 template <int NOUT>
@@ -886,118 +741,6 @@ __global__ __launch_bounds__(kBlock) void k_neighbours(Grid g, const float* __re
     if (!pass && threadIdx.x == 0) counts[blockIdx.x] = run;
 }
 
-// ----------------------------------------------------------------------------------
-// Host runtime
-// ----------------------------------------------------------------------------------
-static thread_local std::string t_err;
-
-static int fail(int code, const std::string& msg) {
-    t_err = msg;
-    return code;
-}
-
-#define ASP_HIP(expr)                                                                    \
-    do {                                                                                 \
-        hipError_t e_ = (expr);                                                          \
-        if (e_ != hipSuccess)                                                            \
-            return fail(ASP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
-    } while (0)
-
-struct Buf {
-    void* p = nullptr;
-    size_t cap = 0;
-};
-
-constexpr int kStages = 10;
-enum Stage {
-    kSMemset = 0, kSCount, kSColscan, kSTilescan, kSScatter, kSScale, kSDeposit, kSMerge,
-    kSWide, kSRatio
-};
-
-struct Workspace {
-    std::mutex mu;
-    // HIP-event profiling (asp_profile): per-stage start/stop events of the last call,
-    // folded into the running sums at the next call or at asp_profile_read.
-    bool prof = false;
-    hipEvent_t ev[2 * kStages] = {};
-    bool ev_live[kStages] = {};
-    double stage_ms[kStages] = {};
-    long long stage_n[kStages] = {};
-    Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
-        wide, slabs, morton, aux[6];
-    int* h_counters = nullptr;  // pinned
-    int morton_ntx = -1, morton_nty = -1;
-    long long stats[8] = {0};
-};
-
-static Workspace g_ws[64];
-
-static int prof_fold(Workspace& ws) {
-    for (int k = 0; k < kStages; ++k) {
-        if (!ws.ev_live[k]) continue;
-        ASP_HIP(hipEventSynchronize(ws.ev[2 * k + 1]));
-        float ms = 0.0f;
-        ASP_HIP(hipEventElapsedTime(&ms, ws.ev[2 * k], ws.ev[2 * k + 1]));
-        ws.stage_ms[k] += ms;
-        ws.stage_n[k] += 1;
-        ws.ev_live[k] = false;
-    }
-    return ASP_OK;
-}
-
-// Stage bracket: record start/stop events around a launch when profiling.
-struct StageMark {
-    Workspace& ws;
-    int k;
-    hipStream_t st;
-    StageMark(Workspace& w, int stage, hipStream_t s) : ws(w), k(stage), st(s) {
-        if (ws.prof) (void)hipEventRecord(ws.ev[2 * k], st);
-    }
-    void done() {
-        if (ws.prof) {
-            (void)hipEventRecord(ws.ev[2 * k + 1], st);
-            ws.ev_live[k] = true;
-        }
-    }
-};
-
-static int ensure(Buf& b, size_t bytes) {
-    if (bytes == 0) bytes = 16;
-    if (b.cap >= bytes) return ASP_OK;
-    if (b.p) {
-        hipError_t e = hipFree(b.p);
-        (void)e;
-        b.p = nullptr;
-        b.cap = 0;
-    }
-    size_t want = bytes + bytes / 4;
-    hipError_t e = hipMalloc(&b.p, want);
-    if (e != hipSuccess) {
-        e = hipMalloc(&b.p, bytes);
-        want = bytes;
-    }
-    if (e != hipSuccess) {
-        b.p = nullptr;
-        return fail(ASP_ERR_NOMEM, "hipMalloc(" + std::to_string(bytes) + ") failed: " +
-                                       hipGetErrorString(e));
-    }
-    b.cap = want;
-    return ASP_OK;
-}
-
-#define ASP_TRY(expr)                  \
-    do {                               \
-        int rc_ = (expr);              \
-        if (rc_ != ASP_OK) return rc_; \
-    } while (0)
-
-#define ASP_LAUNCHED()                                                                    \
-    do {                                                                                  \
-        hipError_t e_ = hipGetLastError();                                                \
-        if (e_ != hipSuccess)                                                             \
-            return fail(ASP_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e_)); \
-    } while (0)
-
 static uint32_t spread_bits(uint32_t x) {
     x &= 0xffff;
     x = (x | (x << 8)) & 0x00ff00ff;
@@ -1535,7 +1278,7 @@ int asp_release(int32_t device) {
         Buf* all[] = {&ws.in[0], &ws.in[1], &ws.in[2], &ws.in[3], &ws.in[4], &ws.out[0],
                       &ws.out[1], &ws.hist, &ws.cmx, &ws.tile_total, &ws.tile_start,
                       &ws.tile_k, &ws.items, &ws.merges, &ws.counters, &ws.recs, &ws.wide,
-                      &ws.slabs, &ws.morton, &ws.aux[0], &ws.aux[1], &ws.aux[2], &ws.aux[3],
+                      &ws.slabs, &ws.morton, &ws.morton3, &ws.aux[0], &ws.aux[1], &ws.aux[2], &ws.aux[3],
                       &ws.aux[4], &ws.aux[5]};
         for (Buf* b : all) {
             if (b->p) (void)hipFree(b->p);
@@ -1545,6 +1288,7 @@ int asp_release(int32_t device) {
         if (ws.h_counters) (void)hipHostFree(ws.h_counters);
         ws.h_counters = nullptr;
         ws.morton_ntx = ws.morton_nty = -1;
+        ws.morton3_key[0] = ws.morton3_key[1] = ws.morton3_key[2] = -1;
     }
     return ASP_OK;
 }

@@ -1,0 +1,569 @@
+// asp_project3d.hip -- MI355X (gfx950) SPH particle -> voxel-cube deposit (512^3 cube,
+// SURVEY.md §8(a) last row; BASELINE.json configs[4]).
+//
+// The reference has no volumetric path; the cube's semantics are the build's own,
+// restated on the CPU by oracle/asp_oracle.c (oracle_project3d): voxel-corner sampling
+// with each axis' own pitch, 3-D distance, the same kernels and the same strict
+// r2 < (2h)^2 neighbour test as the 2-D map (_pixel_calculations.pyx:11-14, :30-34).
+//
+// Same pipeline shape as the 2-D projector, on 16 x 16 x 32 voxel bricks (z fastest,
+// matching the (nx, ny, nz) C-order output, so one brick row is a 128-byte run):
+//   C1 count     streaming pass over (x, y, z, h): LDS histogram of (particle, brick)
+//                insertions per workgroup -> hist[block][brick]
+//   C2 colscan / tilescan   shared with the 2-D path (asp_binning.hpp), bricks in 3-D
+//                Morton order
+//   C3 scatter   second pass: 32-byte records {x, y, z, h}, {a} into their bricks' runs
+//   C4 deposit   one workgroup per work item: fp64 LDS brick accumulator (64 KiB);
+//                small boxes lane-per-record, large ones swept by a whole wave over the
+//                flattened box; the neighbour decision is the oracle's fp64 arithmetic
+//                (bit-exact neighbour sets), the term A*W is fp32, summed in fp64
+//   C5 merge     bricks split over several items: fp64 slab sum in slab order
+// A call may produce a slab of planes [k_lo, k_hi) only (Z-slab ownership across GPUs,
+// asp_amd.distributed.project3d_sharded).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/asp.h"
+#include "asp_binning.hpp"
+#include "asp_device.hpp"
+#include "asp_host.hpp"
+
+namespace asp {
+
+constexpr int kBX = 16, kBY = 16, kBZ = 32;  // brick edge (voxels); z fastest
+constexpr int kBXs = 4, kBYs = 4, kBZs = 5;
+constexpr int kBrickVox = kBX * kBY * kBZ;   // 8192 -> 64 KiB of fp64 accumulators
+constexpr int kMaxBricks = 16384;            // C1/C3 LDS: one int per brick (64 KiB)
+constexpr int k3Block = 512;                 // count / scatter / deposit workgroup
+constexpr int kSmallVox = 32;                // boxes up to this many voxels: lane-per-record
+
+struct Grid3 {
+    double x_min, y_min, z_min;
+    double px, py, pz;       // (max - min) / n per axis
+    double ipx, ipy, ipz;    // reciprocals (candidate boxes only)
+    int nx, ny, nz;
+    int k_lo, nzl;           // output planes [k_lo, k_lo + nzl)
+    int nbx, nby, nbz, nb;   // bricks over the output slab
+};
+
+struct Box3 {
+    int i0, i1, j0, j1, k0, k1;  // inclusive voxel ranges (absolute indices)
+};
+
+// Superset of {c in [lo, hi] : |w_min + c * pitch - w| <= rad}: fp64 estimate widened by
+// a margin far above its rounding error (2^-40 relative to the operand magnitudes, plus
+// 2^-20 cell), so the exact test below never misses a voxel.
+__device__ __forceinline__ bool axis_cells(double w, double rad, double w_min, double ip, int lo,
+                                           int hi, int& a, int& b) {
+    double t0 = (w - rad - w_min) * ip, t1 = (w + rad - w_min) * ip;
+    double d = (fabs(w) + rad + fabs(w_min)) * ip * 0x1p-40 + 0x1p-20;
+    double f0 = fmax(ceil(t0 - d), (double)lo);
+    double f1 = fmin(floor(t1 + d), (double)hi);
+    if (!(f0 <= f1)) return false;
+    a = (int)f0;
+    b = (int)f1;
+    return true;
+}
+
+__device__ __forceinline__ bool footprint3(const Grid3& g, float x, float y, float z, float h,
+                                           Box3& b) {
+    double rad = fabs(2.0 * (double)h);
+    if (!(rad > 0.0) || !__builtin_isfinite(rad)) return false;  // h == 0: r2 < 0 never holds
+    if (!__builtin_isfinite(x) || !__builtin_isfinite(y) || !__builtin_isfinite(z)) return false;
+    return axis_cells(x, rad, g.x_min, g.ipx, 0, g.nx - 1, b.i0, b.i1) &&
+           axis_cells(y, rad, g.y_min, g.ipy, 0, g.ny - 1, b.j0, b.j1) &&
+           axis_cells(z, rad, g.z_min, g.ipz, g.k_lo, g.k_lo + g.nzl - 1, b.k0, b.k1);
+}
+
+__device__ __forceinline__ void load3(const float* __restrict__ x, const float* __restrict__ y,
+                                      const float* __restrict__ z, const float* __restrict__ h,
+                                      long long p, long long p1, float& px, float& py, float& pz,
+                                      float& ph) {
+    bool in = p < p1;
+    px = in ? x[p] : 0.0f;
+    py = in ? y[p] : 0.0f;
+    pz = in ? z[p] : 0.0f;
+    ph = in ? h[p] : 0.0f;  // h = 0: no footprint
+}
+
+// ----------------------------------------------------------------------------------
+// C1: count insertions per (block, brick)
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(k3Block) void k3_count(const float* __restrict__ x,
+                                                    const float* __restrict__ y,
+                                                    const float* __restrict__ z,
+                                                    const float* __restrict__ h, long long n,
+                                                    long long per_block, Grid3 g,
+                                                    int* __restrict__ hist) {
+    extern __shared__ __attribute__((aligned(16))) int lh[];
+    for (int t = threadIdx.x; t < g.nb; t += k3Block) lh[t] = 0;
+    __syncthreads();
+    long long p0 = (long long)blockIdx.x * per_block;
+    long long p1 = min(n, p0 + per_block);
+    float cx, cy, cz, ch;
+    load3(x, y, z, h, p0 + threadIdx.x, p1, cx, cy, cz, ch);
+    for (long long base = p0; base < p1; base += k3Block) {
+        float nx_, ny_, nz_, nh_;
+        load3(x, y, z, h, base + k3Block + threadIdx.x, p1, nx_, ny_, nz_, nh_);
+        Box3 b;
+        if (footprint3(g, cx, cy, cz, ch, b)) {
+            int bi0 = b.i0 >> kBXs, bi1 = b.i1 >> kBXs, bj0 = b.j0 >> kBYs, bj1 = b.j1 >> kBYs;
+            int bk0 = (b.k0 - g.k_lo) >> kBZs, bk1 = (b.k1 - g.k_lo) >> kBZs;
+            for (int bi = bi0; bi <= bi1; ++bi)
+                for (int bj = bj0; bj <= bj1; ++bj)
+                    for (int bk = bk0; bk <= bk1; ++bk)
+                        atomicAdd(&lh[(bi * g.nby + bj) * g.nbz + bk], 1);
+        }
+        cx = nx_;
+        cy = ny_;
+        cz = nz_;
+        ch = nh_;
+    }
+    __syncthreads();
+    int* row = hist + (long long)blockIdx.x * g.nb;
+    for (int t = threadIdx.x; t < g.nb; t += k3Block) row[t] = lh[t];
+}
+
+// ----------------------------------------------------------------------------------
+// C3: scatter 32-byte records {x, y, z, h}, {a, 0, 0, 0} into the bricks' runs
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(k3Block) void k3_scatter(
+    const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
+    const float* __restrict__ h, const float* __restrict__ a, long long n, long long per_block,
+    Grid3 g, const int* __restrict__ hist, const long long* __restrict__ brick_start,
+    float4* __restrict__ recs) {
+    extern __shared__ __attribute__((aligned(16))) int cur[];
+    const int* row = hist + (long long)blockIdx.x * g.nb;
+    for (int t = threadIdx.x; t < g.nb; t += k3Block) cur[t] = (int)brick_start[t] + row[t];
+    __syncthreads();
+    long long p0 = (long long)blockIdx.x * per_block;
+    long long p1 = min(n, p0 + per_block);
+    float cx, cy, cz, ch, ca;
+    load3(x, y, z, h, p0 + threadIdx.x, p1, cx, cy, cz, ch);
+    ca = p0 + threadIdx.x < p1 ? a[p0 + threadIdx.x] : 0.0f;
+    for (long long base = p0; base < p1; base += k3Block) {
+        float nx_, ny_, nz_, nh_, na_;
+        long long q = base + k3Block + threadIdx.x;
+        load3(x, y, z, h, q, p1, nx_, ny_, nz_, nh_);
+        na_ = q < p1 ? a[q] : 0.0f;
+        Box3 b;
+        if (footprint3(g, cx, cy, cz, ch, b)) {
+            float4 r0 = make_float4(cx, cy, cz, ch), r1 = make_float4(ca, 0.0f, 0.0f, 0.0f);
+            int bi0 = b.i0 >> kBXs, bi1 = b.i1 >> kBXs, bj0 = b.j0 >> kBYs, bj1 = b.j1 >> kBYs;
+            int bk0 = (b.k0 - g.k_lo) >> kBZs, bk1 = (b.k1 - g.k_lo) >> kBZs;
+            for (int bi = bi0; bi <= bi1; ++bi)
+                for (int bj = bj0; bj <= bj1; ++bj)
+                    for (int bk = bk0; bk <= bk1; ++bk) {
+                        int slot = atomicAdd(&cur[(bi * g.nby + bj) * g.nbz + bk], 1);
+                        recs[2 * (long long)slot] = r0;
+                        recs[2 * (long long)slot + 1] = r1;
+                    }
+        }
+        cx = nx_;
+        cy = ny_;
+        cz = nz_;
+        ch = nh_;
+        ca = na_;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// C4: deposit one work item (a run of records of one brick) into the LDS brick
+// ----------------------------------------------------------------------------------
+struct Rec3 {
+    double x, y, z, thr;  // fp64 copies of the fp32 inputs; thr = (2h)^2 in fp64
+    float hinv, s;        // 1 / h, a * norm(h)
+    Box3 b;               // clipped to the brick, brick-local indices
+};
+
+template <int KID>
+__device__ __forceinline__ void pair3(const Rec3& R, int li, int lj, int lk, const double* xt,
+                                      const double* yt, const double* zt, double* acc) {
+    // .pyx:30-31 extended to 3-D; the oracle's voxel_pass, operation for operation
+    double dx = R.x - xt[li];
+    double dy = R.y - yt[lj];
+    double dz = R.z - zt[lk];
+    double r2 = dx * dx + dy * dy + dz * dz;
+    if (r2 < R.thr) {
+        float q = __builtin_amdgcn_sqrtf((float)r2) * R.hinv;
+        float w = kernel_shape<KID>(q);
+        atomicAdd(&acc[(li * kBY + lj) * kBZ + lk], (double)(R.s * w));
+    }
+}
+
+template <int KID>
+__global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __restrict__ recs,
+                                                      const Item* __restrict__ items,
+                                                      double* __restrict__ slabs,
+                                                      float* __restrict__ out, int accumulate) {
+    extern __shared__ __attribute__((aligned(16))) double acc[];
+    double* xt = acc + kBrickVox;
+    double* yt = xt + kBX;
+    double* zt = yt + kBY;
+    const Item it = items[blockIdx.x];
+    int bi = it.tile / (g.nby * g.nbz);
+    int rem = it.tile - bi * (g.nby * g.nbz);
+    int bj = rem / g.nbz, bk = rem - (rem / g.nbz) * g.nbz;
+    int I0 = bi * kBX, J0 = bj * kBY, K0 = g.k_lo + bk * kBZ;
+    int TW = min(kBX, g.nx - I0), TH = min(kBY, g.ny - J0), TD = min(kBZ, g.k_lo + g.nzl - K0);
+    auto out_index = [&](int v) -> long long {
+        int li = v >> (kBYs + kBZs), lj = (v >> kBZs) & (kBY - 1), lk = v & (kBZ - 1);
+        if (li >= TW || lj >= TH || lk >= TD) return -1;
+        return ((long long)(I0 + li) * g.ny + (J0 + lj)) * g.nzl + (K0 - g.k_lo + lk);
+    };
+    if (it.count == 0) {  // empty brick
+        if (accumulate) return;
+        for (int v = threadIdx.x; v < kBrickVox; v += k3Block) {
+            long long o = out_index(v);
+            if (o >= 0) out[o] = 0.0f;
+        }
+        return;
+    }
+    for (int v = threadIdx.x; v < kBrickVox; v += k3Block) acc[v] = 0.0;
+    if (threadIdx.x < kBX) xt[threadIdx.x] = g.x_min + (double)(I0 + (int)threadIdx.x) * g.px;
+    else if (threadIdx.x < kBX + kBY)
+        yt[threadIdx.x - kBX] = g.y_min + (double)(J0 + (int)threadIdx.x - kBX) * g.py;
+    else if (threadIdx.x < kBX + kBY + kBZ)
+        zt[threadIdx.x - kBX - kBY] = g.z_min + (double)(K0 + (int)threadIdx.x - kBX - kBY) * g.pz;
+    __syncthreads();
+    int lane = threadIdx.x & 63;
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
+    if ((int)threadIdx.x < it.count) {
+        r0 = recs[2 * (it.start + threadIdx.x)];
+        r1 = recs[2 * (it.start + threadIdx.x) + 1];
+    }
+    for (int base = 0; base < it.count; base += k3Block) {
+        int i = base + threadIdx.x;
+        float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0;
+        if (i + k3Block < it.count) {
+            n0 = recs[2 * (it.start + i + k3Block)];
+            n1 = recs[2 * (it.start + i + k3Block) + 1];
+        }
+        Rec3 R;
+        bool live = false;
+        if (i < it.count && footprint3(g, r0.x, r0.y, r0.z, r0.w, R.b)) {
+            R.b.i0 = max(R.b.i0, I0) - I0;
+            R.b.i1 = min(R.b.i1, I0 + TW - 1) - I0;
+            R.b.j0 = max(R.b.j0, J0) - J0;
+            R.b.j1 = min(R.b.j1, J0 + TH - 1) - J0;
+            R.b.k0 = max(R.b.k0, K0) - K0;
+            R.b.k1 = min(R.b.k1, K0 + TD - 1) - K0;
+            live = R.b.i0 <= R.b.i1 && R.b.j0 <= R.b.j1 && R.b.k0 <= R.b.k1;
+            R.x = r0.x;
+            R.y = r0.y;
+            R.z = r0.z;
+            double t = 2.0 * (double)r0.w;
+            R.thr = t * t;
+            R.hinv = 1.0f / r0.w;
+            R.s = (float)term_coef<KID>(r1.x, r0.w);
+        }
+        r0 = n0;
+        r1 = n1;
+        int bw = R.b.i1 - R.b.i0 + 1, bh = R.b.j1 - R.b.j0 + 1, bd = R.b.k1 - R.b.k0 + 1;
+        bool small = live && bw * bh * bd <= kSmallVox;
+        if (small) {
+            for (int li = R.b.i0; li <= R.b.i1; ++li)
+                for (int lj = R.b.j0; lj <= R.b.j1; ++lj)
+                    for (int lk = R.b.k0; lk <= R.b.k1; ++lk)
+                        pair3<KID>(R, li, lj, lk, xt, yt, zt, acc);
+        }
+        unsigned long long big = __ballot(live && !small);
+        while (big) {
+            int l = __builtin_ctzll(big);
+            big &= big - 1;
+            Rec3 Q;
+            Q.x = __shfl(R.x, l);
+            Q.y = __shfl(R.y, l);
+            Q.z = __shfl(R.z, l);
+            Q.thr = __shfl(R.thr, l);
+            Q.hinv = bcast(R.hinv, l);
+            Q.s = bcast(R.s, l);
+            Q.b.i0 = bcast(R.b.i0, l);
+            Q.b.j0 = bcast(R.b.j0, l);
+            Q.b.k0 = bcast(R.b.k0, l);
+            int qw = bcast(bw, l), qh = bcast(bh, l), qd = bcast(bd, l);
+            // Lanes walk the flattened box (k fastest) in steps of 64 with a mixed-radix
+            // increment: no division inside the loop.
+            int plane = qh * qd, vol = qw * plane;
+            int dk = 64 % qd, dj = (64 / qd) % qh, di = 64 / plane;
+            int ci = lane / plane, rr = lane - ci * plane;
+            int cj = rr / qd, ck = rr - cj * qd;
+            for (int v = lane; v < vol; v += 64) {
+                pair3<KID>(Q, Q.b.i0 + ci, Q.b.j0 + cj, Q.b.k0 + ck, xt, yt, zt, acc);
+                ck += dk;
+                if (ck >= qd) { ck -= qd; ++cj; }
+                cj += dj;
+                if (cj >= qh) { cj -= qh; ++ci; }
+                ci += di;
+            }
+        }
+    }
+    __syncthreads();
+    if (it.slab >= 0) {
+        double* dst = slabs + (long long)it.slab * kBrickVox;
+        for (int v = threadIdx.x; v < kBrickVox; v += k3Block) dst[v] = acc[v];
+        return;
+    }
+    for (int v = threadIdx.x; v < kBrickVox; v += k3Block) {
+        long long o = out_index(v);
+        if (o < 0) continue;
+        float val = (float)acc[v];
+        out[o] = accumulate ? out[o] + val : val;
+    }
+}
+
+// C5: bricks split over several items -- fp64 sum of their slabs in slab order.
+__global__ __launch_bounds__(k3Block) void k3_merge(Grid3 g, const Merge* __restrict__ merges,
+                                                    const double* __restrict__ slabs,
+                                                    float* __restrict__ out, int accumulate) {
+    const Merge m = merges[blockIdx.x];
+    int bi = m.tile / (g.nby * g.nbz);
+    int rem = m.tile - bi * (g.nby * g.nbz);
+    int bj = rem / g.nbz, bk = rem - (rem / g.nbz) * g.nbz;
+    int I0 = bi * kBX, J0 = bj * kBY, K0 = g.k_lo + bk * kBZ;
+    int TW = min(kBX, g.nx - I0), TH = min(kBY, g.ny - J0), TD = min(kBZ, g.k_lo + g.nzl - K0);
+    for (int v = threadIdx.x; v < kBrickVox; v += k3Block) {
+        int li = v >> (kBYs + kBZs), lj = (v >> kBZs) & (kBY - 1), lk = v & (kBZ - 1);
+        if (li >= TW || lj >= TH || lk >= TD) continue;
+        double s = 0.0;
+        for (int j = 0; j < m.nslab; ++j) s += slabs[(long long)(m.slab0 + j) * kBrickVox + v];
+        long long o = ((long long)(I0 + li) * g.ny + (J0 + lj)) * g.nzl + (K0 - g.k_lo + lk);
+        float val = (float)s;
+        out[o] = accumulate ? out[o] + val : val;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// Host side
+// ----------------------------------------------------------------------------------
+static uint32_t spread3(uint32_t v) {  // 10 bits -> every third bit
+    v &= 0x3ff;
+    v = (v | (v << 16)) & 0x030000ff;
+    v = (v | (v << 8)) & 0x0300f00f;
+    v = (v | (v << 4)) & 0x030c30c3;
+    v = (v | (v << 2)) & 0x09249249;
+    return v;
+}
+
+static int ensure_morton3(Workspace& ws, const Grid3& g, hipStream_t st) {
+    if (ws.morton3_key[0] == g.nbx && ws.morton3_key[1] == g.nby && ws.morton3_key[2] == g.nbz)
+        return ASP_OK;
+    std::vector<std::pair<uint32_t, int>> key((size_t)g.nb);
+    for (int bi = 0; bi < g.nbx; ++bi)
+        for (int bj = 0; bj < g.nby; ++bj)
+            for (int bk = 0; bk < g.nbz; ++bk) {
+                int t = (bi * g.nby + bj) * g.nbz + bk;
+                key[t] = {spread3(bi) << 2 | spread3(bj) << 1 | spread3(bk), t};
+            }
+    std::sort(key.begin(), key.end());
+    std::vector<int> order(key.size());
+    for (size_t i = 0; i < key.size(); ++i) order[i] = key[i].second;
+    ASP_TRY(ensure(ws.morton3, order.size() * sizeof(int)));
+    ASP_HIP(hipMemcpyAsync(ws.morton3.p, order.data(), order.size() * sizeof(int),
+                           hipMemcpyHostToDevice, st));
+    ASP_HIP(hipStreamSynchronize(st));
+    ws.morton3_key[0] = g.nbx;
+    ws.morton3_key[1] = g.nby;
+    ws.morton3_key[2] = g.nbz;
+    return ASP_OK;
+}
+
+static bool make_grid3(const double* ext, int nx, int ny, int nz, int k_lo, int k_hi,
+                       Grid3& g) {
+    if (!(nx > 0 && ny > 0 && nz > 0) || k_lo < 0 || k_hi > nz || k_lo >= k_hi) return false;
+    for (int a = 0; a < 3; ++a)
+        if (!std::isfinite(ext[2 * a]) || !std::isfinite(ext[2 * a + 1]) ||
+            !(ext[2 * a + 1] > ext[2 * a]))
+            return false;
+    g.x_min = ext[0];
+    g.y_min = ext[2];
+    g.z_min = ext[4];
+    g.px = (ext[1] - ext[0]) / nx;
+    g.py = (ext[3] - ext[2]) / ny;
+    g.pz = (ext[5] - ext[4]) / nz;
+    if (!(g.px > 0.0 && g.py > 0.0 && g.pz > 0.0)) return false;
+    g.ipx = 1.0 / g.px;
+    g.ipy = 1.0 / g.py;
+    g.ipz = 1.0 / g.pz;
+    if (!std::isfinite(g.ipx) || !std::isfinite(g.ipy) || !std::isfinite(g.ipz)) return false;
+    g.nx = nx;
+    g.ny = ny;
+    g.nz = nz;
+    g.k_lo = k_lo;
+    g.nzl = k_hi - k_lo;
+    g.nbx = (nx + kBX - 1) / kBX;
+    g.nby = (ny + kBY - 1) / kBY;
+    g.nbz = (g.nzl + kBZ - 1) / kBZ;
+    long long nb = (long long)g.nbx * g.nby * g.nbz;
+    g.nb = nb > kMaxBricks ? -1 : (int)nb;
+    return true;
+}
+
+static int project3d(const float* x, const float* y, const float* z, const float* h,
+                     const float* a, long long n, const double* ext, int nx, int ny, int nz,
+                     int k_lo, int k_hi, int kid, int flags, float* out, int device,
+                     void* stream) {
+    if (n < 0) return fail(ASP_ERR_INVALID, "n < 0");
+    if (kid < 0 || kid > 2) return fail(ASP_ERR_INVALID, "unknown kernel_id");
+    if (!out) return fail(ASP_ERR_INVALID, "out is NULL");
+    if (flags & ~(ASP_F_DEVICE_PTRS | ASP_F_ACCUMULATE))
+        return fail(ASP_ERR_UNSUPPORTED, "asp_project3d supports ASP_F_DEVICE_PTRS and "
+                                         "ASP_F_ACCUMULATE only");
+    if (n > 0 && (!x || !y || !z || !h || !a)) return fail(ASP_ERR_INVALID, "NULL particle array");
+    if (n > 0x7fffffffLL) return fail(ASP_ERR_UNSUPPORTED, "n >= 2^31 particles per call");
+    Grid3 g;
+    if (!make_grid3(ext, nx, ny, nz, k_lo, k_hi, g))
+        return fail(ASP_ERR_INVALID,
+                    "invalid cube: need nx, ny, nz >= 1, 0 <= k_lo < k_hi <= nz and finite "
+                    "max > min on every axis");
+    if (g.nb < 0)
+        return fail(ASP_ERR_UNSUPPORTED, "cube slab too large for one call (more than 16384 "
+                                         "16x16x32 bricks): split the planes [k_lo, k_hi)");
+    if (device < 0 || device >= 64) return fail(ASP_ERR_INVALID, "bad device");
+    int ndev = 0;
+    ASP_HIP(hipGetDeviceCount(&ndev));
+    if (device >= ndev) return fail(ASP_ERR_INVALID, "device index out of range");
+    ASP_HIP(hipSetDevice(device));
+    Workspace& ws = g_ws[device];
+    std::lock_guard<std::mutex> lock(ws.mu);
+    hipStream_t st = (hipStream_t)stream;
+    const bool dev = flags & ASP_F_DEVICE_PTRS;
+    const int acc = (flags & ASP_F_ACCUMULATE) ? 1 : 0;
+    const long long nvox = (long long)nx * ny * g.nzl;
+    const float *dx = x, *dy = y, *dz = z, *dh = h, *da = a;
+    float* dout = out;
+    if (!dev) {
+        const float* src[5] = {x, y, z, h, a};
+        for (int k = 0; k < 5; ++k) {
+            ASP_TRY(ensure(ws.in[k], (size_t)n * sizeof(float)));
+            if (n > 0)
+                ASP_HIP(hipMemcpyAsync(ws.in[k].p, src[k], (size_t)n * sizeof(float),
+                                       hipMemcpyHostToDevice, st));
+        }
+        dx = (const float*)ws.in[0].p;
+        dy = (const float*)ws.in[1].p;
+        dz = (const float*)ws.in[2].p;
+        dh = (const float*)ws.in[3].p;
+        da = (const float*)ws.in[4].p;
+        ASP_TRY(ensure(ws.out[0], (size_t)nvox * sizeof(float)));
+        dout = (float*)ws.out[0].p;
+        if (acc)
+            ASP_HIP(hipMemcpyAsync(dout, out, nvox * sizeof(float), hipMemcpyHostToDevice, st));
+    }
+    if (ws.prof) ASP_TRY(prof_fold(ws));
+    long long n_recs = 0;
+    int n_items = 0, n_merges = 0, n_slabs = 0;
+    if (n == 0) {
+        if (!acc) {
+            StageMark m(ws, kSMemset, st);
+            ASP_HIP(hipMemsetAsync(dout, 0, nvox * sizeof(float), st));
+            m.done();
+        }
+    } else {
+        ASP_TRY(ensure_morton3(ws, g, st));
+        long long nblk = std::min<long long>(512, std::max<long long>(1, (n + 8191) / 8192));
+        long long per_block = (n + nblk - 1) / nblk;
+        nblk = (n + per_block - 1) / per_block;
+        ASP_TRY(ensure(ws.hist, (size_t)nblk * g.nb * sizeof(int)));
+        ASP_TRY(ensure(ws.tile_total, (size_t)g.nb * sizeof(int)));
+        ASP_TRY(ensure(ws.tile_start, (size_t)g.nb * sizeof(long long)));
+        ASP_TRY(ensure(ws.items, (size_t)(g.nb + kTargetItems + 16) * sizeof(Item)));
+        ASP_TRY(ensure(ws.merges, (size_t)(g.nb + 16) * sizeof(Merge)));
+        ASP_TRY(ensure(ws.counters, cNum * sizeof(int)));
+        if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, cNum * sizeof(int)));
+        int* dc = (int*)ws.counters.p;
+        ASP_HIP(hipMemsetAsync(dc, 0, cNum * sizeof(int), st));
+        const size_t lds_bins = (size_t)g.nb * sizeof(int);
+        {
+            StageMark m(ws, kS3Count, st);
+            hipLaunchKernelGGL(k3_count, dim3((unsigned)nblk), dim3(k3Block), lds_bins, st, dx, dy,
+                               dz, dh, n, per_block, g, (int*)ws.hist.p);
+            ASP_LAUNCHED();
+            m.done();
+        }
+        {
+            StageMark m(ws, kS3Colscan, st);
+            hipLaunchKernelGGL(k_colscan, dim3((g.nb + 63) / 64), dim3(kBlock), 0, st,
+                               (int*)ws.hist.p, (int)nblk, g.nb, (int*)ws.tile_total.p);
+            ASP_LAUNCHED();
+            m.done();
+        }
+        {
+            StageMark m(ws, kS3Tilescan, st);
+            hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(kScanThreads), 0, st,
+                               (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb,
+                               (long long*)ws.tile_start.p, (Item*)ws.items.p,
+                               (Merge*)ws.merges.p, dc);
+            ASP_LAUNCHED();
+            m.done();
+        }
+        ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, cNum * sizeof(int), hipMemcpyDeviceToHost, st));
+        ASP_HIP(hipStreamSynchronize(st));
+        n_items = ws.h_counters[cItems];
+        n_recs = ws.h_counters[cRecs];
+        n_slabs = ws.h_counters[cSlabs];
+        n_merges = ws.h_counters[cMerges];
+        if (n_recs >= 0x7fffffffLL)
+            return fail(ASP_ERR_UNSUPPORTED, "more than 2^31 particle-brick records");
+        ASP_TRY(ensure(ws.recs, (size_t)n_recs * 2 * sizeof(float4)));
+        ASP_TRY(ensure(ws.slabs, (size_t)n_slabs * kBrickVox * sizeof(double)));
+        {
+            StageMark m(ws, kS3Scatter, st);
+            hipLaunchKernelGGL(k3_scatter, dim3((unsigned)nblk), dim3(k3Block), lds_bins, st, dx,
+                               dy, dz, dh, da, n, per_block, g, (const int*)ws.hist.p,
+                               (const long long*)ws.tile_start.p, (float4*)ws.recs.p);
+            ASP_LAUNCHED();
+            m.done();
+        }
+        {
+            StageMark m(ws, kS3Deposit, st);
+            size_t lds = (size_t)kBrickVox * sizeof(double) + (kBX + kBY + kBZ) * sizeof(double);
+            auto kern = kid == 0 ? k3_deposit<0> : kid == 1 ? k3_deposit<1> : k3_deposit<2>;
+            hipLaunchKernelGGL(kern, dim3(n_items), dim3(k3Block), lds, st, g,
+                               (const float4*)ws.recs.p, (const Item*)ws.items.p,
+                               (double*)ws.slabs.p, dout, acc);
+            ASP_LAUNCHED();
+            m.done();
+        }
+        if (n_merges > 0) {
+            StageMark m(ws, kS3Merge, st);
+            hipLaunchKernelGGL(k3_merge, dim3(n_merges), dim3(k3Block), 0, st, g,
+                               (const Merge*)ws.merges.p, (const double*)ws.slabs.p, dout, acc);
+            ASP_LAUNCHED();
+            m.done();
+        }
+    }
+    if (!dev) {
+        ASP_HIP(hipMemcpyAsync(out, dout, nvox * sizeof(float), hipMemcpyDeviceToHost, st));
+        ASP_HIP(hipStreamSynchronize(st));
+    }
+    ws.stats[0] = n_recs;
+    ws.stats[1] = n_items;
+    ws.stats[2] = 0;
+    ws.stats[3] = kBrickVox;
+    ws.stats[4] = g.nb;
+    ws.stats[5] = n > 0 ? ws.h_counters[cChunk] : 0;
+    ws.stats[6] = n_merges;
+    ws.stats[7] = n_slabs;
+    return ASP_OK;
+}
+
+}  // namespace asp
+
+using namespace asp;
+
+extern "C" int asp_project3d(const float* x, const float* y, const float* z, const float* h,
+                             const float* a, int64_t n, double x_min, double x_max, double y_min,
+                             double y_max, double z_min, double z_max, int32_t nx, int32_t ny,
+                             int32_t nz, int32_t k_lo, int32_t k_hi, int32_t kernel_id,
+                             int32_t flags, float* out, int32_t device, void* stream) {
+    t_err.clear();
+    const double ext[6] = {x_min, x_max, y_min, y_max, z_min, z_max};
+    return project3d(x, y, z, h, a, n, ext, nx, ny, nz, k_lo, k_hi, kernel_id, flags, out, device,
+                     stream);
+}

@@ -87,6 +87,25 @@ int asp_project2d(const float *u, const float *v, const float *h, const float *a
                   int32_t flags, float *out0, float *out1, int32_t device, void *stream);
 
 /*
+ * 3-D voxel cube (build-defined; SURVEY.md §8(a) "512^3 cube" -- no reference
+ * counterpart, it extends create_image's pixel semantics (_pixel_calculations.pyx:11-14,
+ * :30-34) to voxels; CPU restatement: oracle/asp_oracle.c oracle_project3d):
+ *
+ *   out[i, j, k - k_lo] = sum_p a[p] * W(r_p, h_p)  over p with r_p^2 < (2 h_p)^2,
+ *   r_p^2 = ((x_p - X_i)^2 + (y_p - Y_j)^2) + (z_p - Z_k)^2   (fp64, bit-exact sets),
+ *   X_i = x_min + i * (x_max - x_min)/nx, Y_j and Z_k likewise with ny and nz.
+ *
+ * Only planes k_lo <= k < k_hi are produced (Z-slab ownership across GPUs); out is
+ * (nx, ny, k_hi - k_lo) C-order float32.  At most 16384 bricks of 16x16x32 voxels per
+ * call (a whole 512^3 cube fits).  flags: ASP_F_DEVICE_PTRS, ASP_F_ACCUMULATE.
+ */
+int asp_project3d(const float *x, const float *y, const float *z, const float *h,
+                  const float *a, int64_t n, double x_min, double x_max, double y_min,
+                  double y_max, double z_min, double z_max, int32_t nx, int32_t ny, int32_t nz,
+                  int32_t k_lo, int32_t k_hi, int32_t kernel_id, int32_t flags, float *out,
+                  int32_t device, void *stream);
+
+/*
  * Kernel evaluation on the device: replaces quartic_spline_kernel(r, h)
  * (_kernels.pyx:9-20) for kernel_id 0; fp64 in and out, same formula and branch order.
  * Host pointers unless ASP_F_DEVICE_PTRS.
@@ -141,7 +160,8 @@ int asp_last_stats(int32_t device, int64_t *stats, int32_t nstats);
  * (enable != 0 starts and resets, 0 stops).  asp_profile_read returns, per stage, the
  * summed milliseconds and the number of launches since the last reset.  Stages:
  * 0 memset, 1 count, 2 colscan, 3 tilescan, 4 scatter, 5 scale, 6 deposit, 7 merge,
- * 8 wide, 9 ratio.
+ * 8 wide, 9 ratio; cube (asp_project3d): 10 count, 11 colscan, 12 tilescan, 13 scatter,
+ * 14 deposit, 15 merge.
  */
 int asp_profile(int32_t device, int32_t enable);
 int asp_profile_read(int32_t device, double *ms_sum, int64_t *launches, int32_t nstages);

@@ -398,3 +398,127 @@ void oracle_chunk_ranges(const double *u, const double *v, const double *h, int6
         cx0[p] = a; cx1[p] = b; cy0[p] = c; cy1[p] = d;
     }
 }
+
+/* ==================================================================================
+ * 3-D density cube (build-defined; SURVEY.md §8(a) "512^3 cube" -- the reference has no
+ * volumetric path, so this restatement IS the definition and parity is pinned by it
+ * alone).  It extends the 2-D pixel semantics (.pyx:11-14, :30-34) to voxels:
+ *   X_i = x_min + i * ((x_max - x_min) / nx), likewise Y_j (ny) and Z_k (nz) -- each axis
+ *         with its own pitch (the 2-D S2 quirk is a reference bug, not carried over);
+ *   r2  = ((x - X_i)^2 + (y - Y_j)^2) + (z - Z_k)^2, fp64, left to right;
+ *   voxel (i, j, k) sees particle p iff r2 < (2 h)^2 (strict, as .pyx:31);
+ *   cube[i, j, k - k_lo] = sum_p a_p W(sqrt(r2), h_p)   for planes k_lo <= k < k_hi,
+ * with the same kernels as the map (3-D normalisation, so the cube of A = m is the SPH
+ * density field sampled at voxel corners).  Layout (nx, ny, k_hi - k_lo) C-order.
+ * ================================================================================== */
+typedef struct {
+    double x_min, y_min, z_min, px, py, pz;
+    int nx, ny, nz;
+} grid3_t;
+
+static grid3_t make_grid3(int nx, int ny, int nz, double x_min, double x_max, double y_min,
+                          double y_max, double z_min, double z_max)
+{
+    grid3_t g;
+    g.x_min = x_min; g.y_min = y_min; g.z_min = z_min;
+    g.px = (x_max - x_min) / nx;
+    g.py = (y_max - y_min) / ny;
+    g.pz = (z_max - z_min) / nz;
+    g.nx = nx; g.ny = ny; g.nz = nz;
+    return g;
+}
+
+static int voxel_pass(const grid3_t *g, double x, double y, double z, double h, int i, int j,
+                      int k, double *r2_out)
+{
+    double dx = x - (g->x_min + (double)i * g->px);
+    double dy = y - (g->y_min + (double)j * g->py);
+    double dz = z - (g->z_min + (double)k * g->pz);
+    double r2 = dx * dx + dy * dy + dz * dz;
+    double t = 2.0 * h;
+    *r2_out = r2;
+    return r2 < t * t;
+}
+
+/* Candidate index range along one axis (a superset: one cell of slack each side). */
+static int axis_cells(double w, double rad, double w_min, double pitch, int lo, int hi,
+                      int *a, int *b)
+{
+    double f0 = floor((w - rad - w_min) / pitch) - 1, f1 = ceil((w + rad - w_min) / pitch) + 1;
+    if (!(f1 >= lo && f0 <= hi))
+        return 0;
+    *a = f0 < lo ? lo : (int)f0;
+    *b = f1 > hi ? hi : (int)f1;
+    return 1;
+}
+
+/* O(pairs) scatter; threads own disjoint bands of x planes (deterministic).  Terms are
+ * added in particle order per voxel. */
+int oracle_project3d(const double *x, const double *y, const double *z, const double *h,
+                     const double *A, int64_t n, int nx, int ny, int nz, int k_lo, int k_hi,
+                     double x_min, double x_max, double y_min, double y_max, double z_min,
+                     double z_max, int kid, int nthreads, double *out)
+{
+    if (nx <= 0 || ny <= 0 || nz <= 0 || k_lo < 0 || k_hi > nz || k_lo >= k_hi)
+        return -1;
+    grid3_t g = make_grid3(nx, ny, nz, x_min, x_max, y_min, y_max, z_min, z_max);
+    int nzl = k_hi - k_lo;
+    memset(out, 0, sizeof(double) * (size_t)nx * ny * nzl);
+    int nt = 1;
+#ifdef _OPENMP
+    nt = nthreads > 0 ? nthreads : omp_get_max_threads();
+#else
+    (void)nthreads;
+#endif
+    int nband = nt * 4 < nx ? nt * 4 : nx;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+    for (int b = 0; b < nband; ++b) {
+        int bx0 = (int)((int64_t)nx * b / nband), bx1 = (int)((int64_t)nx * (b + 1) / nband);
+        for (int64_t p = 0; p < n; ++p) {
+            double hp = h[p], t = 2.0 * hp;
+            if (!(t * t > 0.0))
+                continue;
+            double rad = fabs(t);
+            int i0, i1, j0, j1, k0, k1;
+            if (!axis_cells(x[p], rad, x_min, g.px, bx0, bx1 - 1, &i0, &i1) ||
+                !axis_cells(y[p], rad, y_min, g.py, 0, ny - 1, &j0, &j1) ||
+                !axis_cells(z[p], rad, z_min, g.pz, k_lo, k_hi - 1, &k0, &k1))
+                continue;
+            for (int i = i0; i <= i1; ++i)
+                for (int j = j0; j <= j1; ++j)
+                    for (int k = k0; k <= k1; ++k) {
+                        double r2;
+                        if (voxel_pass(&g, x[p], y[p], z[p], hp, i, j, k, &r2))
+                            out[((int64_t)i * ny + j) * nzl + (k - k_lo)] +=
+                                A[p] * kernel_w(kid, sqrt(r2), hp);
+                    }
+        }
+    }
+    return 0;
+}
+
+/* Neighbour CSR for a list of voxels (id = (i * ny + j) * nz + k), ascending particle
+ * indices, brute force over all particles.  Returns total or -needed. */
+int64_t oracle_voxel_neighbours(const double *x, const double *y, const double *z,
+                                const double *h, int64_t n, int nx, int ny, int nz,
+                                double x_min, double x_max, double y_min, double y_max,
+                                double z_min, double z_max, const int64_t *vox, int64_t nvox,
+                                int64_t *offsets, int32_t *index, int64_t cap)
+{
+    grid3_t g = make_grid3(nx, ny, nz, x_min, x_max, y_min, y_max, z_min, z_max);
+    int64_t t = 0;
+    offsets[0] = 0;
+    for (int64_t q = 0; q < nvox; ++q) {
+        int k = (int)(vox[q] % nz), j = (int)((vox[q] / nz) % ny), i = (int)(vox[q] / nz / ny);
+        for (int64_t p = 0; p < n; ++p) {
+            double r2;
+            if (voxel_pass(&g, x[p], y[p], z[p], h[p], i, j, k, &r2)) {
+                if (t < cap)
+                    index[t] = (int32_t)p;
+                ++t;
+            }
+        }
+        offsets[q + 1] = t;
+    }
+    return t <= cap ? t : -t;
+}

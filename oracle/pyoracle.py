@@ -56,6 +56,13 @@ def lib():
         L.oracle_chunk_ranges.argtypes = [_d, _d, _d, C.c_int64, C.c_int, C.c_int, C.c_int,
                                           C.c_double, C.c_double, C.c_double, C.c_double,
                                           _i32, _i32, _i32, _i32]
+        L.oracle_project3d.argtypes = [_d, _d, _d, _d, _d, C.c_int64, C.c_int, C.c_int, C.c_int,
+                                       C.c_int, C.c_int] + [C.c_double] * 6 + [C.c_int, C.c_int,
+                                                                                _d]
+        L.oracle_voxel_neighbours.argtypes = [_d, _d, _d, _d, C.c_int64, C.c_int, C.c_int,
+                                              C.c_int] + [C.c_double] * 6 + [_i64, C.c_int64,
+                                                                            _i64, _i32, C.c_int64]
+        L.oracle_voxel_neighbours.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -158,3 +165,34 @@ def chunk_ranges(u, v, h, image_size, chunk_size, x_min, x_max, y_min, y_max):
                               int(chunk_size), float(x_min), float(x_max), float(y_min),
                               float(y_max), *[_p(o, _i32) for o in out])
     return tuple(out)
+
+
+def project3d(x, y, z, h, a, cube_size, extent, kernel="cubic", planes=None, nthreads=0):
+    """Cube restatement (scatter, fp64): (nx, ny, k_hi - k_lo) float64.
+    ``extent = (x_min, x_max, y_min, y_max, z_min, z_max)``."""
+    x, y, z, h, a = (_f64(t) for t in (x, y, z, h, a))
+    nx, ny, nz = (int(c) for c in cube_size)
+    k_lo, k_hi = (0, nz) if planes is None else (int(planes[0]), int(planes[1]))
+    out = np.empty((nx, ny, k_hi - k_lo), np.float64)
+    rc = lib().oracle_project3d(_p(x), _p(y), _p(z), _p(h), _p(a), x.size, nx, ny, nz, k_lo,
+                                k_hi, *[float(e) for e in extent], KERNELS[kernel],
+                                int(nthreads), _p(out))
+    if rc != 0:
+        raise RuntimeError(f"oracle_project3d failed ({rc})")
+    return out
+
+
+def voxel_neighbours(x, y, z, h, cube_size, extent, voxels):
+    x, y, z, h = (_f64(t) for t in (x, y, z, h))
+    vox = np.ascontiguousarray(voxels, dtype=np.int64)
+    offs = np.zeros(vox.size + 1, np.int64)
+    cap = max(1, x.size)
+    while True:
+        idx = np.empty(cap, np.int32)
+        t = lib().oracle_voxel_neighbours(_p(x), _p(y), _p(z), _p(h), x.size,
+                                          *[int(c) for c in cube_size],
+                                          *[float(e) for e in extent], _p(vox, _i64), vox.size,
+                                          _p(offs, _i64), _p(idx, _i32), cap)
+        if t >= 0:
+            return offs, idx[:t]
+        cap = -t

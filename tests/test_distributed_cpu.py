@@ -101,3 +101,63 @@ def test_zslab_sharded_sum_world2():
         np.testing.assert_allclose(out[r]["reduce_scatter"][0], full0[rows], atol=tol, rtol=0)
     # the slabs really are partial maps: neither rank alone holds the full map
     assert not np.allclose(out[1]["reduce"][0], full0, atol=tol)
+
+
+# --------------------------------------------------------------------------- 3-D cube
+CUBE = (16, 12, 20)
+CEXT = (-2.0, 2.0, -2.0, 2.0, -2.0, 2.0)
+
+
+def _oracle_cube(x, y, z, h, a, *, cube_size, extent, kernel, planes):
+    import pyoracle
+    o = pyoracle.project3d(x.numpy(), y.numpy(), z.numpy(), h.numpy(), a.numpy(), cube_size,
+                           extent, kernel=kernel, planes=planes)
+    return torch.from_numpy(o.astype(np.float32))
+
+
+def _cube_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, PKG_ROOT)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from asp_amd.distributed import project3d_sharded
+        x, y, z, h, m, T = _data()
+        # an arbitrary (not Z-sorted) input split, as an MPI-split reader would give
+        keep = (torch.arange(x.numel()) % world) == rank
+        sl = [t[keep].contiguous() for t in (x, y, z, h, m)]
+        slab = project3d_sharded(*sl, cube_size=CUBE, extent=CEXT, kernel="wendland_c2",
+                                 projector=_oracle_cube)
+        full = project3d_sharded(*sl, cube_size=CUBE, extent=CEXT, kernel="wendland_c2",
+                                 gather="all", projector=_oracle_cube)
+        q.put((rank, {"slab": slab.numpy().copy(), "full": full.numpy().copy()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cube_plane_slabs_halo_exchange_world2():
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    from asp_amd.distributed import plane_slabs
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cube_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    x, y, z, h, m, T = _data()
+    ref = pyoracle.project3d(x.numpy(), y.numpy(), z.numpy(), h.numpy(), m.numpy(), CUBE, CEXT,
+                             kernel="wendland_c2").astype(np.float32)
+    K = plane_slabs(CUBE[2], world)
+    tol = 1e-6 * np.abs(ref).max()
+    for r in range(world):
+        np.testing.assert_allclose(out[r]["slab"], ref[:, :, K[r]:K[r + 1]], atol=tol, rtol=1e-6)
+        np.testing.assert_allclose(out[r]["full"], ref, atol=tol, rtol=1e-6)
