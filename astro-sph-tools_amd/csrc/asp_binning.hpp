@@ -69,10 +69,17 @@ static __global__ __launch_bounds__(kBlock) void k_colscan(int* __restrict__ his
 // K2b: single workgroup.  Tile start offsets in Morton order of the tiles (spatially
 // adjacent tiles' records are adjacent in HBM), the deposit work list (also Morton
 // order: every tile gets >= 1 item, empty tiles a zero item) and the merge list.
+//
+// nstream = 2 (2-D map): column t + ntiles of tile_total holds tile t's NON-SMALL records
+// (clipped box wider than 4 x 4 pixels), stored right after its small-record run and
+// handed out in items of their own (Item::mode = 1, row-band deposit), chunked
+// independently: each stream aims at its own item count.
 // ----------------------------------------------------------------------------------
 constexpr int kScanThreads = 1024;
 constexpr int kTargetItems = 2048;
 constexpr int kMinItemRecords = 2048;
+constexpr int kTargetItems1 = 4096;    // mode-1 items (a record there costs ~10-1000x)
+constexpr int kMinItemRecords1 = 256;
 
 static __device__ __forceinline__ void block_scan_ll(long long* s, int tid) {
     for (int o = 1; o < kScanThreads; o <<= 1) {
@@ -83,36 +90,54 @@ static __device__ __forceinline__ void block_scan_ll(long long* s, int tid) {
     }
 }
 
-static __global__ __launch_bounds__(kScanThreads) void k_tilescan(const int* __restrict__ tile_total,
-                                                           const int* __restrict__ morton,
-                                                           int ntiles,
-                                                           long long* __restrict__ tile_start,
-                                                           Item* __restrict__ items,
-                                                           Merge* __restrict__ merges,
-                                                           int* __restrict__ ctr) {
+// items of one tile: regular ones of ch records, large ones of chl records
+static __device__ __forceinline__ void tile_items(int cs, int cl, int ch, int chl, int& ks,
+                                                  int& kl) {
+    ks = cs > 0 ? (cs + ch - 1) / ch : 0;
+    kl = cl > 0 ? (cl + chl - 1) / chl : 0;
+    if (ks + kl == 0) ks = 1;  // empty tile: one zero item writes the zeros
+}
+
+static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
+    const int* __restrict__ tile_total, const int* __restrict__ morton, int ntiles, int nstream,
+    long long* __restrict__ tile_start, Item* __restrict__ items, Merge* __restrict__ merges,
+    int* __restrict__ ctr) {
     __shared__ long long s_rec[kScanThreads], s_item[kScanThreads], s_slab[kScanThreads],
         s_merge[kScanThreads];
     int tid = threadIdx.x;
     int per = (ntiles + kScanThreads - 1) / kScanThreads;
     int r0 = min(ntiles, tid * per), r1 = min(ntiles, r0 + per);
-    long long loc = 0;
-    for (int r = r0; r < r1; ++r) loc += tile_total[morton[r]];
+    auto large = [&](int t) { return nstream == 2 ? tile_total[t + ntiles] : 0; };
+    long long loc = 0, wloc = 0;  // all records; stream-1 records
+    for (int r = r0; r < r1; ++r) {
+        int t = morton[r];
+        loc += tile_total[t] + large(t);
+        wloc += large(t);
+    }
     s_rec[tid] = loc;
+    s_item[tid] = wloc;
     __syncthreads();
     block_scan_ll(s_rec, tid);
+    block_scan_ll(s_item, tid);
     long long total = s_rec[kScanThreads - 1];
+    long long total1 = s_item[kScanThreads - 1];
     long long base = s_rec[tid] - loc;
-    int ch = (int)max((long long)kMinItemRecords, (total + kTargetItems - 1) / kTargetItems);
+    int ch = (int)max((long long)kMinItemRecords,
+                      (total - total1 + kTargetItems - 1) / kTargetItems);
+    int chl = (int)max((long long)kMinItemRecords1, (total1 + kTargetItems1 - 1) / kTargetItems1);
+    __syncthreads();
     long long nit = 0, nsl = 0, nmg = 0;
     for (int r = r0; r < r1; ++r) {
         int t = morton[r];
-        int c = tile_total[t];
+        int cs = tile_total[t], cl = large(t);
         tile_start[t] = base;
-        base += c;
-        int k = c > 0 ? (c + ch - 1) / ch : 1;
-        nit += k;
-        if (k > 1) {
-            nsl += k;
+        if (nstream == 2) tile_start[t + ntiles] = base + cs;
+        base += cs + cl;
+        int ks, kl;
+        tile_items(cs, cl, ch, chl, ks, kl);
+        nit += ks + kl;
+        if (ks + kl > 1) {
+            nsl += ks + kl;
             nmg += 1;
         }
     }
@@ -126,16 +151,21 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(const int* __r
     long long ib = s_item[tid] - nit, sb = s_slab[tid] - nsl, mb = s_merge[tid] - nmg;
     for (int r = r0; r < r1; ++r) {
         int t = morton[r];
-        int c = tile_total[t];
-        int k = c > 0 ? (c + ch - 1) / ch : 1;
+        int cs = tile_total[t], cl = large(t);
+        int ks, kl;
+        tile_items(cs, cl, ch, chl, ks, kl);
+        int k = ks + kl;
         long long s0 = tile_start[t];
         for (int j = 0; j < k; ++j) {
             Item it;
-            it.start = s0 + (long long)j * ch;
+            bool lg = j >= ks;
+            int jj = lg ? j - ks : j;
+            int c = lg ? cl : cs, chunk = lg ? chl : ch;
+            it.start = (lg ? s0 + cs : s0) + (long long)jj * chunk;
             it.tile = t;
-            it.count = c > 0 ? min(ch, c - j * ch) : 0;
+            it.count = c > 0 ? min(chunk, c - jj * chunk) : 0;
             it.slab = k > 1 ? (int)(sb + j) : -1;
-            it.pad = 0;
+            it.mode = lg ? 1 : 0;
             items[ib + j] = it;
         }
         ib += k;

@@ -30,7 +30,10 @@ constexpr int kBlock = 256;        // threads per workgroup for streaming kernel
 constexpr int kDepBlock = 512;     // deposit workgroup (8 waves; 2 per CU at 64 KiB LDS)
 constexpr int kTile = 64;          // GPU tile edge in pixels
 constexpr int kTileShift = 6;
-constexpr int kWideTiles = 64;     // particles overlapping more GPU tiles take the wide path
+#ifndef ASP_WIDE_TILES
+#define ASP_WIDE_TILES 256
+#endif
+constexpr int kWideTiles = ASP_WIDE_TILES;  // particles overlapping more tiles take the wide path
 constexpr int kScaleBits = 61;     // per-tile bound n_t * max|c| maps to <= 2^61
 constexpr int kAccF64 = 0;         // LDS fp64 accumulation
 constexpr int kAccFix = 1;         // LDS int64 fixed point (deterministic)
@@ -47,6 +50,9 @@ struct Grid {
     int ncx, ncy;     // reference chunks per axis
     int ntx, nty, ntiles;  // GPU tiles
     int nonsquare;    // nx != ny: the y chunk cull is not implied by the r2 test
+    int band_cols;    // records spanning >= this many tile columns: row-band deposit
+    int nstream;      // 2: second record run per tile for them (histogram columns x 2)
+    int wide_tiles;   // particles over more tiles than this take the wide path (K6)
 };
 
 struct Box {
@@ -68,7 +74,7 @@ struct Item {       // one deposit work item: a run of records of one GPU tile
     int tile;
     int count;      // 0: empty tile (write zeros)
     int slab;       // -1: the tile's only item (writes the map); >= 0: int64 partial slab
-    int pad;
+    int mode;       // 0: regular records; 1: large records (2-D map, gathered)
 };
 
 struct Merge {      // a tile split over several items: sum their slabs

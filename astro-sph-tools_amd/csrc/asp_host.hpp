@@ -32,12 +32,13 @@ struct Buf {
     size_t cap = 0;
 };
 
-constexpr int kStages = 16;
+constexpr int kStages = 17;
 enum Stage {
     kSMemset = 0, kSCount, kSColscan, kSTilescan, kSScatter, kSScale, kSDeposit, kSMerge,
     kSWide, kSRatio,
     // 3-D cube (asp_project3d)
-    kS3Count = 10, kS3Colscan, kS3Tilescan, kS3Scatter, kS3Deposit, kS3Merge
+    kS3Count = 10, kS3Colscan, kS3Tilescan, kS3Scatter, kS3Deposit, kS3Merge,
+    kSBand = 16  // 2-D row-band deposit of non-small records
 };
 
 struct Workspace {

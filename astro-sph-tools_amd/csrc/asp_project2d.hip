@@ -19,7 +19,7 @@
 //                whole wave; the tile is converted and written once, or (split tiles)
 //                stored as an int64 partial slab
 //   K5 merge     split tiles: exact int64 sum of their slabs, convert, write
-//   K6 wide      particles overlapping > kWideTiles tiles, per tile, wave sweeps
+//   K6 wide      particles overlapping > kWideTiles tiles, per tile, gathered
 //   K7 ratio     out0 / out1 (mass-weighted maps) when not fused into K4/K5
 //
 // No MFMA: this is gather/scatter work; the bounds are HBM bytes and VALU/LDS-atomic
@@ -30,9 +30,11 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/asp.h"
@@ -43,6 +45,18 @@
 namespace asp {
 
 constexpr int kCountBlock = 512;  // count / scatter workgroup
+
+// A record whose box clipped to its tile spans >= g.band_cols columns is WIDE: it is
+// binned into a second run per tile (histogram column t + ntiles) and deposited by row
+// bands (K4b: lanes own columns, register accumulation, no atomics), which beats the
+// atomic-bound wave sweep only when most of a wave's 64 lanes have work.
+__device__ __forceinline__ int tile_column(const Grid& g, const Box& b, bool maybe_wide, int tx,
+                                           int ty) {
+    int t = tx * g.nty + ty;
+    if (!maybe_wide) return t;
+    int hh = min(b.y1, ty * kTile + kTile - 1) - max(b.y0, ty * kTile) + 1;
+    return hh >= g.band_cols ? t + g.ntiles : t;
+}
 constexpr int kUnroll = 2;        // particles in flight per thread in count / scatter
 
 // Load kUnroll particles (lane-strided by the block size); h = 0 past the end, which has
@@ -70,8 +84,8 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
                                                        long long n, long long per_block, Grid g,
                                                        int* __restrict__ hist,
                                                        int* __restrict__ ctr) {
-    extern __shared__ __attribute__((aligned(16))) int lh[];
-    for (int t = threadIdx.x; t < g.ntiles; t += kCountBlock) lh[t] = 0;
+    extern __shared__ __attribute__((aligned(16))) int lh[];  // 2 * ntiles columns
+    for (int t = threadIdx.x; t < g.nstream * g.ntiles; t += kCountBlock) lh[t] = 0;
     __syncthreads();
     long long p0 = (long long)blockIdx.x * per_block;
     long long p1 = min(n, p0 + per_block);
@@ -89,12 +103,14 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
             if (!footprint(g, pu[k], pv[k], ph[k], b)) continue;
             int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
             int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
-            if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > kWideTiles) {
+            if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > g.wide_tiles) {
                 ++nwide;
                 continue;
             }
+            bool mb = g.nstream == 2 && b.y1 - b.y0 + 1 >= g.band_cols;
             for (int tx = tx0; tx <= tx1; ++tx)
-                for (int ty = ty0; ty <= ty1; ++ty) atomicAdd(&lh[tx * g.nty + ty], 1);
+                for (int ty = ty0; ty <= ty1; ++ty)
+                    atomicAdd(&lh[tile_column(g, b, mb, tx, ty)], 1);
         }
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
@@ -105,8 +121,8 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
     }
     if (nwide) atomicAdd(&ctr[cWideCount], nwide);
     __syncthreads();
-    int* row = hist + (long long)blockIdx.x * g.ntiles;
-    for (int t = threadIdx.x; t < g.ntiles; t += kCountBlock) row[t] = lh[t];
+    int* row = hist + (long long)blockIdx.x * g.nstream * g.ntiles;
+    for (int t = threadIdx.x; t < g.nstream * g.ntiles; t += kCountBlock) row[t] = lh[t];
 }
 
 template <int NOUT>
@@ -135,18 +151,16 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
     Grid g, const int* __restrict__ hist, const long long* __restrict__ tile_start,
     float4* __restrict__ recs, unsigned* __restrict__ cmx, int* __restrict__ wide_list,
     int* __restrict__ ctr) {
-    extern __shared__ __attribute__((aligned(16))) int cur[];  // absolute record cursors
+    // absolute record cursors, regular runs then large runs (2 * ntiles)
+    extern __shared__ __attribute__((aligned(16))) int cur[];
     // per-wave staging for the paired record stores (NOUT == 2): 64 records x 32 B
-    float4* stage = (float4*)(cur + ((g.ntiles + 3) & ~3));
+    float4* stage = (float4*)(cur + g.nstream * g.ntiles);
     unsigned* cm = (unsigned*)(stage + (NOUT == 2 ? (kCountBlock / 64) * 128 : 0));
-    const int* row = hist + (long long)blockIdx.x * g.ntiles;
-    for (int t = threadIdx.x; t < g.ntiles; t += kCountBlock) {
+    const int* row = hist + (long long)blockIdx.x * g.nstream * g.ntiles;
+    for (int t = threadIdx.x; t < g.nstream * g.ntiles; t += kCountBlock)
         cur[t] = (int)tile_start[t] + row[t];  // n_recs < 2^31 (checked on the host)
-        if constexpr (ACC == kAccFix) {
-#pragma unroll
-            for (int o = 0; o < NOUT; ++o) cm[t * NOUT + o] = 0u;
-        }
-    }
+    if constexpr (ACC == kAccFix)
+        for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kCountBlock) cm[t] = 0u;
     __syncthreads();
     long long p0 = (long long)blockIdx.x * per_block;
     long long p1 = min(n, p0 + per_block);
@@ -176,7 +190,7 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
             }
             int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
             int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
-            if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > kWideTiles) {
+            if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > g.wide_tiles) {
                 wide_list[atomicAdd(&ctr[cWideCursor], 1)] = (int)p;
                 if constexpr (ACC == kAccFix) {
                     atomicMax((unsigned*)&ctr[cWideMax0], c0);
@@ -186,10 +200,11 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
             }
             float4 r0 = make_float4(pu[k], pv[k], ph[k], pa0[k]);
             float4 r1 = make_float4(pa1[k], 0.0f, 0.0f, 0.0f);
+            bool mb = g.nstream == 2 && b.y1 - b.y0 + 1 >= g.band_cols;
             for (int tx = tx0; tx <= tx1; ++tx)
                 for (int ty = ty0; ty <= ty1; ++ty) {
                     int t = tx * g.nty + ty;
-                    int slot = atomicAdd(&cur[t], 1);
+                    int slot = atomicAdd(&cur[tile_column(g, b, mb, tx, ty)], 1);
                     if constexpr (ACC == kAccFix) {
                         atomicMax(&cm[t * NOUT], c0);
                         if (NOUT == 2) atomicMax(&cm[t * NOUT + 1], c1);
@@ -259,7 +274,7 @@ __device__ __forceinline__ int scale_exp(long long n, float cmax) {
 // ----------------------------------------------------------------------------------
 template <int NOUT>
 __global__ __launch_bounds__(kBlock) void k_tilescale(const unsigned* __restrict__ cmx, int nblk,
-                                                      int ntiles,
+                                                      int ntiles, int nstream,
                                                       const int* __restrict__ tile_total,
                                                       int2* __restrict__ tile_k) {
     __shared__ unsigned part[4][64][NOUT];
@@ -283,7 +298,8 @@ __global__ __launch_bounds__(kBlock) void k_tilescale(const unsigned* __restrict
         for (int o = 0; o < NOUT; ++o) {
             unsigned mm = max(max(part[0][lane][o], part[1][lane][o]),
                               max(part[2][lane][o], part[3][lane][o]));
-            k[o] = scale_exp(tile_total[t], __uint_as_float(mm));
+            k[o] = scale_exp((long long)tile_total[t] + (nstream == 2 ? tile_total[t + ntiles] : 0),
+                             __uint_as_float(mm));
         }
         tile_k[t] = make_int2(k[0], k[1]);
     }
@@ -429,6 +445,267 @@ __device__ __forceinline__ void emit_pixel(long long o, unsigned long long s0,
 }
 
 // ----------------------------------------------------------------------------------
+// Gather form for large records (clipped box >= kGatherArea pixels).  A sweep costs one
+// LDS atomic per pair and map; here every thread OWNS 8 pixels of the tile (row
+// t >> 3, columns (t & 7) * 8 .. + 7), walks a block-wide LDS list of large records and
+// sums their terms in registers -- no atomics per pair, only a flush per list round.
+// ----------------------------------------------------------------------------------
+constexpr int kBandCols2 = kTile + 1;  // row-band threshold for two-map maps (off)
+constexpr int kGatherCap = 128;  // list entries per round (5 KiB of LDS)
+
+struct GRec {  // 40 bytes; all lanes read the same entry (LDS broadcast)
+    float u, v, thr, band, hinv, s0, s1, h;
+    int xr, yr;  // tile-local box: x0 | x1 << 16, y0 | y1 << 16
+};
+
+__device__ __forceinline__ GRec make_grec(const Prep& P, int X0, int Y0) {
+    GRec r;
+    r.u = P.u; r.v = P.v; r.thr = P.thr; r.band = P.band; r.hinv = P.hinv;
+    r.s0 = P.s0; r.s1 = P.s1; r.h = P.h;
+    r.xr = (P.b.x0 - X0) | ((P.b.x1 - X0) << 16);
+    r.yr = (P.b.y0 - Y0) | ((P.b.y1 - Y0) << 16);
+    return r;
+}
+
+// Register accumulators of one thread's 8 pixels: fp32 partial sums (flushed into the
+// fp64 LDS tile every list round, <= kGatherCap terms each) or exact int64 fixed point.
+template <int NOUT, int ACC>
+struct GAcc {
+    using T = typename std::conditional<ACC == kAccFix, unsigned long long, float>::type;
+    T a0[8], a1[8];
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { a0[j] = 0; a1[j] = 0; }
+    }
+    __device__ __forceinline__ void add(int j, float t0, float t1) {
+        if constexpr (ACC == kAccFix) {
+            a0[j] += f2fix(t0);
+            if (NOUT == 2) a1[j] += f2fix(t1);
+        } else {
+            a0[j] += t0;
+            if (NOUT == 2) a1[j] += t1;
+        }
+    }
+    // add into the LDS tile (atomics: other waves may still be depositing there)
+    __device__ __forceinline__ void flush(unsigned long long* acc0, unsigned long long* acc1,
+                                          int pix0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if constexpr (ACC == kAccFix) {
+                if (a0[j]) atomicAdd(&acc0[pix0 + j], a0[j]);
+                if (NOUT == 2 && a1[j]) atomicAdd(&acc1[pix0 + j], a1[j]);
+            } else {
+                if (a0[j] != 0.0f) atomicAdd((double*)&acc0[pix0 + j], (double)a0[j]);
+                if (NOUT == 2 && a1[j] != 0.0f) atomicAdd((double*)&acc1[pix0 + j], (double)a1[j]);
+            }
+        }
+        zero();
+    }
+};
+
+// One list record against this thread's 8 pixels (row lx, columns ly0 .. ly0 + 7).
+template <int KID, int NOUT, int ACC>
+__device__ __forceinline__ void gather_rec(const Grid& g, const GRec& R, int X0, int Y0, int lx,
+                                           int ly0, float X, const float* Yc,
+                                           GAcc<NOUT, ACC>& ra) {
+    int x0 = R.xr & 0xffff, x1 = R.xr >> 16, y0 = R.yr & 0xffff, y1 = R.yr >> 16;
+    if (lx < x0 || lx > x1 || ly0 + 7 < y0 || ly0 > y1) return;
+    float dx = R.u - X;
+    float dx2 = dx * dx;
+    unsigned amb = 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        float dy = R.v - Yc[j];
+        float r2 = dx2 + dy * dy;
+        bool inb = ly0 + j >= y0 && ly0 + j <= y1;
+        bool a = inb && fabsf(r2 - R.thr) <= R.band;
+        bool in = inb && r2 < R.thr && !a;
+        amb |= a ? (1u << j) : 0u;
+        float w = kernel_shape<KID>(__builtin_amdgcn_sqrtf(r2) * R.hinv);
+        ra.add(j, in ? R.s0 * w : 0.0f, in ? R.s1 * w : 0.0f);
+    }
+    if (amb) {  // band pairs (rare): the reference's fp64 decision
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {  // static indices: ra and Yc stay in registers
+            if (!(amb & (1u << j))) continue;
+            if (exact_pair(g, R.u, R.v, R.h, X0 + lx, Y0 + ly0 + j)) {
+                float dy = R.v - Yc[j];
+                float w = kernel_shape<KID>(__builtin_amdgcn_sqrtf(dx2 + dy * dy) * R.hinv);
+                ra.add(j, R.s0 * w, R.s1 * w);
+            }
+        }
+    }
+}
+
+// Block-wide: append this thread's large record (if any) to the LDS list and let the
+// whole workgroup gather it, kGatherCap records per round.  Every thread of the block
+// must call this (it contains barriers).
+template <int KID, int NOUT, int ACC>
+__device__ __forceinline__ void gather_rounds(const Grid& g, bool large, const Prep& P, int X0,
+                                              int Y0, GRec* list, int* s_n, const float* xt,
+                                              const float* yt, unsigned long long* acc0,
+                                              unsigned long long* acc1) {
+    const int lx = threadIdx.x >> 3, ly0 = (threadIdx.x & 7) << 3;
+    // (registers live only inside a round: nothing is held across the record loop)
+    const float X = xt[lx];
+    float Yc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Yc[j] = yt[ly0 + j];
+    GAcc<NOUT, ACC> ra;
+    ra.zero();
+    bool pending = large;
+    for (;;) {
+        if (threadIdx.x == 0) *s_n = 0;
+        __syncthreads();
+        if (pending) {
+            int slot = atomicAdd(s_n, 1);
+            if (slot < kGatherCap) {
+                list[slot] = make_grec(P, X0, Y0);
+                pending = false;
+            }
+        }
+        __syncthreads();
+        int total = *s_n;
+        int n = min(total, kGatherCap);
+        if (lx < kTile)
+            for (int k = 0; k < n; ++k)
+                gather_rec<KID, NOUT, ACC>(g, list[k], X0, Y0, lx, ly0, X, Yc, ra);
+        if (lx < kTile) ra.flush(acc0, acc1, lx * kTile + ly0);
+        __syncthreads();  // the list is rewritten next round
+        if (total <= kGatherCap) break;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// K4 mode 1: a run of non-small records of one tile, deposited by ROW BANDS.  Wave w
+// owns tile rows 8w .. 8w+7, lane l owns column l: every wave streams all records of the
+// item, keeps those whose clipped box meets its rows and adds their terms to its own
+// register accumulators -- no atomics, no LDS tile, waves never wait for each other.
+// fp32 partial sums of one 64-record batch are folded into fp64 registers (kAccF64) or
+// terms go straight to int64 fixed point (kAccFix).
+// ----------------------------------------------------------------------------------
+template <int NOUT, int ACC>
+struct RowAcc {
+    using W = typename std::conditional<ACC == kAccFix, unsigned long long, double>::type;
+    W s0[8], s1[8];
+    float f0[8], f1[8];
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            s0[r] = 0; s1[r] = 0; f0[r] = 0.0f; f1[r] = 0.0f;
+        }
+    }
+    __device__ __forceinline__ void add(int r, float t0, float t1) {
+        if constexpr (ACC == kAccFix) {
+            s0[r] += f2fix(t0);
+            if (NOUT == 2) s1[r] += f2fix(t1);
+        } else {
+            f0[r] += t0;
+            if (NOUT == 2) f1[r] += t1;
+        }
+    }
+    __device__ __forceinline__ void fold() {
+        if constexpr (ACC != kAccFix) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                s0[r] += (double)f0[r];
+                f0[r] = 0.0f;
+                if (NOUT == 2) {
+                    s1[r] += (double)f1[r];
+                    f1[r] = 0.0f;
+                }
+            }
+        }
+    }
+    __device__ __forceinline__ unsigned long long word0(int r) const {
+        if constexpr (ACC == kAccFix) return s0[r];
+        else return (unsigned long long)__double_as_longlong(s0[r]);
+    }
+    __device__ __forceinline__ unsigned long long word1(int r) const {
+        if constexpr (ACC == kAccFix) return s1[r];
+        else return (unsigned long long)__double_as_longlong(s1[r]);
+    }
+};
+
+template <int KID, int NOUT, int ACC>
+__device__ __forceinline__ void band_item(const Grid& g, const float4* __restrict__ recs,
+                                          const Item& it, int X0, int Y0, int TW, int TH,
+                                          int2 kk, const float* xt, const float* yt,
+                                          unsigned long long* __restrict__ slabs,
+                                          float* __restrict__ out0, float* __restrict__ out1,
+                                          int flags) {
+    const int lane = threadIdx.x & 63, rb0 = blockIdx.y * 32 + (threadIdx.x >> 6) * 8;
+    const float Yl = yt[lane];
+    float Xr[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) Xr[r] = xt[rb0 + r];
+    RowAcc<NOUT, ACC> ra;
+    ra.zero();
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
+    if (lane < it.count) load_rec4<NOUT>(recs, it.start + lane, r0, r1);
+    for (int base = 0; base < it.count; base += 64) {
+        float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0;
+        if (base + 64 + lane < it.count) load_rec4<NOUT>(recs, it.start + base + 64 + lane, n0, n1);
+        Prep P;
+        bool hit = base + lane < it.count &&
+                   prep_record<KID, ACC>(g, r0.x, r0.y, r0.z, r0.w, r1.x, kk.x, kk.y, P) &&
+                   clip(P.b, X0, Y0, TW, TH) && P.b.x0 - X0 <= rb0 + 7 && P.b.x1 - X0 >= rb0;
+        r0 = n0;
+        r1 = n1;
+        unsigned long long m = __ballot(hit);
+        while (m) {
+            int l = __builtin_ctzll(m);
+            m &= m - 1;
+            Prep Q = bcast_prep(P, l);
+            const int ra0 = max(Q.b.x0 - X0 - rb0, 0), ra1 = min(Q.b.x1 - X0 - rb0, 7);
+            const bool col = Y0 + lane >= Q.b.y0 && Y0 + lane <= Q.b.y1;
+            const float dy = Q.v - Yl;
+            const float dy2 = dy * dy;
+            unsigned amb = 0u;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                if (r < ra0 || r > ra1) continue;  // wave-uniform
+                float dx = Q.u - Xr[r];
+                float r2 = dx * dx + dy2;
+                bool a = col && fabsf(r2 - Q.thr) <= Q.band;
+                bool in = col && r2 < Q.thr && !a;
+                amb |= a ? (1u << r) : 0u;
+                float w = kernel_shape<KID>(__builtin_amdgcn_sqrtf(r2) * Q.hinv);
+                ra.add(r, in ? Q.s0 * w : 0.0f, in ? Q.s1 * w : 0.0f);
+            }
+            if (amb) {  // band pairs (rare): the reference's fp64 decision
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {  // static indices: ra stays in registers
+                    if (!(amb & (1u << r))) continue;
+                    if (exact_pair(g, Q.u, Q.v, Q.h, X0 + rb0 + r, Y0 + lane)) {
+                        float dx = Q.u - Xr[r];
+                        float w =
+                            kernel_shape<KID>(__builtin_amdgcn_sqrtf(dx * dx + dy2) * Q.hinv);
+                        ra.add(r, Q.s0 * w, Q.s1 * w);
+                    }
+                }
+            }
+        }
+        ra.fold();
+    }
+    if (lane >= TH) return;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        int lx = rb0 + r;
+        if (lx >= TW) break;
+        if (it.slab >= 0) {
+            unsigned long long* dst = slabs + (long long)it.slab * NOUT * kTilePix;
+            dst[lx * kTile + lane] = ra.word0(r);
+            if (NOUT == 2) dst[kTilePix + lx * kTile + lane] = ra.word1(r);
+        } else {
+            long long o = (long long)(X0 + lx) * g.ny + (Y0 + lane);
+            emit_pixel<NOUT, ACC>(o, ra.word0(r), NOUT == 2 ? ra.word1(r) : 0ull, kk.x, kk.y,
+                                  out0, out1, flags);
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------
 // K4: deposit one work item (a run of records of one tile) into LDS, then write the
 // tile (single-item tiles) or its int64 partial slab (split tiles).
 // ----------------------------------------------------------------------------------
@@ -443,6 +720,7 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
     float* xt = (float*)(acc + NOUT * kTilePix);
     float* yt = xt + kTile;
     const Item it = items[blockIdx.x];
+    if (it.mode != 0) return;  // K4b's
     int tx = it.tile / g.nty, ty = it.tile - (it.tile / g.nty) * g.nty;
     int X0 = tx * kTile, Y0 = ty * kTile;
     int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
@@ -457,94 +735,96 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
         }
         return;
     }
-    tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
     const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
-    int lane = threadIdx.x & 63;
-    // Software pipeline, two batches deep: batches i+1 and i+2 load while batch i deposits
-    // (16 waves/CU x 64 lanes x 32 B x 2 in flight per CU).
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, q0 = r0, q1 = r0;
-    if ((int)threadIdx.x < it.count) load_rec4<NOUT>(recs, it.start + threadIdx.x, r0, r1);
-    if ((int)threadIdx.x + kDepBlock < it.count)
-        load_rec4<NOUT>(recs, it.start + threadIdx.x + kDepBlock, q0, q1);
-    for (int base = 0; base < it.count; base += kDepBlock) {
-        int i = base + threadIdx.x;
-        float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0;
-        if (i + 2 * kDepBlock < it.count)
-            load_rec4<NOUT>(recs, it.start + i + 2 * kDepBlock, n0, n1);
-        Prep P;
-        P.b = Box{0, -1, 0, -1};
-        bool live = false;
-#if ASP_ABLATE == 3
-        asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x));
-        r0 = q0; r1 = q1; q0 = n0; q1 = n1;
-        continue;
-#endif
-        if (i < it.count)
-            live = prep_record<KID, ACC>(g, r0.x, r0.y, r0.z, r0.w, r1.x, kk.x, kk.y, P) &&
-                   clip(P.b, X0, Y0, TW, TH);
-        r0 = q0;
-        r1 = q1;
-        q0 = n0;
-        q1 = n1;
-#if ASP_ABLATE == 2
-        asm volatile("" ::"v"(P.u), "v"(P.v), "v"(P.thr), "v"(P.band), "v"(P.s0), "v"(P.s1),
-                     "v"(P.b.x0), "v"(P.b.y1), "v"(live ? 1 : 0));
-        continue;
-#endif
-        int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
-        bool small = live && bw <= 4 && bh <= 4;
-        if (small) {
-            // lane-per-record: <= 4 x 4 box, dy^2 per column kept in registers
-            float dy2[4];
-            int yc[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                int yi = min(P.b.y0 + j, P.b.y1);
-                yc[j] = yi;
-                float dy = P.v - yt[yi - Y0];
-                dy2[j] = dy * dy;
-            }
-            // Unrolled 4x4 pass decides every pair whose fp32 r2 is outside the error band
-            // and accumulates it; band pairs (~0.1 %) only set a bit, resolved below in
-            // fp64 -- keeping the rare slow path out of the unrolled body.
-            unsigned amb = 0u;
-#pragma unroll
-            for (int ii = 0; ii < 4; ++ii) {
-                if (ii < bw) {
-                    int xi = P.b.x0 + ii;
-                    float dx = P.u - xt[xi - X0];
-                    float dx2 = dx * dx;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        if (j < bh) {
-                            float r2 = dx2 + dy2[j];
-                            bool in = r2 < P.thr;
-                            bool a = fabsf(r2 - P.thr) <= P.band;
-                            amb |= a ? (1u << (ii * 4 + j)) : 0u;
-                            if (in && !a)
-                                accumulate<KID, NOUT, ACC>(P, r2, acc0, acc1,
-                                                           (xi - X0) * kTile + (yc[j] - Y0));
+    tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
+    {
+        int lane = threadIdx.x & 63;
+        // Software pipeline, two batches deep: batches i+1 and i+2 load while batch i deposits
+        // (16 waves/CU x 64 lanes x 32 B x 2 in flight per CU).
+        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, q0 = r0, q1 = r0;
+        if ((int)threadIdx.x < it.count) load_rec4<NOUT>(recs, it.start + threadIdx.x, r0, r1);
+        if ((int)threadIdx.x + kDepBlock < it.count)
+            load_rec4<NOUT>(recs, it.start + threadIdx.x + kDepBlock, q0, q1);
+        for (int base = 0; base < it.count; base += kDepBlock) {
+            int i = base + threadIdx.x;
+            float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0;
+            if (i + 2 * kDepBlock < it.count)
+                load_rec4<NOUT>(recs, it.start + i + 2 * kDepBlock, n0, n1);
+            Prep P;
+            P.b = Box{0, -1, 0, -1};
+            bool live = false;
+    #if ASP_ABLATE == 3
+            asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x));
+            r0 = q0; r1 = q1; q0 = n0; q1 = n1;
+            continue;
+    #endif
+            if (i < it.count)
+                live = prep_record<KID, ACC>(g, r0.x, r0.y, r0.z, r0.w, r1.x, kk.x, kk.y, P) &&
+                       clip(P.b, X0, Y0, TW, TH);
+            r0 = q0;
+            r1 = q1;
+            q0 = n0;
+            q1 = n1;
+    #if ASP_ABLATE == 2
+            asm volatile("" ::"v"(P.u), "v"(P.v), "v"(P.thr), "v"(P.band), "v"(P.s0), "v"(P.s1),
+                         "v"(P.b.x0), "v"(P.b.y1), "v"(live ? 1 : 0));
+            continue;
+    #endif
+            int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
+            bool small = live && bw <= 4 && bh <= 4;
+            if (small) {
+                // lane-per-record: <= 4 x 4 box, dy^2 per column kept in registers
+                float dy2[4];
+                int yc[4];
+    #pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    int yi = min(P.b.y0 + j, P.b.y1);
+                    yc[j] = yi;
+                    float dy = P.v - yt[yi - Y0];
+                    dy2[j] = dy * dy;
+                }
+                // Unrolled 4x4 pass decides every pair whose fp32 r2 is outside the error band
+                // and accumulates it; band pairs (~0.1 %) only set a bit, resolved below in
+                // fp64 -- keeping the rare slow path out of the unrolled body.
+                unsigned amb = 0u;
+    #pragma unroll
+                for (int ii = 0; ii < 4; ++ii) {
+                    if (ii < bw) {
+                        int xi = P.b.x0 + ii;
+                        float dx = P.u - xt[xi - X0];
+                        float dx2 = dx * dx;
+    #pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            if (j < bh) {
+                                float r2 = dx2 + dy2[j];
+                                bool in = r2 < P.thr;
+                                bool a = fabsf(r2 - P.thr) <= P.band;
+                                amb |= a ? (1u << (ii * 4 + j)) : 0u;
+                                if (in && !a)
+                                    accumulate<KID, NOUT, ACC>(P, r2, acc0, acc1,
+                                                               (xi - X0) * kTile + (yc[j] - Y0));
+                            }
                         }
                     }
                 }
-            }
-            while (amb) {
-                int bit = __builtin_ctz(amb);
-                amb &= amb - 1u;
-                int xi = P.b.x0 + (bit >> 2), yi = yc[bit & 3];
-                if (exact_pair(g, P.u, P.v, P.h, xi, yi)) {
-                    float dx = P.u - xt[xi - X0], dy = P.v - yt[yi - Y0];
-                    accumulate<KID, NOUT, ACC>(P, dx * dx + dy * dy, acc0, acc1,
-                                               (xi - X0) * kTile + (yi - Y0));
+                while (amb) {
+                    int bit = __builtin_ctz(amb);
+                    amb &= amb - 1u;
+                    int xi = P.b.x0 + (bit >> 2), yi = yc[bit & 3];
+                    if (exact_pair(g, P.u, P.v, P.h, xi, yi)) {
+                        float dx = P.u - xt[xi - X0], dy = P.v - yt[yi - Y0];
+                        accumulate<KID, NOUT, ACC>(P, dx * dx + dy * dy, acc0, acc1,
+                                                   (xi - X0) * kTile + (yi - Y0));
+                    }
                 }
             }
-        }
-        unsigned long long big = __ballot(live && !small);
-        while (big) {
-            int l = __builtin_ctzll(big);
-            big &= big - 1;
-            Prep Q = bcast_prep(P, l);
-            sweep<KID, NOUT, ACC>(g, Q, X0, Y0, xt, yt, acc0, acc1, lane);
+            unsigned long long big = __ballot(live && !small);
+            while (big) {
+                int l = __builtin_ctzll(big);
+                big &= big - 1;
+                Prep Q = bcast_prep(P, l);
+                sweep<KID, NOUT, ACC>(g, Q, X0, Y0, xt, yt, acc0, acc1, lane);
+            }
         }
     }
     __syncthreads();
@@ -560,6 +840,32 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
         emit_pixel<NOUT, ACC>(o, acc0[k], NOUT == 2 ? acc1[k] : 0ull, kk.x, kk.y, out0, out1,
                               flags);
     }
+}
+
+// K4b: mode-1 items (non-small records), row bands; grid (items, 2): blockIdx.y picks
+// the tile half, each of the 4 waves 8 rows of it.  Writes the tile (or its slab half).
+template <int KID, int NOUT, int ACC>
+__global__ __launch_bounds__(kBlock) void k_band(Grid g, const float4* __restrict__ recs,
+                                                 const Item* __restrict__ items,
+                                                 const int2* __restrict__ tile_k,
+                                                 unsigned long long* __restrict__ slabs,
+                                                 float* __restrict__ out0,
+                                                 float* __restrict__ out1, int flags) {
+    __shared__ float xt[kTile], yt[kTile];
+    const Item it = items[blockIdx.x];
+    if (it.mode != 1) return;
+    int tx = it.tile / g.nty, ty = it.tile - (it.tile / g.nty) * g.nty;
+    int X0 = tx * kTile, Y0 = ty * kTile;
+    int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
+    if ((int)blockIdx.y * 32 >= TW) return;
+    const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
+    if (threadIdx.x < kTile)
+        xt[threadIdx.x] = (float)corner_x(g, X0 + threadIdx.x);
+    else if (threadIdx.x < 2 * kTile)
+        yt[threadIdx.x - kTile] = (float)corner_y(g, Y0 + threadIdx.x - kTile);
+    __syncthreads();
+    static_assert(kBlock == 4 * 64, "row bands: 4 waves x 8 rows per tile half");
+    band_item<KID, NOUT, ACC>(g, recs, it, X0, Y0, TW, TH, kk, xt, yt, slabs, out0, out1, flags);
 }
 
 // ----------------------------------------------------------------------------------
@@ -591,49 +897,56 @@ __global__ __launch_bounds__(kBlock) void k_merge(Grid g, const Merge* __restric
 }
 
 // ----------------------------------------------------------------------------------
-// K6: wide particles (footprint over > kWideTiles tiles).  One workgroup per tile, each
-// wave takes every 4th wide particle and sweeps its clipped box; fixed point with the
-// wide particles' own bound, added onto the tile (this workgroup is its only writer).
+// K6: wide particles (footprint over > kWideTiles tiles): they are never binned.  One
+// workgroup per tile walks the wide list kGatherCap particles at a time, keeps those
+// whose clipped box meets the tile and gathers them (register sums, no per-pair
+// atomics); fixed point with the wide particles' own bound.  Adds onto the tile K4/K5
+// wrote (this workgroup is its only writer).
 // ----------------------------------------------------------------------------------
 template <int KID, int NOUT, int ACC>
-__global__ __launch_bounds__(kBlock) void k_wide(Grid g, const float* __restrict__ u,
-                                                 const float* __restrict__ v,
-                                                 const float* __restrict__ h,
-                                                 const float* __restrict__ a0,
-                                                 const float* __restrict__ a1,
-                                                 const int* __restrict__ wide_list, int n_wide,
-                                                 const int* __restrict__ ctr,
-                                                 float* __restrict__ out0,
-                                                 float* __restrict__ out1) {
+__global__ __launch_bounds__(kDepBlock) void k_wide(Grid g, const float* __restrict__ u,
+                                                    const float* __restrict__ v,
+                                                    const float* __restrict__ h,
+                                                    const float* __restrict__ a0,
+                                                    const float* __restrict__ a1,
+                                                    const int* __restrict__ wide_list, int n_wide,
+                                                    const int* __restrict__ ctr,
+                                                    float* __restrict__ out0,
+                                                    float* __restrict__ out1) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];
     unsigned long long* acc0 = acc;
     unsigned long long* acc1 = acc + kTilePix;
     float* xt = (float*)(acc + NOUT * kTilePix);
     float* yt = xt + kTile;
-    int* any = (int*)(yt + kTile);
+    __shared__ GRec glist[kGatherCap];
+    __shared__ int gcount;
     int t = blockIdx.x;
     int tx = t / g.nty, ty = t - (t / g.nty) * g.nty;
     int X0 = tx * kTile, Y0 = ty * kTile;
     int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
-    if (threadIdx.x == 0) *any = 0;
-    tile_prologue<NOUT, kBlock>(g, X0, Y0, acc, xt, yt);
+    tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
     int k0 = ACC == kAccFix ? scale_exp(n_wide, __uint_as_float((unsigned)ctr[cWideMax0])) : 0;
     int k1 = (ACC == kAccFix && NOUT == 2)
                  ? scale_exp(n_wide, __uint_as_float((unsigned)ctr[cWideMax1])) : 0;
-    int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int k = wv; k < n_wide; k += kBlock / 64) {
-        int p = wide_list[k];
+    bool any = false;
+    for (int c = 0; c < n_wide; c += kGatherCap) {
         Prep P;
-        if (!prep_record<KID, ACC>(g, u[p], v[p], h[p], a0[p], NOUT == 2 ? a1[p] : 0.0f, k0, k1,
-                                   P))
-            continue;
-        if (!clip(P.b, X0, Y0, TW, TH)) continue;
-        if (lane == 0) *any = 1;
-        sweep<KID, NOUT, ACC>(g, P, X0, Y0, xt, yt, acc0, acc1, lane);
+        bool live = false;
+        int k = c + (int)threadIdx.x;
+        if (threadIdx.x < kGatherCap && k < n_wide) {
+            int p = wide_list[k];
+            live = prep_record<KID, ACC>(g, u[p], v[p], h[p], a0[p], NOUT == 2 ? a1[p] : 0.0f, k0,
+                                         k1, P) &&
+                   clip(P.b, X0, Y0, TW, TH);
+        }
+        if (__syncthreads_or(live)) {
+            any = true;
+            gather_rounds<KID, NOUT, ACC>(g, live, P, X0, Y0, glist, &gcount, xt, yt, acc0, acc1);
+        }
     }
+    if (!any) return;  // uniform: every thread saw the same __syncthreads_or results
     __syncthreads();
-    if (!*any) return;
-    for (int k = threadIdx.x; k < kTilePix; k += kBlock) {
+    for (int k = threadIdx.x; k < kTilePix; k += kDepBlock) {
         int lx = k >> kTileShift, ly = k & (kTile - 1);
         if (lx >= TW || ly >= TH) continue;
         long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
@@ -798,10 +1111,13 @@ static bool make_grid(double x_min, double x_max, double y_min, double y_max, in
     g.nty = (ny + kTile - 1) / kTile;
     g.ntiles = g.ntx * g.nty;
     g.nonsquare = nx != ny;
+    g.band_cols = kTile + 1;  // row bands off unless project2d enables them
+    g.nstream = 1;
+    g.wide_tiles = kWideTiles;
     return true;
 }
 
-constexpr int kMaxTiles = 4096;  // K3 LDS: cursor + per-tile max (12 B/tile at 2 maps)
+constexpr int kMaxTiles = 4096;  // K1/K3 LDS: 2 cursors + per-tile max (16 B/tile at 2 maps)
 
 struct Plan {
     long long n, nblk, per_block;
@@ -820,7 +1136,7 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     int dflags = ((flags & ASP_F_ACCUMULATE) ? kFlagAccumulate : 0) | (fuse_ratio ? kFlagRatio : 0);
     {
         StageMark m(ws, kSScatter, st);
-        size_t lds = (size_t)((g.ntiles + 3) & ~3) * sizeof(int) +
+        size_t lds = (size_t)g.nstream * g.ntiles * sizeof(int) +
                      (NOUT == 2 ? (size_t)(kCountBlock / 64) * 128 * sizeof(float4) : 0) +
                      (ACC == kAccFix ? (size_t)g.ntiles * NOUT * sizeof(unsigned) : 0);
         hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC>), dim3((unsigned)pl.nblk), dim3(kCountBlock),
@@ -833,7 +1149,7 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     if (ACC == kAccFix) {
         StageMark m(ws, kSScale, st);
         hipLaunchKernelGGL((k_tilescale<NOUT>), dim3((g.ntiles + 63) / 64), dim3(kBlock), 0, st,
-                           (const unsigned*)ws.cmx.p, (int)pl.nblk, g.ntiles,
+                           (const unsigned*)ws.cmx.p, (int)pl.nblk, g.ntiles, g.nstream,
                            (const int*)ws.tile_total.p, (int2*)ws.tile_k.p);
         ASP_LAUNCHED();
         m.done();
@@ -842,6 +1158,15 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
         StageMark m(ws, kSDeposit, st);
         size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4;
         hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(pl.n_items), dim3(kDepBlock), lds, st, g,
+                           (const float4*)ws.recs.p, (const Item*)ws.items.p,
+                           (const int2*)ws.tile_k.p, (unsigned long long*)ws.slabs.p, o0, o1,
+                           dflags);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    if (g.nstream == 2) {
+        StageMark m(ws, kSBand, st);
+        hipLaunchKernelGGL((k_band<KID, NOUT, ACC>), dim3(pl.n_items, 2), dim3(kBlock), 0, st, g,
                            (const float4*)ws.recs.p, (const Item*)ws.items.p,
                            (const int2*)ws.tile_k.p, (unsigned long long*)ws.slabs.p, o0, o1,
                            dflags);
@@ -858,8 +1183,8 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     }
     if (pl.n_wide > 0) {
         StageMark m(ws, kSWide, st);
-        size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4 + 16;
-        hipLaunchKernelGGL((k_wide<KID, NOUT, ACC>), dim3(g.ntiles), dim3(kBlock), lds, st, g, u, v, h,
+        size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4;
+        hipLaunchKernelGGL((k_wide<KID, NOUT, ACC>), dim3(g.ntiles), dim3(kDepBlock), lds, st, g, u, v, h,
                            a0, a1, (const int*)ws.wide.p, pl.n_wide, (const int*)dc, o0, o1);
         ASP_LAUNCHED();
         m.done();
@@ -895,6 +1220,13 @@ static int project2d(const float* u, const float* v, const float* h, const float
         return fail(ASP_ERR_INVALID,
                     "invalid grid: need nx, ny, chunk_size >= 1, finite x_max > x_min, "
                     "y_max > y_min");
+    // Row bands (K4b) are correct for any threshold but, as measured so far, slower than
+    // the LDS-atomic sweep even for full-width boxes, so they are off by
+    // default; ASP_BAND_COLS=c routes records spanning >= c tile columns to them.
+    g.band_cols = (out1 != nullptr) ? kBandCols2 : kTile + 1;
+    if (const char* e = getenv("ASP_BAND_COLS")) g.band_cols = std::max(1, atoi(e));
+    g.nstream = g.band_cols <= kTile ? 2 : 1;  // a second record run per tile for K4b
+    if (const char* e = getenv("ASP_WIDE_TILES")) g.wide_tiles = std::max(1, atoi(e));
     if (g.ntiles > kMaxTiles)
         return fail(ASP_ERR_UNSUPPORTED, "grid too large (more than 4096 64x64 tiles)");
     if (device < 0 || device >= 64) return fail(ASP_ERR_INVALID, "bad device");
@@ -955,13 +1287,13 @@ static int project2d(const float* u, const float* v, const float* h, const float
         pl.nblk = std::min<long long>(1024, std::max<long long>(1, (n + 8191) / 8192));
         pl.per_block = (n + pl.nblk - 1) / pl.nblk;
         pl.nblk = (n + pl.per_block - 1) / pl.per_block;
-        ASP_TRY(ensure(ws.hist, (size_t)pl.nblk * g.ntiles * sizeof(int)));
+        ASP_TRY(ensure(ws.hist, (size_t)pl.nblk * g.nstream * g.ntiles * sizeof(int)));
         const bool det = (flags & ASP_F_DETERMINISTIC) != 0;
         if (det) ASP_TRY(ensure(ws.cmx, (size_t)pl.nblk * g.ntiles * nout * sizeof(unsigned)));
-        ASP_TRY(ensure(ws.tile_total, (size_t)g.ntiles * sizeof(int)));
-        ASP_TRY(ensure(ws.tile_start, (size_t)g.ntiles * sizeof(long long)));
+        ASP_TRY(ensure(ws.tile_total, (size_t)2 * g.ntiles * sizeof(int)));
+        ASP_TRY(ensure(ws.tile_start, (size_t)2 * g.ntiles * sizeof(long long)));
         ASP_TRY(ensure(ws.tile_k, (size_t)g.ntiles * sizeof(int2)));
-        ASP_TRY(ensure(ws.items, (size_t)(g.ntiles + kTargetItems + 16) * sizeof(Item)));
+        ASP_TRY(ensure(ws.items, (size_t)(2 * g.ntiles + kTargetItems + kTargetItems1 + 16) * sizeof(Item)));
         ASP_TRY(ensure(ws.merges, (size_t)(g.ntiles + 16) * sizeof(Merge)));
         ASP_TRY(ensure(ws.counters, cNum * sizeof(int)));
         if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, cNum * sizeof(int)));
@@ -970,22 +1302,24 @@ static int project2d(const float* u, const float* v, const float* h, const float
         {
             StageMark m(ws, kSCount, st);
             hipLaunchKernelGGL(k_count, dim3((unsigned)pl.nblk), dim3(kCountBlock),
-                               (size_t)g.ntiles * sizeof(int), st, du, dv, dh, n, pl.per_block, g,
+                               (size_t)g.nstream * g.ntiles * sizeof(int), st, du, dv, dh, n,
+                               pl.per_block, g,
                                (int*)ws.hist.p, dc);
             ASP_LAUNCHED();
             m.done();
         }
         {
             StageMark m(ws, kSColscan, st);
-            hipLaunchKernelGGL(k_colscan, dim3((g.ntiles + 63) / 64), dim3(kBlock), 0, st,
-                               (int*)ws.hist.p, (int)pl.nblk, g.ntiles, (int*)ws.tile_total.p);
+            hipLaunchKernelGGL(k_colscan, dim3((g.nstream * g.ntiles + 63) / 64), dim3(kBlock),
+                               0, st, (int*)ws.hist.p, (int)pl.nblk, g.nstream * g.ntiles,
+                               (int*)ws.tile_total.p);
             ASP_LAUNCHED();
             m.done();
         }
         {
             StageMark m(ws, kSTilescan, st);
             hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(kScanThreads), 0, st,
-                               (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles,
+                               (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles, g.nstream,
                                (long long*)ws.tile_start.p, (Item*)ws.items.p,
                                (Merge*)ws.merges.p, dc);
             ASP_LAUNCHED();

@@ -496,7 +496,7 @@ static int project3d(const float* x, const float* y, const float* z, const float
         {
             StageMark m(ws, kS3Tilescan, st);
             hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(kScanThreads), 0, st,
-                               (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb,
+                               (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1,
                                (long long*)ws.tile_start.p, (Item*)ws.items.p,
                                (Merge*)ws.merges.p, dc);
             ASP_LAUNCHED();

@@ -161,7 +161,7 @@ int asp_last_stats(int32_t device, int64_t *stats, int32_t nstats);
  * summed milliseconds and the number of launches since the last reset.  Stages:
  * 0 memset, 1 count, 2 colscan, 3 tilescan, 4 scatter, 5 scale, 6 deposit, 7 merge,
  * 8 wide, 9 ratio; cube (asp_project3d): 10 count, 11 colscan, 12 tilescan, 13 scatter,
- * 14 deposit, 15 merge.
+ * 14 deposit, 15 merge; 16 band (2-D row-band deposit of non-small records).
  */
 int asp_profile(int32_t device, int32_t enable);
 int asp_profile_read(int32_t device, double *ms_sum, int64_t *launches, int32_t nstages);

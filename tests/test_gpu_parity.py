@@ -235,15 +235,17 @@ def test_weighted_map(gpu, oracle):
 
 
 def test_wide_particles(gpu, oracle):
-    """Huge smoothing lengths (wide path, > 64 GPU tiles) mixed with small ones."""
+    """Huge smoothing lengths (wide path, > kWideTiles GPU tiles), large ones (gather path:
+    clipped boxes >= 1024 pixels) and small ones (lane / wave paths) mixed."""
     from asp_amd.tools.projections import create_image, indicator_kernel
     rng = np.random.default_rng(5)
     n = 3000
     pos = np.asarray(rng.uniform(-1, 1, (n, 3)), np.float32).astype(np.float64)
-    h = np.asarray(rng.uniform(0.005, 0.02, n), np.float32).astype(np.float64)
+    h = np.asarray(rng.uniform(0.0025, 0.01, n), np.float32).astype(np.float64)
     h[:40] = np.asarray(rng.uniform(0.3, 2.0, 40), np.float32)
+    h[40:400] = np.asarray(rng.uniform(0.01, 0.06, 360), np.float32)
     A = np.asarray(rng.uniform(0.5, 1.5, n), np.float32).astype(np.float64)
-    G = 1024
+    G = 2048
     ext = (-1.0, 1.0, -1.0, 1.0)
     img = create_image(pos, h, A, (G, G), 32, 2, *ext)
     ref, _ = oracle.project_scatter(pos[:, 0], pos[:, 1], h, A, None, (G, G), 32, *ext)
@@ -352,3 +354,28 @@ def test_default_vs_deterministic_modes(gpu):
     a = create_image(p["pos"], p["h"], p["m"], (1024, 1024), 64, 2, *ext)
     b = create_image(p["pos"], p["h"], p["m"], (1024, 1024), 64, 2, *ext, deterministic=True)
     assert_map_close(b, a, abs_tol=1e-6, rel_tol=1e-5)
+
+
+@pytest.mark.parametrize("band_cols", ["1", "17", "65"])
+def test_row_band_path(gpu, oracle, band_cols, monkeypatch):
+    """Force records into the row-band deposit (K4b; ASP_BAND_COLS = minimum clipped box
+    columns) or keep them all on the sweep/lane paths: neighbour counts stay bit-exact and
+    values within tolerance either way."""
+    from asp_amd.tools.projections import create_image, create_weighted_image, indicator_kernel
+    monkeypatch.setenv("ASP_BAND_COLS", band_cols)
+    rng = np.random.default_rng(11)
+    n = 6000
+    pos = np.asarray(rng.normal(0, 0.4, (n, 3)), np.float32).astype(np.float64)
+    h = np.asarray(rng.uniform(0.002, 0.08, n), np.float32).astype(np.float64)
+    A = np.asarray(rng.uniform(0.5, 1.5, n), np.float32).astype(np.float64)
+    T = np.asarray(rng.uniform(1.0, 3.0, n), np.float32).astype(np.float64)
+    G, ext = 512, (-1.0, 1.0, -1.0, 1.0)
+    cnt = create_image(pos, h, np.ones(n), (G, G), 64, 2, *ext, kernel_func=indicator_kernel)
+    want, _ = oracle.project_scatter(pos[:, 0], pos[:, 1], h, np.ones(n), None, (G, G), 64,
+                                     *ext, kernel="indicator")
+    assert np.array_equal(cnt, want)
+    r, s0, s1 = create_weighted_image(pos, h, A, T, (G, G), 64, 2, *ext, return_components=True)
+    AT = np.asarray(A * T, np.float32).astype(np.float64)
+    w0, w1 = oracle.project_scatter(pos[:, 0], pos[:, 1], h, AT, A, (G, G), 64, *ext)
+    assert_map_close(s0, w0)
+    assert_map_close(s1, w1)
