@@ -46,6 +46,11 @@ namespace asp {
 
 constexpr int kCountBlock = 512;  // count / scatter workgroup
 
+#ifndef ASP_ABLATE_SCATTER
+#define ASP_ABLATE_SCATTER 0  // diagnostic builds only: 1 = no first-record stores,
+                              // 2 = first records stored to coalesced slots (wrong map)
+#endif
+
 // A record whose box clipped to its tile spans >= g.band_cols columns is WIDE: it is
 // binned into a second run per tile (histogram column t + ntiles) and deposited by row
 // bands (K4b: lanes own columns, register accumulation, no atomics), which beats the
@@ -209,6 +214,9 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
                         atomicMax(&cm[t * NOUT], c0);
                         if (NOUT == 2) atomicMax(&cm[t * NOUT + 1], c1);
                     }
+#if ASP_ABLATE_SCATTER == 2
+                    slot = (int)p;  // diagnostic: coalesced destinations, same bytes
+#endif
                     if constexpr (NOUT == 2) {
                         if (tx == tx0 && ty == ty0) {
                             first_slot[k] = slot;  // written by the paired store below
@@ -238,7 +246,11 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
                     int src = half * 32 + (lane >> 1);
                     int slot = __shfl(first_slot[k], src);
                     float4 val = st[2 * src + (lane & 1)];
+#if ASP_ABLATE_SCATTER == 1
+                    asm volatile("" ::"v"(val.x), "v"(val.y), "v"(val.z), "v"(val.w), "v"(slot));
+#else
                     if (slot >= 0) recs[2 * (long long)slot + (lane & 1)] = val;
+#endif
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
@@ -705,6 +717,54 @@ __device__ __forceinline__ void band_item(const Grid& g, const float4* __restric
     }
 }
 
+// Lane-per-record deposit of a box of at most S x S pixels: dy^2 per column in
+// registers, an unrolled S x S pass decides every pair whose fp32 r2 is outside the error
+// band and accumulates it; band pairs (~0.1 %) only set a bit, resolved afterwards in
+// fp64 -- keeping the rare slow path out of the unrolled body.
+template <int KID, int NOUT, int ACC, int S>
+__device__ __forceinline__ void small_box(const Grid& g, const Prep& P, int bw, int bh, int X0,
+                                          int Y0, const float* xt, const float* yt,
+                                          unsigned long long* acc0, unsigned long long* acc1) {
+    float dy2[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        float dy = P.v - yt[min(P.b.y0 + j, P.b.y1) - Y0];
+        dy2[j] = dy * dy;
+    }
+    unsigned amb = 0u;
+#pragma unroll
+    for (int ii = 0; ii < S; ++ii) {
+        if (ii < bw) {
+            int xi = P.b.x0 + ii;
+            float dx = P.u - xt[xi - X0];
+            float dx2 = dx * dx;
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                if (j < bh) {
+                    float r2 = dx2 + dy2[j];
+                    bool in = r2 < P.thr;
+                    bool a = fabsf(r2 - P.thr) <= P.band;
+                    amb |= a ? (1u << (ii * S + j)) : 0u;
+                    if (in && !a)
+                        accumulate<KID, NOUT, ACC>(P, r2, acc0, acc1,
+                                                   (xi - X0) * kTile + (P.b.y0 + j - Y0));
+                }
+            }
+        }
+    }
+    while (amb) {
+        int bit = __builtin_ctz(amb);
+        amb &= amb - 1u;
+        int ii = bit / S, j = bit - (bit / S) * S;
+        int xi = P.b.x0 + ii, yi = P.b.y0 + j;
+        if (exact_pair(g, P.u, P.v, P.h, xi, yi)) {
+            float dx = P.u - xt[xi - X0], dy = P.v - yt[yi - Y0];
+            accumulate<KID, NOUT, ACC>(P, dx * dx + dy * dy, acc0, acc1,
+                                       (xi - X0) * kTile + (yi - Y0));
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------------
 // K4: deposit one work item (a run of records of one tile) into LDS, then write the
 // tile (single-item tiles) or its int64 partial slab (split tiles).
@@ -773,50 +833,13 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
             int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
             bool small = live && bw <= 4 && bh <= 4;
             if (small) {
-                // lane-per-record: <= 4 x 4 box, dy^2 per column kept in registers
-                float dy2[4];
-                int yc[4];
-    #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    int yi = min(P.b.y0 + j, P.b.y1);
-                    yc[j] = yi;
-                    float dy = P.v - yt[yi - Y0];
-                    dy2[j] = dy * dy;
-                }
-                // Unrolled 4x4 pass decides every pair whose fp32 r2 is outside the error band
-                // and accumulates it; band pairs (~0.1 %) only set a bit, resolved below in
-                // fp64 -- keeping the rare slow path out of the unrolled body.
-                unsigned amb = 0u;
-    #pragma unroll
-                for (int ii = 0; ii < 4; ++ii) {
-                    if (ii < bw) {
-                        int xi = P.b.x0 + ii;
-                        float dx = P.u - xt[xi - X0];
-                        float dx2 = dx * dx;
-    #pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            if (j < bh) {
-                                float r2 = dx2 + dy2[j];
-                                bool in = r2 < P.thr;
-                                bool a = fabsf(r2 - P.thr) <= P.band;
-                                amb |= a ? (1u << (ii * 4 + j)) : 0u;
-                                if (in && !a)
-                                    accumulate<KID, NOUT, ACC>(P, r2, acc0, acc1,
-                                                               (xi - X0) * kTile + (yc[j] - Y0));
-                            }
-                        }
-                    }
-                }
-                while (amb) {
-                    int bit = __builtin_ctz(amb);
-                    amb &= amb - 1u;
-                    int xi = P.b.x0 + (bit >> 2), yi = yc[bit & 3];
-                    if (exact_pair(g, P.u, P.v, P.h, xi, yi)) {
-                        float dx = P.u - xt[xi - X0], dy = P.v - yt[yi - Y0];
-                        accumulate<KID, NOUT, ACC>(P, dx * dx + dy * dy, acc0, acc1,
-                                                   (xi - X0) * kTile + (yi - Y0));
-                    }
-                }
+                // lane-per-record; 3 x 3 unrolled body when no lane of the wave needs 4
+                // (pixel-scale h: a 2h = 1.5 px disc spans 3 corners per axis but for a
+                // measure-zero set of centres)
+                if (__ballot(bw > 3 || bh > 3) == 0ull)
+                    small_box<KID, NOUT, ACC, 3>(g, P, bw, bh, X0, Y0, xt, yt, acc0, acc1);
+                else
+                    small_box<KID, NOUT, ACC, 4>(g, P, bw, bh, X0, Y0, xt, yt, acc0, acc1);
             }
             unsigned long long big = __ballot(live && !small);
             while (big) {

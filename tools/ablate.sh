@@ -1,8 +1,10 @@
 #!/bin/bash
 # Build diagnostic variants of libasp_hip.so (never the product library):
-#   lib/libasp_hip_ablate<k>.so with -DASP_ABLATE=k
+#   lib/libasp_hip_<MACRO><k>.so with -D<MACRO>=k   (MACRO: ASP_ABLATE, ASP_ABLATE_SCATTER)
+#   usage: tools/ablate.sh MACRO k1 k2 ...
 cd "$(dirname "$0")/../astro-sph-tools_amd" || exit 1
+m=$1; shift
 for k in "$@"; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -munsafe-fp-atomics \
-    -DASP_ABLATE=$k -shared -o lib/libasp_hip_ablate$k.so csrc/asp_project2d.hip || exit 1
+    -D$m=$k -shared -o lib/libasp_hip_$m$k.so csrc/asp_project2d.hip csrc/asp_project3d.hip || exit 1
 done
