@@ -40,6 +40,21 @@ def zslab_bounds(z, world_size: int, sample: int = 1 << 20, seed: int = 0):
     return edges
 
 
+def _adjacent(o0, o1):
+    """A 1-D view over both maps when out1 directly follows out0 in one allocation."""
+    if o1 is None or o0.dtype != o1.dtype or o0.device != o1.device:
+        return None
+    n = o0.numel()
+    if o1.numel() != n or o1.data_ptr() != o0.data_ptr() + n * o0.element_size():
+        return None
+    base = o0.view(-1)
+    try:
+        import torch
+        return torch.as_strided(base, (2 * n,), (1,))
+    except Exception:  # pragma: no cover
+        return None
+
+
 def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
                       kernel="cubic", ratio: bool = False, op: str = "reduce", dst: int = 0,
                       group=None, out0=None, out1=None, projector=None,
@@ -61,7 +76,13 @@ def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     outs = [o0] if o1 is None else [o0, o1]
-    if world > 1:
+    fused = _adjacent(o0, o1)  # both maps in one buffer: one collective of 2 maps
+    if world > 1 and fused is not None and op in ("reduce", "allreduce"):
+        if op == "reduce":
+            dist.reduce(fused, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        else:
+            dist.all_reduce(fused, op=dist.ReduceOp.SUM, group=group)
+    elif world > 1:
         if op == "reduce":
             for t in outs:
                 dist.reduce(t, dst=dst, op=dist.ReduceOp.SUM, group=group)

@@ -230,8 +230,10 @@ def main():
         log(f"[rank {rank}] data ready: {n_local} particles in {time.time() - t0:.1f}s")
 
     ratio = args.map == "weighted"
-    out0 = torch.empty((G, G), dtype=torch.float32, device=dev)
-    out1 = torch.empty((G, G), dtype=torch.float32, device=dev) if a1 is not None else None
+    # both component maps in one allocation: N > 1 sums them with ONE RCCL collective
+    maps = torch.empty((2 if a1 is not None else 1, G, G), dtype=torch.float32, device=dev)
+    out0 = maps[0]
+    out1 = maps[1] if a1 is not None else None
 
     def step():
         if world > 1:

@@ -35,6 +35,12 @@ def _oracle_projector(u, v, h, a0, a1, *, image_size, extent, chunk_size, kernel
                                       chunk_size, *extent, kernel=kernel)
     t0 = torch.from_numpy(o0.astype(np.float32))
     t1 = None if o1 is None else torch.from_numpy(o1.astype(np.float32))
+    if out0 is not None:  # write into the caller's buffers, as the device path does
+        out0.copy_(t0)
+        t0 = out0
+        if t1 is not None and out1 is not None:
+            out1.copy_(t1)
+            t1 = out1
     return t0, t1
 
 
@@ -66,6 +72,13 @@ def _worker(rank, world, port, q):
                                        image_size=(G, G), extent=EXT, chunk_size=16,
                                        kernel="cubic", op=op, projector=_oracle_projector)
             res[op] = (o0.numpy().copy(), o1.numpy().copy())
+        maps = torch.empty((2, G, G))  # adjacent maps: one fused collective
+        for op in ("reduce", "allreduce"):
+            o0, o1 = project2d_sharded(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3],
+                                       image_size=(G, G), extent=EXT, chunk_size=16,
+                                       kernel="cubic", op=op, projector=_oracle_projector,
+                                       out0=maps[0], out1=maps[1])
+            res["fused_" + op] = (o0.numpy().copy(), o1.numpy().copy())
         res["n_local"] = int(keep.sum())
         q.put((rank, res))
     finally:
@@ -95,7 +108,11 @@ def test_zslab_sharded_sum_world2():
     tol = 1e-5 * np.abs(full0).max()
     np.testing.assert_allclose(out[0]["reduce"][0], full0, atol=tol, rtol=0)  # dst = 0
     np.testing.assert_allclose(out[0]["reduce"][1], full1, atol=1e-5 * np.abs(full1).max(), rtol=0)
+    np.testing.assert_allclose(out[0]["fused_reduce"][0], full0, atol=tol, rtol=0)
+    np.testing.assert_allclose(out[0]["fused_reduce"][1], full1, atol=1e-5 * np.abs(full1).max(),
+                               rtol=0)
     for r in range(world):
+        np.testing.assert_allclose(out[r]["fused_allreduce"][0], full0, atol=tol, rtol=0)
         np.testing.assert_allclose(out[r]["allreduce"][0], full0, atol=tol, rtol=0)
         rows = slice(r * G // world, (r + 1) * G // world)
         np.testing.assert_allclose(out[r]["reduce_scatter"][0], full0[rows], atol=tol, rtol=0)
