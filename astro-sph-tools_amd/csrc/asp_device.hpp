@@ -62,8 +62,8 @@ struct Box {
 // Per-record state for the pair loop.
 struct Prep {
     float u, v, h;
-    float thr;   // (2h)^2 in fp32
-    float band;  // |r2_32 - thr_32| <= band  ->  decide in fp64
+    float lo;    // fp32 r2 < lo: inside for sure;  lo <= r2 <= hi: decide in fp64;
+    float hi;    // r2 > hi: outside  (lo, hi = (2h)^2 -/+ error band; +-inf: always fp64)
     float hinv;  // 1/h
     float s0, s1;  // a * norm(h) (kAccF64) or a * norm(h) * 2^k_tile (kAccFix)
     Box b;
@@ -170,8 +170,12 @@ template <int KID>
 __device__ __forceinline__ double kernel_norm64(float h) {
     double hd = (double)h;
     double h3 = hd * hd * hd;
-    if constexpr (KID == 0) return (1.0 / M_PI) / h3;                    // _kernels.pyx:16,18
-    else if constexpr (KID == 1) return (21.0 / (16.0 * M_PI)) / h3;
+    // 1/h^3: hardware reciprocal + one Newton step (a few ulp; the value path is held to
+    // the fp32 tolerance).  Deterministic, so the fixed-point bound of K3 stays exact.
+    double r = __builtin_amdgcn_rcp(h3);
+    r = r * (2.0 - h3 * r);
+    if constexpr (KID == 0) return (1.0 / M_PI) * r;                     // _kernels.pyx:16,18
+    else if constexpr (KID == 1) return (21.0 / (16.0 * M_PI)) * r;
     else return 1.0;
 }
 
@@ -211,12 +215,16 @@ __device__ __forceinline__ bool prep_record(const Grid& g, float u, float v, flo
     P.h = h;
     float D = 2.0f * h;
     float Da = fabsf(D);
-    P.thr = D * D;
+    float thr = D * D;
     float eps = 0x1p-22f * (g.mg + Da);
     float band = 4.0f * Da * eps + 2.0f * eps * eps + 0x1p-20f * Da * Da;
     // Negative h narrows the chunk cull below the disc: decide every pair in fp64.
-    P.band = (h < 0.0f || !__builtin_isfinite(band)) ? __builtin_inff() : band;
-    P.hinv = 1.0f / h;
+    if (h < 0.0f || !__builtin_isfinite(band)) band = __builtin_inff();
+    // thr -/+ band rounded: the band bounds the decision error with a >= 2x margin and
+    // its 2^-20 D^2 term alone exceeds these two roundings (2^-24 thr each).
+    P.lo = thr - band;
+    P.hi = thr + band;
+    P.hinv = __builtin_amdgcn_rcpf(h);  // value path only (fp32 tolerance)
     if constexpr (ACC == kAccFix) {
         P.s0 = (float)ldexp(term_coef<KID>(a0, h), k0);
         P.s1 = (float)ldexp(term_coef<KID>(a1, h), k1);
@@ -245,8 +253,8 @@ __device__ __forceinline__ bool decide(const Grid& g, const Prep& P, int xi, int
     float dx = P.u - X;
     float dy = P.v - Y;
     r2 = dx * dx + dy * dy;
-    bool in = r2 < P.thr;
-    if (fabsf(r2 - P.thr) <= P.band) in = exact_pair(g, P.u, P.v, P.h, xi, yi);
+    bool in = r2 < P.lo;
+    if (r2 >= P.lo && r2 <= P.hi) in = exact_pair(g, P.u, P.v, P.h, xi, yi);
     return in;
 }
 

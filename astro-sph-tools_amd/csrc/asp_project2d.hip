@@ -377,8 +377,8 @@ __device__ __forceinline__ Prep bcast_prep(const Prep& P, int l) {
     Q.u = bcast(P.u, l);
     Q.v = bcast(P.v, l);
     Q.h = bcast(P.h, l);
-    Q.thr = bcast(P.thr, l);
-    Q.band = bcast(P.band, l);
+    Q.lo = bcast(P.lo, l);
+    Q.hi = bcast(P.hi, l);
     Q.hinv = bcast(P.hinv, l);
     Q.s0 = bcast(P.s0, l);
     Q.s1 = bcast(P.s1, l);
@@ -466,13 +466,13 @@ constexpr int kBandCols2 = kTile + 1;  // row-band threshold for two-map maps (o
 constexpr int kGatherCap = 128;  // list entries per round (5 KiB of LDS)
 
 struct GRec {  // 40 bytes; all lanes read the same entry (LDS broadcast)
-    float u, v, thr, band, hinv, s0, s1, h;
+    float u, v, lo, hi, hinv, s0, s1, h;
     int xr, yr;  // tile-local box: x0 | x1 << 16, y0 | y1 << 16
 };
 
 __device__ __forceinline__ GRec make_grec(const Prep& P, int X0, int Y0) {
     GRec r;
-    r.u = P.u; r.v = P.v; r.thr = P.thr; r.band = P.band; r.hinv = P.hinv;
+    r.u = P.u; r.v = P.v; r.lo = P.lo; r.hi = P.hi; r.hinv = P.hinv;
     r.s0 = P.s0; r.s1 = P.s1; r.h = P.h;
     r.xr = (P.b.x0 - X0) | ((P.b.x1 - X0) << 16);
     r.yr = (P.b.y0 - Y0) | ((P.b.y1 - Y0) << 16);
@@ -530,8 +530,8 @@ __device__ __forceinline__ void gather_rec(const Grid& g, const GRec& R, int X0,
         float dy = R.v - Yc[j];
         float r2 = dx2 + dy * dy;
         bool inb = ly0 + j >= y0 && ly0 + j <= y1;
-        bool a = inb && fabsf(r2 - R.thr) <= R.band;
-        bool in = inb && r2 < R.thr && !a;
+        bool a = inb && r2 >= R.lo && r2 <= R.hi;
+        bool in = inb && r2 < R.lo;
         amb |= a ? (1u << j) : 0u;
         float w = kernel_shape<KID>(__builtin_amdgcn_sqrtf(r2) * R.hinv);
         ra.add(j, in ? R.s0 * w : 0.0f, in ? R.s1 * w : 0.0f);
@@ -679,8 +679,8 @@ __device__ __forceinline__ void band_item(const Grid& g, const float4* __restric
                 if (r < ra0 || r > ra1) continue;  // wave-uniform
                 float dx = Q.u - Xr[r];
                 float r2 = dx * dx + dy2;
-                bool a = col && fabsf(r2 - Q.thr) <= Q.band;
-                bool in = col && r2 < Q.thr && !a;
+                bool a = col && r2 >= Q.lo && r2 <= Q.hi;
+                bool in = col && r2 < Q.lo;
                 amb |= a ? (1u << r) : 0u;
                 float w = kernel_shape<KID>(__builtin_amdgcn_sqrtf(r2) * Q.hinv);
                 ra.add(r, in ? Q.s0 * w : 0.0f, in ? Q.s1 * w : 0.0f);
@@ -725,6 +725,7 @@ template <int KID, int NOUT, int ACC, int S>
 __device__ __forceinline__ void small_box(const Grid& g, const Prep& P, int bw, int bh, int X0,
                                           int Y0, const float* xt, const float* yt,
                                           unsigned long long* acc0, unsigned long long* acc1) {
+    const int base = (P.b.x0 - X0) * kTile + (P.b.y0 - Y0);  // LDS word of pixel (0, 0)
     float dy2[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
@@ -742,12 +743,10 @@ __device__ __forceinline__ void small_box(const Grid& g, const Prep& P, int bw, 
             for (int j = 0; j < S; ++j) {
                 if (j < bh) {
                     float r2 = dx2 + dy2[j];
-                    bool in = r2 < P.thr;
-                    bool a = fabsf(r2 - P.thr) <= P.band;
+                    bool a = r2 >= P.lo && r2 <= P.hi;
                     amb |= a ? (1u << (ii * S + j)) : 0u;
-                    if (in && !a)
-                        accumulate<KID, NOUT, ACC>(P, r2, acc0, acc1,
-                                                   (xi - X0) * kTile + (P.b.y0 + j - Y0));
+                    if (r2 < P.lo)
+                        accumulate<KID, NOUT, ACC>(P, r2, acc0, acc1, base + ii * kTile + j);
                 }
             }
         }
@@ -770,7 +769,7 @@ __device__ __forceinline__ void small_box(const Grid& g, const Prep& P, int bw, 
 // tile (single-item tiles) or its int64 partial slab (split tiles).
 // ----------------------------------------------------------------------------------
 template <int KID, int NOUT, int ACC>
-__global__ __launch_bounds__(kDepBlock) void k_deposit(
+__global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_deposit(
     Grid g, const float4* __restrict__ recs, const Item* __restrict__ items,
     const int2* __restrict__ tile_k, unsigned long long* __restrict__ slabs,
     float* __restrict__ out0, float* __restrict__ out1, int flags) {
@@ -826,7 +825,7 @@ __global__ __launch_bounds__(kDepBlock) void k_deposit(
             q0 = n0;
             q1 = n1;
     #if ASP_ABLATE == 2
-            asm volatile("" ::"v"(P.u), "v"(P.v), "v"(P.thr), "v"(P.band), "v"(P.s0), "v"(P.s1),
+            asm volatile("" ::"v"(P.u), "v"(P.v), "v"(P.lo), "v"(P.hi), "v"(P.s0), "v"(P.s1),
                          "v"(P.b.x0), "v"(P.b.y1), "v"(live ? 1 : 0));
             continue;
     #endif
