@@ -44,7 +44,19 @@
 
 namespace asp {
 
-constexpr int kCountBlock = 512;  // count / scatter workgroup
+constexpr int kCountBlock = 512;  // count workgroup
+#ifndef ASP_SCATTER_BLOCK
+#define ASP_SCATTER_BLOCK 1024
+#endif
+#ifndef ASP_SCATTER_GROUP
+#define ASP_SCATTER_GROUP 4
+#endif
+// Scatter workgroup and how many consecutive count workgroups' particles it takes over:
+// fewer, wider scatter workgroups keep fewer partially written record lines open at a
+// time (each workgroup appends to its own segment of every tile), so more of them fill
+// in the caches before they are written back.
+constexpr int kScatterBlock = ASP_SCATTER_BLOCK;
+constexpr int kScatterGroup = ASP_SCATTER_GROUP;
 
 #ifndef ASP_ABLATE_SCATTER
 #define ASP_ABLATE_SCATTER 0  // diagnostic builds only: 1 = no first-record stores,
@@ -66,13 +78,14 @@ constexpr int kUnroll = 2;        // particles in flight per thread in count / s
 
 // Load kUnroll particles (lane-strided by the block size); h = 0 past the end, which has
 // no footprint.
+template <int NT>
 __device__ __forceinline__ void load_batch(const float* __restrict__ u,
                                            const float* __restrict__ v,
                                            const float* __restrict__ h, long long base,
                                            long long p1, float* pu, float* pv, float* ph) {
 #pragma unroll
     for (int k = 0; k < kUnroll; ++k) {
-        long long p = base + threadIdx.x + (long long)k * kCountBlock;
+        long long p = base + threadIdx.x + (long long)k * NT;
         bool in = p < p1;
         pu[k] = in ? u[p] : 0.0f;
         pv[k] = in ? v[p] : 0.0f;
@@ -98,10 +111,10 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
     constexpr long long kStep = (long long)kCountBlock * kUnroll;
     // Software pipeline: the next batch's loads are in flight while this batch is binned.
     float pu[kUnroll], pv[kUnroll], ph[kUnroll];
-    load_batch(u, v, h, p0, p1, pu, pv, ph);
+    load_batch<kCountBlock>(u, v, h, p0, p1, pu, pv, ph);
     for (long long base = p0; base < p1; base += kStep) {
         float nu[kUnroll], nv[kUnroll], nh[kUnroll];
-        load_batch(u, v, h, base + kStep, p1, nu, nv, nh);
+        load_batch<kCountBlock>(u, v, h, base + kStep, p1, nu, nv, nh);
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
             Box b;
@@ -130,13 +143,13 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
     for (int t = threadIdx.x; t < g.nstream * g.ntiles; t += kCountBlock) row[t] = lh[t];
 }
 
-template <int NOUT>
+template <int NOUT, int NT>
 __device__ __forceinline__ void load_props(const float* __restrict__ a0,
                                            const float* __restrict__ a1, long long base,
                                            long long p1, float* pa0, float* pa1) {
 #pragma unroll
     for (int k = 0; k < kUnroll; ++k) {
-        long long p = base + threadIdx.x + (long long)k * kCountBlock;
+        long long p = base + threadIdx.x + (long long)k * NT;
         bool in = p < p1;
         pa0[k] = in ? a0[p] : 0.0f;
         pa1[k] = (in && NOUT == 2) ? a1[p] : 0.0f;
@@ -150,7 +163,7 @@ __device__ __forceinline__ void load_props(const float* __restrict__ a0,
 // records it inserted, the fixed-point bound of K3b.
 // ----------------------------------------------------------------------------------
 template <int KID, int NOUT, int ACC>
-__global__ __launch_bounds__(kCountBlock) void k_scatter(
+__global__ __launch_bounds__(kScatterBlock) void k_scatter(
     const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
     const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long per_block,
     Grid g, const int* __restrict__ hist, const long long* __restrict__ tile_start,
@@ -160,16 +173,18 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
     extern __shared__ __attribute__((aligned(16))) int cur[];
     // per-wave staging for the paired record stores (NOUT == 2): 64 records x 32 B
     float4* stage = (float4*)(cur + g.nstream * g.ntiles);
-    unsigned* cm = (unsigned*)(stage + (NOUT == 2 ? (kCountBlock / 64) * 128 : 0));
-    const int* row = hist + (long long)blockIdx.x * g.nstream * g.ntiles;
-    for (int t = threadIdx.x; t < g.nstream * g.ntiles; t += kCountBlock)
+    unsigned* cm = (unsigned*)(stage + (NOUT == 2 ? (kScatterBlock / 64) * 128 : 0));
+    // this workgroup takes over count workgroups kScatterGroup * b ..: its cursors start
+    // at the prefix row of the first of them
+    const int* row = hist + (long long)blockIdx.x * kScatterGroup * g.nstream * g.ntiles;
+    for (int t = threadIdx.x; t < g.nstream * g.ntiles; t += kScatterBlock)
         cur[t] = (int)tile_start[t] + row[t];  // n_recs < 2^31 (checked on the host)
     if constexpr (ACC == kAccFix)
-        for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kCountBlock) cm[t] = 0u;
+        for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kScatterBlock) cm[t] = 0u;
     __syncthreads();
     long long p0 = (long long)blockIdx.x * per_block;
     long long p1 = min(n, p0 + per_block);
-    constexpr long long kStep = (long long)kCountBlock * kUnroll;
+    constexpr long long kStep = (long long)kScatterBlock * kUnroll;
     // Software pipeline: issue the next batch's loads BEFORE this batch's record stores,
     // so waiting for them (vmcnt counts loads and stores in issue order) never waits on
     // the scattered stores.
@@ -177,15 +192,15 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
     int first_slot[kUnroll];
 #pragma unroll
     for (int k = 0; k < kUnroll; ++k) first_slot[k] = -1;
-    load_batch(u, v, h, p0, p1, pu, pv, ph);
-    load_props<NOUT>(a0, a1, p0, p1, pa0, pa1);
+    load_batch<kScatterBlock>(u, v, h, p0, p1, pu, pv, ph);
+    load_props<NOUT, kScatterBlock>(a0, a1, p0, p1, pa0, pa1);
     for (long long base = p0; base < p1; base += kStep) {
         float nu[kUnroll], nv[kUnroll], nh[kUnroll], na0[kUnroll], na1[kUnroll];
-        load_batch(u, v, h, base + kStep, p1, nu, nv, nh);
-        load_props<NOUT>(a0, a1, base + kStep, p1, na0, na1);
+        load_batch<kScatterBlock>(u, v, h, base + kStep, p1, nu, nv, nh);
+        load_props<NOUT, kScatterBlock>(a0, a1, base + kStep, p1, na0, na1);
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
-            long long p = base + threadIdx.x + (long long)k * kCountBlock;
+            long long p = base + threadIdx.x + (long long)k * kScatterBlock;
             Box b;
             if (!footprint(g, pu[k], pv[k], ph[k], b)) continue;
             unsigned c0 = 0u, c1 = 0u;
@@ -268,8 +283,8 @@ __global__ __launch_bounds__(kCountBlock) void k_scatter(
     }
     if constexpr (ACC == kAccFix) {
         __syncthreads();
-        unsigned* out = cmx + (long long)blockIdx.x * g.ntiles * NOUT;
-        for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kCountBlock) out[t] = cm[t];
+        unsigned* out = cmx + (long long)blockIdx.x * g.ntiles * NOUT;  // per scatter block
+        for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kScatterBlock) out[t] = cm[t];
     }
 }
 
@@ -1139,10 +1154,12 @@ static bool make_grid(double x_min, double x_max, double y_min, double y_max, in
     return true;
 }
 
+constexpr int kMaxBinBlocks = 1024;  // count / scatter workgroups (hist rows)
 constexpr int kMaxTiles = 4096;  // K1/K3 LDS: 2 cursors + per-tile max (16 B/tile at 2 maps)
 
 struct Plan {
     long long n, nblk, per_block;
+    long long nblk_s;  // scatter workgroups (kScatterGroup count workgroups each)
     int n_items, n_merges, n_slabs, n_wide;
     long long n_recs;
 };
@@ -1159,10 +1176,10 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     {
         StageMark m(ws, kSScatter, st);
         size_t lds = (size_t)g.nstream * g.ntiles * sizeof(int) +
-                     (NOUT == 2 ? (size_t)(kCountBlock / 64) * 128 * sizeof(float4) : 0) +
+                     (NOUT == 2 ? (size_t)(kScatterBlock / 64) * 128 * sizeof(float4) : 0) +
                      (ACC == kAccFix ? (size_t)g.ntiles * NOUT * sizeof(unsigned) : 0);
-        hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC>), dim3((unsigned)pl.nblk), dim3(kCountBlock),
-                           lds, st, u, v, h, a0, a1, pl.n, pl.per_block, g, (const int*)ws.hist.p,
+        hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC>), dim3((unsigned)pl.nblk_s), dim3(kScatterBlock),
+                           lds, st, u, v, h, a0, a1, pl.n, pl.per_block * kScatterGroup, g, (const int*)ws.hist.p,
                            (const long long*)ws.tile_start.p, (float4*)ws.recs.p,
                            (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc);
         ASP_LAUNCHED();
@@ -1171,7 +1188,7 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     if (ACC == kAccFix) {
         StageMark m(ws, kSScale, st);
         hipLaunchKernelGGL((k_tilescale<NOUT>), dim3((g.ntiles + 63) / 64), dim3(kBlock), 0, st,
-                           (const unsigned*)ws.cmx.p, (int)pl.nblk, g.ntiles, g.nstream,
+                           (const unsigned*)ws.cmx.p, (int)pl.nblk_s, g.ntiles, g.nstream,
                            (const int*)ws.tile_total.p, (int2*)ws.tile_k.p);
         ASP_LAUNCHED();
         m.done();
@@ -1306,12 +1323,15 @@ static int project2d(const float* u, const float* v, const float* h, const float
         }
     } else {
         ASP_TRY(ensure_morton(ws, g.ntx, g.nty, st));
-        pl.nblk = std::min<long long>(1024, std::max<long long>(1, (n + 8191) / 8192));
+        long long max_blk = kMaxBinBlocks;
+        if (const char* e = getenv("ASP_BIN_BLOCKS")) max_blk = std::max(1, atoi(e));
+        pl.nblk = std::min<long long>(max_blk, std::max<long long>(1, (n + 8191) / 8192));
         pl.per_block = (n + pl.nblk - 1) / pl.nblk;
         pl.nblk = (n + pl.per_block - 1) / pl.per_block;
+        pl.nblk_s = (pl.nblk + kScatterGroup - 1) / kScatterGroup;
         ASP_TRY(ensure(ws.hist, (size_t)pl.nblk * g.nstream * g.ntiles * sizeof(int)));
         const bool det = (flags & ASP_F_DETERMINISTIC) != 0;
-        if (det) ASP_TRY(ensure(ws.cmx, (size_t)pl.nblk * g.ntiles * nout * sizeof(unsigned)));
+        if (det) ASP_TRY(ensure(ws.cmx, (size_t)pl.nblk_s * g.ntiles * nout * sizeof(unsigned)));
         ASP_TRY(ensure(ws.tile_total, (size_t)2 * g.ntiles * sizeof(int)));
         ASP_TRY(ensure(ws.tile_start, (size_t)2 * g.ntiles * sizeof(long long)));
         ASP_TRY(ensure(ws.tile_k, (size_t)g.ntiles * sizeof(int2)));
