@@ -74,17 +74,21 @@ __device__ __forceinline__ int tile_column(const Grid& g, const Box& b, bool may
     int hh = min(b.y1, ty * kTile + kTile - 1) - max(b.y0, ty * kTile) + 1;
     return hh >= g.band_cols ? t + g.ntiles : t;
 }
-constexpr int kUnroll = 2;        // particles in flight per thread in count / scatter
+constexpr int kUnroll = 2;        // particles in flight per thread in scatter
+#ifndef ASP_COUNT_UNROLL
+#define ASP_COUNT_UNROLL 4
+#endif
+constexpr int kCountUnroll = ASP_COUNT_UNROLL;  // ... and in count
 
 // Load kUnroll particles (lane-strided by the block size); h = 0 past the end, which has
 // no footprint.
-template <int NT>
+template <int NT, int U = kUnroll>
 __device__ __forceinline__ void load_batch(const float* __restrict__ u,
                                            const float* __restrict__ v,
                                            const float* __restrict__ h, long long base,
                                            long long p1, float* pu, float* pv, float* ph) {
 #pragma unroll
-    for (int k = 0; k < kUnroll; ++k) {
+    for (int k = 0; k < U; ++k) {
         long long p = base + threadIdx.x + (long long)k * NT;
         bool in = p < p1;
         pu[k] = in ? u[p] : 0.0f;
@@ -108,15 +112,15 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
     long long p0 = (long long)blockIdx.x * per_block;
     long long p1 = min(n, p0 + per_block);
     int nwide = 0;
-    constexpr long long kStep = (long long)kCountBlock * kUnroll;
+    constexpr long long kStep = (long long)kCountBlock * kCountUnroll;
     // Software pipeline: the next batch's loads are in flight while this batch is binned.
-    float pu[kUnroll], pv[kUnroll], ph[kUnroll];
-    load_batch<kCountBlock>(u, v, h, p0, p1, pu, pv, ph);
+    float pu[kCountUnroll], pv[kCountUnroll], ph[kCountUnroll];
+    load_batch<kCountBlock, kCountUnroll>(u, v, h, p0, p1, pu, pv, ph);
     for (long long base = p0; base < p1; base += kStep) {
-        float nu[kUnroll], nv[kUnroll], nh[kUnroll];
-        load_batch<kCountBlock>(u, v, h, base + kStep, p1, nu, nv, nh);
+        float nu[kCountUnroll], nv[kCountUnroll], nh[kCountUnroll];
+        load_batch<kCountBlock, kCountUnroll>(u, v, h, base + kStep, p1, nu, nv, nh);
 #pragma unroll
-        for (int k = 0; k < kUnroll; ++k) {
+        for (int k = 0; k < kCountUnroll; ++k) {
             Box b;
             if (!footprint(g, pu[k], pv[k], ph[k], b)) continue;
             int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
@@ -131,7 +135,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
                     atomicAdd(&lh[tile_column(g, b, mb, tx, ty)], 1);
         }
 #pragma unroll
-        for (int k = 0; k < kUnroll; ++k) {
+        for (int k = 0; k < kCountUnroll; ++k) {
             pu[k] = nu[k];
             pv[k] = nv[k];
             ph[k] = nh[k];
@@ -148,7 +152,7 @@ __device__ __forceinline__ void load_props(const float* __restrict__ a0,
                                            const float* __restrict__ a1, long long base,
                                            long long p1, float* pa0, float* pa1) {
 #pragma unroll
-    for (int k = 0; k < kUnroll; ++k) {
+    for (int k = 0; k < kCountUnroll; ++k) {
         long long p = base + threadIdx.x + (long long)k * NT;
         bool in = p < p1;
         pa0[k] = in ? a0[p] : 0.0f;
