@@ -155,7 +155,7 @@ __device__ __forceinline__ void load_props(const float* __restrict__ a0,
                                            const float* __restrict__ a1, long long base,
                                            long long p1, float* pa0, float* pa1) {
 #pragma unroll
-    for (int k = 0; k < kCountUnroll; ++k) {
+    for (int k = 0; k < kUnroll; ++k) {
         long long p = base + threadIdx.x + (long long)k * NT;
         bool in = p < p1;
         pa0[k] = in ? a0[p] : 0.0f;

@@ -185,6 +185,30 @@ def run_cube(args, world, rank, local, dev):
         dist.destroy_process_group()
 
 
+def output_check(out0, out1, a0, a1, ratio, world=1):
+    """Size-independent sanity of the timed map (the parity proper is tests/): finite,
+    non-negative component sums (W >= 0, m > 0), and for the mass-weighted map every pixel a
+    weighted MEAN of particle temperatures -- inside [min T, max T] wherever sum m W > 0,
+    exactly 0 elsewhere."""
+    import torch
+    if not bool(torch.isfinite(out0).all().item()):
+        return False
+    if not ratio:
+        return bool((out0 >= 0).all().item()) and float(out0.sum().item()) > 0
+    if not bool(torch.isfinite(out1).all().item()) or not bool((out1 >= 0).all().item()):
+        return False
+    t = a0 / a1
+    rng = torch.stack([-t.min(), t.max()]).double()
+    if world > 1:  # the reduced map averages every rank's particles
+        import torch.distributed as dist
+        dist.all_reduce(rng, op=dist.ReduceOp.MAX)
+    lo, hi = -float(rng[0].item()), float(rng[1].item())
+    cov = out1 > 0
+    inside = (out0[cov] >= lo * (1 - 1e-5)) & (out0[cov] <= hi * (1 + 1e-5))
+    return (bool(cov.any().item()) and bool(inside.all().item())
+            and bool((out0[~cov] == 0).all().item()))
+
+
 def main():
     args = parse()
     import torch
@@ -264,7 +288,7 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    ok = bool(torch.isfinite(out0).all().item()) and float(out0.abs().sum().item()) > 0
+    ok = output_check(out0, out1, a0, a1, ratio, world)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -325,6 +349,9 @@ def main():
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not ok:
+        log("bench: the timed map FAILED its output check")
+        sys.exit(3)
 
 
 if __name__ == "__main__":
