@@ -130,10 +130,10 @@ def ptr(a, t=_f):
 
 
 def last_stats(device: int = 0):
-    s = (C.c_int64 * 8)()
-    check(lib().asp_last_stats(device, s, 8))
+    s = (C.c_int64 * 9)()
+    check(lib().asp_last_stats(device, s, 9))
     return {"records": s[0], "items": s[1], "wide": s[2], "tile": s[3], "tiles": s[4],
-            "records_per_item": s[5], "merges": s[6], "slabs": s[7]}
+            "records_per_item": s[5], "merges": s[6], "slabs": s[7], "chunks": s[8]}
 
 
 def profile(device: int = 0, enable: bool = True):

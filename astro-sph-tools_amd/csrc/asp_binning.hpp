@@ -27,14 +27,19 @@ enum Ctr {
 
 // ----------------------------------------------------------------------------------
 // K2a: per tile, exclusive prefix of hist over blocks (in place); tile totals.
-// 64 tiles per workgroup (one per lane), the 4 waves split the block range.
+// 64 tiles per workgroup (one per lane), the 4 waves split the block range.  Blocks come
+// in chunks of cb (blockIdx.y = chunk): the prefix restarts at every chunk and chunk c's
+// totals go to tile_total[c * ntiles + t] (one chunk: cb >= nblk, gridDim.y = 1).
 // ----------------------------------------------------------------------------------
 static __global__ __launch_bounds__(kBlock) void k_colscan(int* __restrict__ hist, int nblk, int ntiles,
-                                                    int* __restrict__ tile_total) {
+                                                    int* __restrict__ tile_total, int cb) {
     __shared__ int part[4][64];
     int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int t = blockIdx.x * 64 + lane;
-    int b0 = (int)((long long)nblk * w / 4), b1 = (int)((long long)nblk * (w + 1) / 4);
+    int c0 = (int)min((long long)nblk, (long long)blockIdx.y * cb);
+    int cn = min(nblk - c0, cb);
+    tile_total += (long long)blockIdx.y * ntiles;
+    int b0 = c0 + (int)((long long)cn * w / 4), b1 = c0 + (int)((long long)cn * (w + 1) / 4);
     int s = 0;
     if (t < ntiles) {
         int b = b0;

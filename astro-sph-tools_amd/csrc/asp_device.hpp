@@ -66,6 +66,8 @@ struct Prep {
     float hi;    // r2 > hi: outside  (lo, hi = (2h)^2 -/+ error band; +-inf: always fp64)
     float hinv;  // 1/h
     float s0, s1;  // a * norm(h) (kAccF64) or a * norm(h) * 2^k_tile (kAccFix)
+    float thr;   // (2h)^2 in fp32
+    float band;  // |r2 - thr| <= band: the fp32 decision is not trusted (inf: never)
     Box b;
 };
 
@@ -132,8 +134,11 @@ __device__ __forceinline__ void chunk_range(double w, double h, double w_min, do
 
 // Candidate pixel box of a particle: a superset of the pixels that can pass the exact
 // test.  fp32 estimate of (w - 2|h| - w_min) / pitch with a margin delta that bounds its
-// rounding error (~10x over: 2^-19 relative to the operand magnitudes, plus 2^-12 px so
-// that a corner at exactly 2h stays a candidate).  False when nothing can pass.
+// rounding error: at most ~6 roundings of 2^-24 relative to (|w| + |w_min| + 2|h|) / pitch
+// (w_min and 1/pitch to fp32, the difference, the product, the two offsets), so 2^-20
+// leaves a 2.7x margin; plus 2^-12 px so that a corner at exactly 2h stays a candidate.
+// (A wider margin makes more pixel-scale boxes 4 corners wide, which leave the fast 3 x 3
+// deposit.)  False when nothing can pass.
 __device__ __forceinline__ bool footprint(const Grid& g, float u, float v, float h, Box& b) {
     float hd = fabsf(2.0f * h);
     if (!(hd > 0.0f) || !__builtin_isfinite(hd)) {
@@ -144,8 +149,8 @@ __device__ __forceinline__ bool footprint(const Grid& g, float u, float v, float
     if (!__builtin_isfinite(u) || !__builtin_isfinite(v)) return false;
     float cx = (u - g.xminf) * g.ipsx, rx = hd * g.ipsx;
     float cy = (v - g.yminf) * g.ipsy, ry = hd * g.ipsy;
-    float dx = (fabsf(u) + fabsf(g.xminf) + hd) * g.ipsx * 0x1p-19f + 0x1p-12f;
-    float dy = (fabsf(v) + fabsf(g.yminf) + hd) * g.ipsy * 0x1p-19f + 0x1p-12f;
+    float dx = (fabsf(u) + fabsf(g.xminf) + hd) * g.ipsx * 0x1p-20f + 0x1p-12f;
+    float dy = (fabsf(v) + fabsf(g.yminf) + hd) * g.ipsy * 0x1p-20f + 0x1p-12f;
     float fx0 = fmaxf(ceilf(cx - rx - dx), 0.0f);
     float fx1 = fminf(floorf(cx + rx + dx), (float)(g.nx - 1));
     float fy0 = fmaxf(ceilf(cy - ry - dy), 0.0f);
@@ -224,6 +229,8 @@ __device__ __forceinline__ bool prep_record(const Grid& g, float u, float v, flo
     // its 2^-20 D^2 term alone exceeds these two roundings (2^-24 thr each).
     P.lo = thr - band;
     P.hi = thr + band;
+    P.thr = thr;
+    P.band = band;
     P.hinv = __builtin_amdgcn_rcpf(h);  // value path only (fp32 tolerance)
     if constexpr (ACC == kAccFix) {
         P.s0 = (float)ldexp(term_coef<KID>(a0, h), k0);
@@ -236,7 +243,7 @@ __device__ __forceinline__ bool prep_record(const Grid& g, float u, float v, flo
 }
 
 // Reference decision in fp64 (.pyx:13-14, :20-31 and the chunk cull): the slow path.
-__device__ __attribute__((noinline)) bool exact_pair(const Grid& g, float u, float v, float h,
+__device__ __forceinline__ bool exact_pair(const Grid& g, float u, float v, float h,
                                                       int xi, int yi) {
     double ud = u, vd = v, hd = h;
     double dx = ud - corner_x(g, xi);

@@ -33,6 +33,7 @@ struct Buf {
 };
 
 constexpr int kStages = 17;
+constexpr int kMarks = 8;  // launches of one stage timed per call
 enum Stage {
     kSMemset = 0, kSCount, kSColscan, kSTilescan, kSScatter, kSScale, kSDeposit, kSMerge,
     kSWide, kSRatio,
@@ -46,8 +47,9 @@ struct Workspace {
     // HIP-event profiling (asp_profile): per-stage start/stop events of the last call,
     // folded into the running sums at the next call or at asp_profile_read.
     bool prof = false;
-    hipEvent_t ev[2 * kStages] = {};
-    bool ev_live[kStages] = {};
+    hipEvent_t ev[kStages][kMarks][2] = {};
+    int ev_live[kStages] = {};  // marks recorded in the last call (a stage may launch
+                                // once per particle chunk)
     double stage_ms[kStages] = {};
     long long stage_n[kStages] = {};
     Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
@@ -56,20 +58,34 @@ struct Workspace {
     int morton_ntx = -1, morton_nty = -1;
     Buf morton3;  // brick order of the 3-D cube
     int morton3_key[3] = {-1, -1, -1};
-    long long stats[8] = {0};
+    long long stats[9] = {0};
+    // Chunked 2-D pipeline: deposits run on a side stream, each behind its chunk's scatter.
+    hipStream_t side = nullptr;
+    hipEvent_t chunk_ev[kMarks] = {};
+    hipEvent_t done_ev = nullptr;
 };
+
+inline int ensure_side(Workspace& ws) {
+    if (ws.side) return ASP_OK;
+    ASP_HIP(hipStreamCreateWithFlags(&ws.side, hipStreamNonBlocking));
+    for (int c = 0; c < kMarks; ++c)
+        ASP_HIP(hipEventCreateWithFlags(&ws.chunk_ev[c], hipEventDisableTiming));
+    ASP_HIP(hipEventCreateWithFlags(&ws.done_ev, hipEventDisableTiming));
+    return ASP_OK;
+}
 
 inline Workspace g_ws[64];
 
 inline int prof_fold(Workspace& ws) {
     for (int k = 0; k < kStages; ++k) {
-        if (!ws.ev_live[k]) continue;
-        ASP_HIP(hipEventSynchronize(ws.ev[2 * k + 1]));
-        float ms = 0.0f;
-        ASP_HIP(hipEventElapsedTime(&ms, ws.ev[2 * k], ws.ev[2 * k + 1]));
-        ws.stage_ms[k] += ms;
-        ws.stage_n[k] += 1;
-        ws.ev_live[k] = false;
+        for (int j = 0; j < ws.ev_live[k]; ++j) {
+            ASP_HIP(hipEventSynchronize(ws.ev[k][j][1]));
+            float ms = 0.0f;
+            ASP_HIP(hipEventElapsedTime(&ms, ws.ev[k][j][0], ws.ev[k][j][1]));
+            ws.stage_ms[k] += ms;
+            ws.stage_n[k] += 1;
+        }
+        ws.ev_live[k] = 0;
     }
     return ASP_OK;
 }
@@ -79,13 +95,15 @@ struct StageMark {
     Workspace& ws;
     int k;
     hipStream_t st;
-    StageMark(Workspace& w, int stage, hipStream_t s) : ws(w), k(stage), st(s) {
-        if (ws.prof) (void)hipEventRecord(ws.ev[2 * k], st);
+    bool on;
+    StageMark(Workspace& w, int stage, hipStream_t s)
+        : ws(w), k(stage), st(s), on(w.prof && w.ev_live[stage] < kMarks) {
+        if (on) (void)hipEventRecord(ws.ev[k][ws.ev_live[k]][0], st);
     }
     void done() {
-        if (ws.prof) {
-            (void)hipEventRecord(ws.ev[2 * k + 1], st);
-            ws.ev_live[k] = true;
+        if (on) {
+            (void)hipEventRecord(ws.ev[k][ws.ev_live[k]][1], st);
+            ws.ev_live[k] += 1;
         }
     }
 };

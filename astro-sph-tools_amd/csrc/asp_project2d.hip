@@ -175,21 +175,22 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long per_block,
     Grid g, const int* __restrict__ hist, const long long* __restrict__ tile_start,
     float4* __restrict__ recs, unsigned* __restrict__ cmx, int* __restrict__ wide_list,
-    int* __restrict__ ctr) {
+    int* __restrict__ ctr, int blk0, int grp) {
     // absolute record cursors, regular runs then large runs (2 * ntiles)
     extern __shared__ __attribute__((aligned(16))) int cur[];
     // per-wave staging for the paired record stores (NOUT == 2): 64 records x 32 B
     float4* stage = (float4*)(cur + g.nstream * g.ntiles);
     unsigned* cm = (unsigned*)(stage + (NOUT == 2 ? (kScatterBlock / 64) * 128 : 0));
-    // this workgroup takes over count workgroups kScatterGroup * b ..: its cursors start
-    // at the prefix row of the first of them
-    const int* row = hist + (long long)blockIdx.x * kScatterGroup * g.nstream * g.ntiles;
+    // this workgroup (global index sb = blk0 + blockIdx.x) takes over count workgroups
+    // grp * sb ..: its cursors start at the prefix row of the first of them
+    const long long sb = blk0 + (long long)blockIdx.x;
+    const int* row = hist + sb * grp * g.nstream * g.ntiles;
     for (int t = threadIdx.x; t < g.nstream * g.ntiles; t += kScatterBlock)
         cur[t] = (int)tile_start[t] + row[t];  // n_recs < 2^31 (checked on the host)
     if constexpr (ACC == kAccFix)
         for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kScatterBlock) cm[t] = 0u;
     __syncthreads();
-    long long p0 = (long long)blockIdx.x * per_block;
+    long long p0 = sb * per_block;
     long long p1 = min(n, p0 + per_block);
     constexpr long long kStep = (long long)kScatterBlock * kUnroll;
     // Software pipeline: issue the next batch's loads BEFORE this batch's record stores,
@@ -343,7 +344,7 @@ __global__ __launch_bounds__(kBlock) void k_tilescale(const unsigned* __restrict
 // Pair accumulation into the LDS tile (int64 fixed point)
 // ----------------------------------------------------------------------------------
 #ifndef ASP_ABLATE
-#define ASP_ABLATE 0  // diagnostic builds only (tools/ablate.sh): 1 = no LDS atomics,
+#define ASP_ABLATE 0  // diagnostic builds only (tools/ablate.sh): 4 = conflict-free atomics, 1 = no LDS atomics,
                       // 2 = no pair loop, 3 = no record prep
 #endif
 
@@ -786,6 +787,139 @@ __device__ __forceinline__ void small_box(const Grid& g, const Prep& P, int bw, 
     }
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) {  // v_pk_fma_f32
+    return __builtin_elementwise_fma(a, b, c);
+}
+
+// Kernel shape on two pairs at once (packed fp32: v_pk_fma_f32 / v_pk_mul_f32).  Only
+// pairs with fp32 r2 < (2h)^2 use the result, so q < 2 up to rounding and the Wendland
+// clamp is not needed there (a q a few ulp over 2 gives a term ~1e-28 of the peak).
+template <int KID>
+__device__ __forceinline__ f2v kernel_shape2(f2v q) {
+    if constexpr (KID == 0) {
+        f2v q2 = q * q;
+        f2v a = fma2(q2, fma2(q, f2v{0.75f, 0.75f}, f2v{-1.5f, -1.5f}), f2v{1.0f, 1.0f});
+        f2v t = f2v{2.0f, 2.0f} - q;
+        f2v b = (t * t) * (t * 0.25f);
+        return f2v{q.x < 1.0f ? a.x : b.x, q.y < 1.0f ? a.y : b.y};
+    } else if constexpr (KID == 1) {
+        f2v t = fma2(q, f2v{-0.5f, -0.5f}, f2v{1.0f, 1.0f});
+        f2v t2 = t * t;
+        return (t2 * t2) * fma2(q, f2v{2.0f, 2.0f}, f2v{1.0f, 1.0f});
+    } else {
+        return f2v{1.0f, 1.0f};
+    }
+}
+
+__device__ __forceinline__ f2v sqrt2(f2v x) {
+    return f2v{__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+}
+
+// Lane-per-record deposit of a box of at most 3 x 3 pixel corners (pixel-scale h), the
+// common case: the nine fp32 r2 and kernel values are computed branch-free in packed
+// fp32, and every pair with r2 < (2h)^2 is added.  Valid only when no pair lies in the
+// error band (min |r2 - thr| > band): returns false for such a record WITHOUT touching the
+// tile; the caller defers it to the exact path (small_box).
+template <int KID, int NOUT, int ACC>
+__device__ __forceinline__ bool small3_fast(const Prep& P, int bw, int bh, int X0, int Y0,
+                                            const float* xt, const float* yt,
+                                            unsigned long long* acc0, unsigned long long* acc1) {
+    constexpr float kFar = 1e18f;  // outside the box: r2 ~ 1e36, far from any threshold
+    float dx2[3];
+    f2v dy2;
+    float dyc2;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        float d = P.u - xt[min(P.b.x0 + i, P.b.x1) - X0];
+        d = i < bw ? d : kFar;
+        dx2[i] = d * d;
+    }
+    {
+        float d0 = P.v - yt[P.b.y0 - Y0];
+        float d1 = P.v - yt[min(P.b.y0 + 1, P.b.y1) - Y0];
+        float d2 = P.v - yt[min(P.b.y0 + 2, P.b.y1) - Y0];
+        d1 = bh > 1 ? d1 : kFar;
+        d2 = bh > 2 ? d2 : kFar;
+        f2v d = f2v{d0, d1};
+        dy2 = d * d;
+        dyc2 = d2 * d2;
+    }
+    f2v r2[3];
+    float r2c[3];
+    float m = __builtin_inff();
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        r2[i] = dy2 + dx2[i];
+        r2c[i] = dx2[i] + dyc2;
+        f2v e = r2[i] - P.thr;
+        m = fminf(m, fminf(fminf(fabsf(e.x), fabsf(e.y)), fabsf(r2c[i] - P.thr)));
+    }
+    if (!(m > P.band)) return false;  // a pair in the band (or NaN): exact path
+#if ASP_ABLATE == 4  // diagnostic: lanes of each 32-lane half on distinct LDS banks (wrong map)
+    const int base = ((P.b.x0 - X0) & 60) * kTile + (threadIdx.x & 31);
+#else
+    const int base = (P.b.x0 - X0) * kTile + (P.b.y0 - Y0);
+#endif
+    const f2v hv = f2v{P.hinv, P.hinv};
+    // column j = 2 of rows 0, 1 as one packed pair, row 2 with a dummy partner
+    f2v wc01 = kernel_shape2<KID>(sqrt2(f2v{r2c[0], r2c[1]}) * hv);
+    f2v wc2 = kernel_shape2<KID>(sqrt2(f2v{r2c[2], 0.0f}) * hv);
+    const float wc[3] = {wc01.x, wc01.y, wc2.x};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        f2v w = kernel_shape2<KID>(sqrt2(r2[i]) * hv);
+        f2v t0 = w * P.s0, t1 = w * P.s1;
+        f2v c = f2v{wc[i], wc[i]} * f2v{P.s0, P.s1};
+        const int k = base + i * kTile;
+        if (r2[i].x < P.thr) {
+            acc_add<ACC>(&acc0[k], t0.x);
+            if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k], t1.x);
+        }
+        if (r2[i].y < P.thr) {
+            acc_add<ACC>(&acc0[k + 1], t0.y);
+            if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k + 1], t1.y);
+        }
+        if (r2c[i] < P.thr) {
+            acc_add<ACC>(&acc0[k + 2], c.x);
+            if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k + 2], c.y);
+        }
+    }
+    return true;
+}
+
+#ifndef ASP_FAST3
+#define ASP_FAST3 1  // 0: diagnostic builds only, the unpacked 3 x 3 body with in-loop band pairs
+#endif
+
+// Per-wave list of records deferred to the exact path (a pair in the error band).
+constexpr int kDeferCap = 128;
+
+// Exact body for deferred records: lanes 0 .. cnt-1 take list entries first .. first+cnt-1
+// (record indices within the item), reload and re-prepare them and decide every pair
+// with the error-band / fp64 logic of small_box.  Wave-level: no block barrier.
+template <int KID, int NOUT, int ACC>
+__device__ __forceinline__ void deferred(const Grid& g, const float4* __restrict__ recs,
+                                      long long start, const int* dlist, int first, int cnt,
+                                      int X0, int Y0, int TW, int TH, int2 kk, const float* xt,
+                                      const float* yt, unsigned long long* acc0,
+                                      unsigned long long* acc1, int lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int idx = lane < cnt ? dlist[first + lane] : -1;
+    __builtin_amdgcn_wave_barrier();
+    if (idx < 0) return;
+    float4 r0, r1 = make_float4(0.f, 0.f, 0.f, 0.f);
+    load_rec4<NOUT>(recs, start + idx, r0, r1);
+    Prep P;
+    if (!prep_record<KID, ACC>(g, r0.x, r0.y, r0.z, r0.w, r1.x, kk.x, kk.y, P)) return;
+    if (!clip(P.b, X0, Y0, TW, TH)) return;
+    small_box<KID, NOUT, ACC, 4>(g, P, P.b.x1 - P.b.x0 + 1, P.b.y1 - P.b.y0 + 1, X0, Y0, xt, yt,
+                                 acc0, acc1);
+}
+
 // ----------------------------------------------------------------------------------
 // K4: deposit one work item (a run of records of one tile) into LDS, then write the
 // tile (single-item tiles) or its int64 partial slab (split tiles).
@@ -806,7 +940,22 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
     int X0 = tx * kTile, Y0 = ty * kTile;
     int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
     if (it.count == 0) {  // empty tile: the map is 0 there
-        if (flags & kFlagAccumulate) return;
+        if (flags & kFlagAccumulate) {
+            // last chunk of a chunked mass-weighted map: the earlier chunks left the two
+            // raw sums here, the ratio is still to be taken
+            if constexpr (NOUT == 2) {
+                if (flags & kFlagRatio) {
+                    for (int k = threadIdx.x; k < kTilePix; k += kDepBlock) {
+                        int lx = k >> kTileShift, ly = k & (kTile - 1);
+                        if (lx >= TW || ly >= TH) continue;
+                        long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
+                        float v1 = out1[o];
+                        out0[o] = v1 != 0.0f ? out0[o] / v1 : 0.0f;
+                    }
+                }
+            }
+            return;
+        }
         for (int k = threadIdx.x; k < kTilePix; k += kDepBlock) {
             int lx = k >> kTileShift, ly = k & (kTile - 1);
             if (lx >= TW || ly >= TH) continue;
@@ -819,7 +968,10 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
     const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
     tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
     {
+        __shared__ int defer_lds[kDepBlock / 64][kDeferCap];
         int lane = threadIdx.x & 63;
+        int* dlist = defer_lds[threadIdx.x >> 6];
+        int ndef = 0;  // wave-uniform
         // Software pipeline, two batches deep: batches i+1 and i+2 load while batch i deposits
         // (16 waves/CU x 64 lanes x 32 B x 2 in flight per CU).
         float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, q0 = r0, q1 = r0;
@@ -853,14 +1005,36 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
     #endif
             int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
             bool small = live && bw <= 4 && bh <= 4;
+            bool amb = false;
             if (small) {
-                // lane-per-record; 3 x 3 unrolled body when no lane of the wave needs 4
-                // (pixel-scale h: a 2h = 1.5 px disc spans 3 corners per axis but for a
-                // measure-zero set of centres)
+                // lane-per-record.  Boxes of <= 3 x 3 corners (pixel-scale h: a 2h = 1.5 px
+                // disc spans 3 corners per axis unless its centre sits within the box
+                // margin of a half-pixel) take the packed body; 4-wide boxes and records
+                // with a pair in the error band are deferred to the exact body, a full
+                // wave of them at a time
+#if ASP_FAST3
+                if (bw <= 3 && bh <= 3)
+                    amb = !small3_fast<KID, NOUT, ACC>(P, bw, bh, X0, Y0, xt, yt, acc0, acc1);
+                else
+                    amb = true;
+#else
                 if (__ballot(bw > 3 || bh > 3) == 0ull)
                     small_box<KID, NOUT, ACC, 3>(g, P, bw, bh, X0, Y0, xt, yt, acc0, acc1);
                 else
                     small_box<KID, NOUT, ACC, 4>(g, P, bw, bh, X0, Y0, xt, yt, acc0, acc1);
+#endif
+            }
+            {
+                unsigned long long am = __ballot(amb);
+                if (am) {
+                    if (amb) dlist[ndef + __popcll(am & ((1ull << lane) - 1ull))] = i;
+                    ndef += __popcll(am);
+                    if (ndef >= 64) {  // a full wave of deferred records
+                        ndef -= 64;
+                        deferred<KID, NOUT, ACC>(g, recs, it.start, dlist, ndef, 64, X0, Y0, TW, TH, kk,
+                                                 xt, yt, acc0, acc1, lane);
+                    }
+                }
             }
             unsigned long long big = __ballot(live && !small);
             while (big) {
@@ -870,6 +1044,9 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
                 sweep<KID, NOUT, ACC>(g, Q, X0, Y0, xt, yt, acc0, acc1, lane);
             }
         }
+        if (ndef > 0)
+            deferred<KID, NOUT, ACC>(g, recs, it.start, dlist, 0, ndef, X0, Y0, TW, TH, kk, xt, yt,
+                                     acc0, acc1, lane);
     }
     __syncthreads();
     if (it.slab >= 0) {  // split tile: exact partial sums, merged by K5
@@ -1164,14 +1341,40 @@ static bool make_grid(double x_min, double x_max, double y_min, double y_max, in
 constexpr int kMaxBinBlocks = 1024;  // count / scatter workgroups (hist rows)
 constexpr int kMaxTiles = 4096;  // K1/K3 LDS: 2 cursors + per-tile max (16 B/tile at 2 maps)
 
+// The particles are cut into nch chunks (contiguous runs of count workgroups).  Every
+// chunk has its own tile-sorted record region, work list and slabs, so chunk c can be
+// deposited (side stream) while chunk c + 1 is scattered: the scatter is bound by
+// scattered-store issue, the deposit by VALU / LDS, and the two overlap.
+struct Chunk {
+    long long blk0, nblk_s;  // first scatter workgroup, scatter workgroups
+    long long rec0, n_recs;  // record region
+    int n_items, n_merges, n_slabs, slab0;
+};
+
 struct Plan {
     long long n, nblk, per_block;
-    long long nblk_s;  // scatter workgroups (kScatterGroup count workgroups each)
+    long long nblk_s;  // scatter workgroups (grp count workgroups each)
+    int grp;           // count workgroups per scatter workgroup
+    long long cb;      // count workgroups per chunk (a multiple of grp)
+    int nch;           // chunks
+    Chunk ch[kMarks];
     int n_items, n_merges, n_slabs, n_wide;
     long long n_recs;
 };
 
-// K3..K7 for one kernel / map count.
+constexpr long long kChunkMinParticles = 1LL << 22;  // below: one chunk
+#ifndef ASP_CHUNKS
+#define ASP_CHUNKS 1
+#endif
+constexpr int kChunks = ASP_CHUNKS;
+
+// items / merges per chunk in the work-list buffers
+static inline size_t item_cap(const Grid& g) { return (size_t)2 * g.ntiles + kTargetItems + kTargetItems1 + 16; }
+static inline size_t merge_cap(const Grid& g) { return (size_t)g.ntiles + 16; }
+
+// K3..K7 for one kernel / map count.  Scatters run on the caller's stream st; with several
+// chunks the deposits run on the workspace's side stream, each behind its chunk's scatter
+// (one event per chunk), and st waits for the side stream at the end.
 template <int KID, int NOUT, int ACC>
 static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u,
                     const float* v, const float* h, const float* a0, const float* a1, float* o0,
@@ -1179,58 +1382,72 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     int* dc = (int*)ws.counters.p;
     const bool ratio = (flags & ASP_F_RATIO) != 0;
     const bool fuse_ratio = ratio && pl.n_wide == 0;
-    int dflags = ((flags & ASP_F_ACCUMULATE) ? kFlagAccumulate : 0) | (fuse_ratio ? kFlagRatio : 0);
-    {
-        StageMark m(ws, kSScatter, st);
-        size_t lds = (size_t)g.nstream * g.ntiles * sizeof(int) +
-                     (NOUT == 2 ? (size_t)(kScatterBlock / 64) * 128 * sizeof(float4) : 0) +
-                     (ACC == kAccFix ? (size_t)g.ntiles * NOUT * sizeof(unsigned) : 0);
-        hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC>), dim3((unsigned)pl.nblk_s), dim3(kScatterBlock),
-                           lds, st, u, v, h, a0, a1, pl.n, pl.per_block * kScatterGroup, g, (const int*)ws.hist.p,
-                           (const long long*)ws.tile_start.p, (float4*)ws.recs.p,
-                           (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc);
-        ASP_LAUNCHED();
-        m.done();
-    }
-    if (ACC == kAccFix) {
-        StageMark m(ws, kSScale, st);
-        hipLaunchKernelGGL((k_tilescale<NOUT>), dim3((g.ntiles + 63) / 64), dim3(kBlock), 0, st,
-                           (const unsigned*)ws.cmx.p, (int)pl.nblk_s, g.ntiles, g.nstream,
-                           (const int*)ws.tile_total.p, (int2*)ws.tile_k.p);
-        ASP_LAUNCHED();
-        m.done();
-    }
-    {
-        StageMark m(ws, kSDeposit, st);
-        size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4;
-        hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(pl.n_items), dim3(kDepBlock), lds, st, g,
-                           (const float4*)ws.recs.p, (const Item*)ws.items.p,
-                           (const int2*)ws.tile_k.p, (unsigned long long*)ws.slabs.p, o0, o1,
-                           dflags);
-        ASP_LAUNCHED();
-        m.done();
-    }
-    if (g.nstream == 2) {
-        StageMark m(ws, kSBand, st);
-        hipLaunchKernelGGL((k_band<KID, NOUT, ACC>), dim3(pl.n_items, 2), dim3(kBlock), 0, st, g,
-                           (const float4*)ws.recs.p, (const Item*)ws.items.p,
-                           (const int2*)ws.tile_k.p, (unsigned long long*)ws.slabs.p, o0, o1,
-                           dflags);
-        ASP_LAUNCHED();
-        m.done();
-    }
-    if (pl.n_merges > 0) {
-        StageMark m(ws, kSMerge, st);
-        hipLaunchKernelGGL((k_merge<NOUT, ACC>), dim3(pl.n_merges), dim3(kBlock), 0, st, g,
-                           (const Merge*)ws.merges.p, (const unsigned long long*)ws.slabs.p,
-                           (const int2*)ws.tile_k.p, o0, o1, dflags);
-        ASP_LAUNCHED();
-        m.done();
+    const bool piped = pl.nch > 1;
+    hipStream_t sd = piped ? ws.side : st;
+    const size_t icap = item_cap(g), mcap = merge_cap(g);
+    for (int c = 0; c < pl.nch; ++c) {
+        const Chunk& ck = pl.ch[c];
+        float4* recs = (float4*)ws.recs.p + ck.rec0 * NOUT;
+        unsigned long long* slabs = (unsigned long long*)ws.slabs.p + (long long)ck.slab0 * NOUT * kTilePix;
+        const Item* items = (const Item*)ws.items.p + c * icap;
+        const Merge* merges = (const Merge*)ws.merges.p + c * mcap;
+        int dflags = ((flags & ASP_F_ACCUMULATE) || c > 0 ? kFlagAccumulate : 0) |
+                     (fuse_ratio && c == pl.nch - 1 ? kFlagRatio : 0);
+        {
+            StageMark m(ws, kSScatter, st);
+            size_t lds = (size_t)g.nstream * g.ntiles * sizeof(int) +
+                         (NOUT == 2 ? (size_t)(kScatterBlock / 64) * 128 * sizeof(float4) : 0) +
+                         (ACC == kAccFix ? (size_t)g.ntiles * NOUT * sizeof(unsigned) : 0);
+            hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC>), dim3((unsigned)ck.nblk_s), dim3(kScatterBlock),
+                               lds, st, u, v, h, a0, a1, pl.n, pl.per_block * pl.grp, g,
+                               (const int*)ws.hist.p,
+                               (const long long*)ws.tile_start.p + (long long)c * 2 * g.ntiles, recs,
+                               (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc, (int)ck.blk0, pl.grp);
+            ASP_LAUNCHED();
+            m.done();
+        }
+        if (piped) {
+            ASP_HIP(hipEventRecord(ws.chunk_ev[c], st));
+            ASP_HIP(hipStreamWaitEvent(sd, ws.chunk_ev[c], 0));
+        }
+        if (ACC == kAccFix) {  // one chunk only (project2d)
+            StageMark m(ws, kSScale, sd);
+            hipLaunchKernelGGL((k_tilescale<NOUT>), dim3((g.ntiles + 63) / 64), dim3(kBlock), 0, sd,
+                               (const unsigned*)ws.cmx.p, (int)pl.nblk_s, g.ntiles, g.nstream,
+                               (const int*)ws.tile_total.p, (int2*)ws.tile_k.p);
+            ASP_LAUNCHED();
+            m.done();
+        }
+        {
+            StageMark m(ws, kSDeposit, sd);
+            size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4;
+            hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(ck.n_items), dim3(kDepBlock), lds, sd, g,
+                               (const float4*)recs, items, (const int2*)ws.tile_k.p, slabs, o0, o1,
+                               dflags);
+            ASP_LAUNCHED();
+            m.done();
+        }
+        if (g.nstream == 2) {  // one chunk only (project2d)
+            StageMark m(ws, kSBand, sd);
+            hipLaunchKernelGGL((k_band<KID, NOUT, ACC>), dim3(ck.n_items, 2), dim3(kBlock), 0, sd, g,
+                               (const float4*)recs, items, (const int2*)ws.tile_k.p, slabs, o0, o1,
+                               dflags);
+            ASP_LAUNCHED();
+            m.done();
+        }
+        if (ck.n_merges > 0) {
+            StageMark m(ws, kSMerge, sd);
+            hipLaunchKernelGGL((k_merge<NOUT, ACC>), dim3(ck.n_merges), dim3(kBlock), 0, sd, g,
+                               merges, (const unsigned long long*)slabs, (const int2*)ws.tile_k.p,
+                               o0, o1, dflags);
+            ASP_LAUNCHED();
+            m.done();
+        }
     }
     if (pl.n_wide > 0) {
-        StageMark m(ws, kSWide, st);
+        StageMark m(ws, kSWide, sd);
         size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4;
-        hipLaunchKernelGGL((k_wide<KID, NOUT, ACC>), dim3(g.ntiles), dim3(kDepBlock), lds, st, g, u, v, h,
+        hipLaunchKernelGGL((k_wide<KID, NOUT, ACC>), dim3(g.ntiles), dim3(kDepBlock), lds, sd, g, u, v, h,
                            a0, a1, (const int*)ws.wide.p, pl.n_wide, (const int*)dc, o0, o1);
         ASP_LAUNCHED();
         m.done();
@@ -1238,11 +1455,15 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
     if (ratio && !fuse_ratio) {
         long long npix = (long long)g.nx * g.ny;
         long long blocks = std::min<long long>((npix + kBlock - 1) / kBlock, 8192);
-        StageMark m(ws, kSRatio, st);
+        StageMark m(ws, kSRatio, sd);
         hipLaunchKernelGGL(k_ratio, dim3((unsigned)std::max<long long>(1, blocks)), dim3(kBlock),
-                           0, st, o0, (const float*)o1, npix);
+                           0, sd, o0, (const float*)o1, npix);
         ASP_LAUNCHED();
         m.done();
+    }
+    if (piped) {
+        ASP_HIP(hipEventRecord(ws.done_ev, sd));
+        ASP_HIP(hipStreamWaitEvent(st, ws.done_ev, 0));
     }
     return ASP_OK;
 }
@@ -1335,19 +1556,36 @@ static int project2d(const float* u, const float* v, const float* h, const float
         pl.nblk = std::min<long long>(max_blk, std::max<long long>(1, (n + 8191) / 8192));
         pl.per_block = (n + pl.nblk - 1) / pl.nblk;
         pl.nblk = (n + pl.per_block - 1) / pl.per_block;
-        pl.nblk_s = (pl.nblk + kScatterGroup - 1) / kScatterGroup;
-        ASP_TRY(ensure(ws.hist, (size_t)pl.nblk * g.nstream * g.ntiles * sizeof(int)));
         const bool det = (flags & ASP_F_DETERMINISTIC) != 0;
+        // chunks: the fp64 path with one record run per tile; fixed point needs one
+        // per-tile scale over all particles and the row bands one work list
+        int nch = n >= kChunkMinParticles ? kChunks : 1;
+        if (const char* e = getenv("ASP_CHUNKS")) nch = atoi(e);
+        if (det || g.nstream != 1) nch = 1;
+        nch = (int)std::max<long long>(1, std::min<long long>({(long long)nch, (long long)kMarks, pl.nblk}));
+        pl.grp = std::max(1, kScatterGroup / nch);
+        pl.cb = (pl.nblk + nch - 1) / nch;
+        pl.cb = (pl.cb + pl.grp - 1) / pl.grp * pl.grp;
+        pl.nch = (int)((pl.nblk + pl.cb - 1) / pl.cb);
+        pl.nblk_s = 0;
+        for (int c = 0; c < pl.nch; ++c) {
+            long long b0 = c * pl.cb, b1 = std::min(pl.nblk, b0 + pl.cb);
+            pl.ch[c].blk0 = b0 / pl.grp;
+            pl.ch[c].nblk_s = (b1 - b0 + pl.grp - 1) / pl.grp;
+            pl.nblk_s += pl.ch[c].nblk_s;
+        }
+        if (pl.nch > 1) ASP_TRY(ensure_side(ws));
+        ASP_TRY(ensure(ws.hist, (size_t)pl.nblk * g.nstream * g.ntiles * sizeof(int)));
         if (det) ASP_TRY(ensure(ws.cmx, (size_t)pl.nblk_s * g.ntiles * nout * sizeof(unsigned)));
-        ASP_TRY(ensure(ws.tile_total, (size_t)2 * g.ntiles * sizeof(int)));
-        ASP_TRY(ensure(ws.tile_start, (size_t)2 * g.ntiles * sizeof(long long)));
+        ASP_TRY(ensure(ws.tile_total, (size_t)pl.nch * 2 * g.ntiles * sizeof(int)));
+        ASP_TRY(ensure(ws.tile_start, (size_t)pl.nch * 2 * g.ntiles * sizeof(long long)));
         ASP_TRY(ensure(ws.tile_k, (size_t)g.ntiles * sizeof(int2)));
-        ASP_TRY(ensure(ws.items, (size_t)(2 * g.ntiles + kTargetItems + kTargetItems1 + 16) * sizeof(Item)));
-        ASP_TRY(ensure(ws.merges, (size_t)(g.ntiles + 16) * sizeof(Merge)));
-        ASP_TRY(ensure(ws.counters, cNum * sizeof(int)));
-        if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, cNum * sizeof(int)));
+        ASP_TRY(ensure(ws.items, (size_t)pl.nch * item_cap(g) * sizeof(Item)));
+        ASP_TRY(ensure(ws.merges, (size_t)pl.nch * merge_cap(g) * sizeof(Merge)));
+        ASP_TRY(ensure(ws.counters, (size_t)kMarks * cNum * sizeof(int)));
+        if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, kMarks * cNum * sizeof(int)));
         int* dc = (int*)ws.counters.p;
-        ASP_HIP(hipMemsetAsync(dc, 0, cNum * sizeof(int), st));
+        ASP_HIP(hipMemsetAsync(dc, 0, (size_t)pl.nch * cNum * sizeof(int), st));
         {
             StageMark m(ws, kSCount, st);
             hipLaunchKernelGGL(k_count, dim3((unsigned)pl.nblk), dim3(kCountBlock),
@@ -1359,29 +1597,46 @@ static int project2d(const float* u, const float* v, const float* h, const float
         }
         {
             StageMark m(ws, kSColscan, st);
-            hipLaunchKernelGGL(k_colscan, dim3((g.nstream * g.ntiles + 63) / 64), dim3(kBlock),
+            hipLaunchKernelGGL(k_colscan, dim3((g.nstream * g.ntiles + 63) / 64, pl.nch), dim3(kBlock),
                                0, st, (int*)ws.hist.p, (int)pl.nblk, g.nstream * g.ntiles,
-                               (int*)ws.tile_total.p);
+                               (int*)ws.tile_total.p, (int)pl.cb);
             ASP_LAUNCHED();
             m.done();
         }
-        {
+        for (int c = 0; c < pl.nch; ++c) {
             StageMark m(ws, kSTilescan, st);
             hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(kScanThreads), 0, st,
-                               (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles, g.nstream,
-                               (long long*)ws.tile_start.p, (Item*)ws.items.p,
-                               (Merge*)ws.merges.p, dc);
+                               (const int*)ws.tile_total.p + (long long)c * g.nstream * g.ntiles,
+                               (const int*)ws.morton.p, g.ntiles, g.nstream,
+                               (long long*)ws.tile_start.p + (long long)c * 2 * g.ntiles,
+                               (Item*)ws.items.p + c * item_cap(g),
+                               (Merge*)ws.merges.p + c * merge_cap(g), dc + c * cNum);
             ASP_LAUNCHED();
             m.done();
         }
         // One small read-back sizes the record / slab buffers.
-        ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, cNum * sizeof(int), hipMemcpyDeviceToHost, st));
+        ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, (size_t)pl.nch * cNum * sizeof(int),
+                               hipMemcpyDeviceToHost, st));
         ASP_HIP(hipStreamSynchronize(st));
-        pl.n_items = ws.h_counters[cItems];
-        pl.n_recs = ws.h_counters[cRecs];
+        pl.n_items = pl.n_slabs = pl.n_merges = 0;
+        pl.n_recs = 0;
+        for (int c = 0; c < pl.nch; ++c) {
+            const int* hc = ws.h_counters + c * cNum;
+            Chunk& ck = pl.ch[c];
+            ck.rec0 = pl.n_recs;
+            ck.n_recs = hc[cRecs];
+            ck.n_items = hc[cItems];
+            ck.n_merges = hc[cMerges];
+            ck.n_slabs = hc[cSlabs];
+            ck.slab0 = pl.n_slabs;
+            if (ck.n_recs >= 0x7fffffffLL)
+                return fail(ASP_ERR_UNSUPPORTED, "more than 2^31 particle-tile records");
+            pl.n_recs += ck.n_recs;
+            pl.n_items += ck.n_items;
+            pl.n_slabs += ck.n_slabs;
+            pl.n_merges += ck.n_merges;
+        }
         pl.n_wide = ws.h_counters[cWideCount];
-        pl.n_slabs = ws.h_counters[cSlabs];
-        pl.n_merges = ws.h_counters[cMerges];
         if (pl.n_recs >= 0x7fffffffLL)
             return fail(ASP_ERR_UNSUPPORTED, "more than 2^31 particle-tile records");
         ASP_TRY(ensure(ws.recs, (size_t)pl.n_recs * nout * sizeof(float4)));
@@ -1415,6 +1670,7 @@ static int project2d(const float* u, const float* v, const float* h, const float
     ws.stats[5] = n > 0 ? ws.h_counters[cChunk] : 0;
     ws.stats[6] = pl.n_merges;
     ws.stats[7] = pl.n_slabs;
+    ws.stats[8] = n > 0 ? pl.nch : 0;
     return ASP_OK;
 }
 
@@ -1617,12 +1873,14 @@ int asp_profile(int32_t device, int32_t enable) {
     ASP_HIP(hipSetDevice(device));
     Workspace& ws = g_ws[device];
     std::lock_guard<std::mutex> lock(ws.mu);
-    if (enable && !ws.ev[0])
-        for (int k = 0; k < 2 * kStages; ++k) ASP_HIP(hipEventCreate(&ws.ev[k]));
+    if (enable && !ws.ev[0][0][0])
+        for (int k = 0; k < kStages; ++k)
+            for (int j = 0; j < kMarks; ++j)
+                for (int e = 0; e < 2; ++e) ASP_HIP(hipEventCreate(&ws.ev[k][j][e]));
     for (int k = 0; k < kStages; ++k) {
         ws.stage_ms[k] = 0.0;
         ws.stage_n[k] = 0;
-        ws.ev_live[k] = false;
+        ws.ev_live[k] = 0;
     }
     ws.prof = enable != 0;
     return ASP_OK;
@@ -1647,7 +1905,7 @@ int asp_profile_read(int32_t device, double* ms_sum, int64_t* launches, int32_t 
 
 int asp_last_stats(int32_t device, int64_t* stats, int32_t nstats) {
     if (device < 0 || device >= 64 || !stats) return fail(ASP_ERR_INVALID, "bad argument");
-    for (int k = 0; k < nstats && k < 8; ++k) stats[k] = g_ws[device].stats[k];
+    for (int k = 0; k < nstats && k < 9; ++k) stats[k] = g_ws[device].stats[k];
     return ASP_OK;
 }
 

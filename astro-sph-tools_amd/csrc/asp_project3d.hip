@@ -475,7 +475,7 @@ static int project3d(const float* x, const float* y, const float* z, const float
         ASP_TRY(ensure(ws.items, (size_t)(g.nb + kTargetItems + 16) * sizeof(Item)));
         ASP_TRY(ensure(ws.merges, (size_t)(g.nb + 16) * sizeof(Merge)));
         ASP_TRY(ensure(ws.counters, cNum * sizeof(int)));
-        if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, cNum * sizeof(int)));
+        if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, kMarks * cNum * sizeof(int)));
         int* dc = (int*)ws.counters.p;
         ASP_HIP(hipMemsetAsync(dc, 0, cNum * sizeof(int), st));
         const size_t lds_bins = (size_t)g.nb * sizeof(int);
@@ -489,7 +489,7 @@ static int project3d(const float* x, const float* y, const float* z, const float
         {
             StageMark m(ws, kS3Colscan, st);
             hipLaunchKernelGGL(k_colscan, dim3((g.nb + 63) / 64), dim3(kBlock), 0, st,
-                               (int*)ws.hist.p, (int)nblk, g.nb, (int*)ws.tile_total.p);
+                               (int*)ws.hist.p, (int)nblk, g.nb, (int*)ws.tile_total.p, (int)nblk);
             ASP_LAUNCHED();
             m.done();
         }
@@ -550,6 +550,7 @@ static int project3d(const float* x, const float* y, const float* z, const float
     ws.stats[5] = n > 0 ? ws.h_counters[cChunk] : 0;
     ws.stats[6] = n_merges;
     ws.stats[7] = n_slabs;
+    ws.stats[8] = n > 0 ? 1 : 0;
     return ASP_OK;
 }
 

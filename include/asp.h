@@ -151,7 +151,8 @@ int asp_ratio(float *out0, const float *out1, int64_t n, int32_t device, void *s
  * Statistics of the last asp_project2d call on `device` (inspection / roofline):
  * stats[0] = records binned (particle x GPU-tile insertions), stats[1] = work items,
  * stats[2] = wide particles, stats[3] = GPU tile edge (pixels), stats[4] = GPU tiles,
- * stats[5] = records per work item, stats[6] = split tiles, stats[7] = partial slabs.
+ * stats[5] = records per work item, stats[6] = split tiles, stats[7] = partial slabs,
+ * stats[8] = particle chunks of the scatter / deposit pipeline.
  */
 int asp_last_stats(int32_t device, int64_t *stats, int32_t nstats);
 

@@ -379,3 +379,56 @@ def test_row_band_path(gpu, oracle, band_cols, monkeypatch):
     w0, w1 = oracle.project_scatter(pos[:, 0], pos[:, 1], h, AT, A, (G, G), 64, *ext)
     assert_map_close(s0, w0)
     assert_map_close(s1, w1)
+
+
+@pytest.mark.parametrize("chunks", ["2", "3", "5"])
+def test_chunked_pipeline(gpu, oracle, chunks, monkeypatch):
+    """Particles cut into chunks whose deposits overlap the next chunk's scatter (side
+    stream, maps accumulated chunk by chunk, ratio taken by the last chunk): same bars as
+    the one-chunk path -- bit-exact neighbour counts, components and ratio within
+    tolerance; wide particles and split tiles included."""
+    from asp_amd.device import stats
+    from asp_amd.tools.projections import create_image, create_weighted_image, indicator_kernel
+    monkeypatch.setenv("ASP_CHUNKS", chunks)
+    monkeypatch.setenv("ASP_WIDE_TILES", "16")
+    p = plummer_f32(300_000, seed=21, h_law="pixel", grid=1024)
+    pos, h, m, T = p["pos"], p["h"], p["m"], p["T"]
+    h[:30] = np.float32(0.9)  # wide: ~50 > 16 tiles
+    G, ext = 1024, (-4.0, 4.0, -4.0, 4.0)
+    n = h.size
+    cnt = create_image(pos, h, np.ones(n), (G, G), 64, 2, *ext, kernel_func=indicator_kernel)
+    assert stats(0)["chunks"] == int(chunks) and stats(0)["wide"] > 20
+    want, _ = oracle.project_scatter(pos[:, 0], pos[:, 1], h, np.ones(n), None, (G, G), 64,
+                                     *ext, kernel="indicator")
+    assert np.array_equal(cnt, want)
+    r, s0, s1 = create_weighted_image(pos, h, m, T, (G, G), 64, 2, *ext, return_components=True)
+    a0 = (m * T).astype(np.float32).astype(np.float64)
+    o0, o1 = oracle.project_scatter(pos[:, 0], pos[:, 1], h, a0, m, (G, G), 64, *ext)
+    assert_map_close(s0, o0)
+    assert_map_close(s1, o1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ratio_want = np.where(o1 != 0, o0 / o1, 0.0)
+    np.testing.assert_array_equal(r == 0, ratio_want == 0)
+    # the wide path's fixed point (DESIGN.md §4) holds its pixels to the component bar
+    # (2e-5 x max); a ratio of two tail-only sums ~1e-12 x max inherits their relative error
+    sig = o1 >= 1e-6 * o1.max()
+    np.testing.assert_allclose(r[sig], ratio_want[sig], rtol=2e-4, atol=0)
+    # fused ratio (no wide particles) with tiles that are empty in the last chunk
+    hs = h.copy()
+    hs[:30] = h[30:60]
+    r2 = create_weighted_image(pos, hs, m, T, (G, G), 64, 2, *ext)
+    o0, o1 = oracle.project_scatter(pos[:, 0], pos[:, 1], hs, a0, m, (G, G), 64, *ext)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ratio_want = np.where(o1 != 0, o0 / o1, 0.0)
+    np.testing.assert_array_equal(r2 == 0, ratio_want == 0)
+    np.testing.assert_allclose(r2, ratio_want, rtol=2e-4, atol=0)
+    # a clump: split tiles inside chunks
+    rng = np.random.default_rng(22)
+    cl = np.asarray(rng.normal(0, 0.01, (200_000, 3)), np.float32).astype(np.float64)
+    hc = np.full(200_000, 0.004)
+    Ac = np.asarray(rng.uniform(0.5, 1.5, 200_000), np.float32).astype(np.float64)
+    img = create_image(cl, hc, Ac, (512, 512), 64, 2, -1.0, 1.0, -1.0, 1.0)
+    assert stats(0)["merges"] > 0
+    ref, _ = oracle.project_scatter(cl[:, 0], cl[:, 1], hc, Ac, None, (512, 512), 64,
+                                    -1.0, 1.0, -1.0, 1.0)
+    assert_map_close(img, ref)

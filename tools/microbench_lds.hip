@@ -36,6 +36,13 @@ __global__ __launch_bounds__(256) void k(float* out, int span) {
         }
         else if constexpr (MODE == 6) atomicAdd((double*)&lds64[a >> 1], (double)val);  // ds_add_f64
         else if constexpr (MODE == 7) atomicMax((unsigned*)&lds[a], (unsigned)val);    // ds_max_u32
+        else if constexpr (MODE == 8) {  // ds_add_f64, lanes of each 32-lane half on distinct banks
+            int w = ((a >> 1) & ~31) | (threadIdx.x & 31);
+            atomicAdd((double*)&lds64[w & (N / 2 - 1)], (double)val);
+        } else if constexpr (MODE == 9) {  // ds_add_f64, the deposit's column-only bank mapping:
+            int w = ((a >> 1) & ~63) | ((threadIdx.x * 37 + (a >> 7)) & 63);  // random column
+            atomicAdd((double*)&lds64[w & (N / 2 - 1)], (double)val);
+        }
     }
     __syncthreads();
     float acc = 0.f;
@@ -60,14 +67,16 @@ int main() {
     int blocks = 256 * 8;
     float* d; hipMalloc(&d, blocks * 256 * sizeof(float));
     const char* names[] = {"ds_add_f32", "ds_add_u32", "ds_write_b32", "ds_add_u64", "racy_rmw",
-                           "ds_add_rtn_u32", "ds_add_f64", "ds_max_u32"};
+                           "ds_add_rtn_u32", "ds_add_f64", "ds_max_u32", "ds_add_f64 distinct",
+                           "ds_add_f64 random col"};
     for (int span : {8192, 256}) {
-        float t[8];
+        float t[10];
         t[0] = run<0>(d, blocks, span); t[1] = run<1>(d, blocks, span); t[2] = run<2>(d, blocks, span);
         t[3] = run<3>(d, blocks, span); t[4] = run<4>(d, blocks, span); t[5] = run<5>(d, blocks, span);
         t[6] = run<6>(d, blocks, span); t[7] = run<7>(d, blocks, span);
+        t[8] = run<8>(d, blocks, span); t[9] = run<9>(d, blocks, span);
         double ops = (double)blocks * 256 * ITERS;
-        for (int m = 0; m < 8; ++m)
+        for (int m = 0; m < 10; ++m)
             printf("span %5d %-24s %8.3f ms  %7.2f G lane-ops/s  %6.2f lane-ops/clk/CU@2.4GHz\n", span, names[m], t[m],
                    ops / t[m] / 1e6, ops / (t[m] * 1e-3) / 256 / 2.4e9);
     }
