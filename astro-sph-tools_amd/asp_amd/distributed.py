@@ -55,61 +55,89 @@ def _adjacent(o0, o1):
         return None
 
 
+class PendingMap:
+    """A sharded map whose collective may still be in flight (``async_op=True``).
+
+    ``wait()`` makes the caller's current stream wait for the collective (the host is not
+    blocked on RCCL), forms the ratio map where requested, and returns ``(out0, out1)``.
+    Until then the buffers must not be reused: the next projection into them has to be
+    enqueued after ``wait()`` (bench.py double-buffers the component maps so the RCCL
+    sum of map i overlaps the binning and deposit of map i + 1).
+    """
+
+    def __init__(self, outs, works, ratio_here):
+        self._outs = outs
+        self._works = works
+        self._ratio = ratio_here
+        self._done = False
+
+    def wait(self):
+        if not self._done:
+            for w in self._works:
+                w.wait()
+            if self._ratio:
+                import torch
+                o0, o1 = self._outs
+                dev = o0.device
+                _lib.check(_lib.lib().asp_ratio(_lib.ptr(o0), _lib.ptr(o1), o0.numel(),
+                                                dev.index or 0,
+                                                torch.cuda.current_stream(dev).cuda_stream))
+            self._done = True
+        return self._outs[0], (self._outs[1] if len(self._outs) > 1 else None)
+
+
 def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
                       kernel="cubic", ratio: bool = False, op: str = "reduce", dst: int = 0,
                       group=None, out0=None, out1=None, projector=None,
-                      deterministic: bool = False):
+                      deterministic: bool = False, async_op: bool = False):
     """Project this rank's particles, then combine the grids over ``group``.
 
     Returns ``(out0, out1)``: the full map(s) on ``dst`` (``op="reduce"``), on every rank
     (``"allreduce"``), or this rank's row slab (``"reduce_scatter"``; requires
     nx % world_size == 0).  With ``ratio`` the weighted map is formed after the sum.
+    ``async_op=True`` returns a :class:`PendingMap` instead, whose ``wait()`` completes the
+    collective (stream-ordered) and the ratio.
     ``projector`` replaces the local projection (tests drive the collective logic on CPU
     ranks with the oracle through it); the default is the HIP path.
     """
     import torch
     import torch.distributed as dist
+    if ratio and a1 is None:
+        raise ValueError("ratio needs a1")
+    if op not in ("reduce", "allreduce", "reduce_scatter"):
+        raise ValueError(f"unknown op {op!r}")
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    nx = int(image_size[0])
+    if op == "reduce_scatter" and world > 1 and nx % world:
+        raise ValueError("reduce_scatter needs nx divisible by the world size")
     proj = project2d if projector is None else projector
     kw = {"deterministic": True} if deterministic else {}
     o0, o1 = proj(u, v, h, a0, a1, image_size=image_size, extent=extent,
                   chunk_size=chunk_size, kernel=kernel, ratio=False, out0=out0, out1=out1, **kw)
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
     outs = [o0] if o1 is None else [o0, o1]
+    works = []
     fused = _adjacent(o0, o1)  # both maps in one buffer: one collective of 2 maps
-    if world > 1 and fused is not None and op in ("reduce", "allreduce"):
-        if op == "reduce":
-            dist.reduce(fused, dst=dst, op=dist.ReduceOp.SUM, group=group)
-        else:
-            dist.all_reduce(fused, op=dist.ReduceOp.SUM, group=group)
-    elif world > 1:
-        if op == "reduce":
-            for t in outs:
-                dist.reduce(t, dst=dst, op=dist.ReduceOp.SUM, group=group)
-        elif op == "allreduce":
-            for t in outs:
-                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-        elif op == "reduce_scatter":
-            nx = int(image_size[0])
-            if nx % world:
-                raise ValueError("reduce_scatter needs nx divisible by the world size")
+    if world > 1:
+        if op == "reduce_scatter":
             res = []
             for t in outs:
                 part = torch.empty((nx // world, t.shape[1]), dtype=t.dtype, device=t.device)
-                dist.reduce_scatter_tensor(part, t, op=dist.ReduceOp.SUM, group=group)
+                works.append(dist.reduce_scatter_tensor(part, t, op=dist.ReduceOp.SUM,
+                                                        group=group, async_op=True))
                 res.append(part)
             outs = res
         else:
-            raise ValueError(f"unknown op {op!r}")
-    if ratio:
-        if o1 is None:
-            raise ValueError("ratio needs a1")
-        if op != "reduce" or rank == dst or world == 1:
-            dev = outs[0].device
-            _lib.check(_lib.lib().asp_ratio(_lib.ptr(outs[0]), _lib.ptr(outs[1]),
-                                            outs[0].numel(), dev.index or 0,
-                                            torch.cuda.current_stream(dev).cuda_stream))
-    return outs[0], (outs[1] if len(outs) > 1 else None)
+            for t in ([fused] if fused is not None else outs):
+                if op == "reduce":
+                    works.append(dist.reduce(t, dst=dst, op=dist.ReduceOp.SUM, group=group,
+                                             async_op=True))
+                else:
+                    works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group,
+                                                 async_op=True))
+    ratio_here = ratio and (op != "reduce" or rank == dst or world == 1)
+    pending = PendingMap(outs, works, ratio_here)
+    return pending if async_op else pending.wait()
 
 
 # ---------------------------------------------------------------------------------------

@@ -1090,8 +1090,12 @@ __global__ __launch_bounds__(kBlock) void k_band(Grid g, const float4* __restric
 }
 
 // ----------------------------------------------------------------------------------
-// K5: split tiles -- exact int64 sum of the item slabs, convert, write.
+// K5: split tiles -- exact int64 sum of the item slabs, convert, write.  Grid
+// (merges, kTilePix / kBlock): each workgroup one 4-row strip of a tile, one pixel per
+// thread; the slab loop issues kMergeBatch independent loads per map before summing them
+// in slab order (deterministic), so a thread has up to 2 x kMergeBatch loads in flight.
 // ----------------------------------------------------------------------------------
+constexpr int kMergeBatch = 8;
 template <int NOUT, int ACC>
 __global__ __launch_bounds__(kBlock) void k_merge(Grid g, const Merge* __restrict__ merges,
                                                   const unsigned long long* __restrict__ slabs,
@@ -1102,19 +1106,34 @@ __global__ __launch_bounds__(kBlock) void k_merge(Grid g, const Merge* __restric
     int tx = m.tile / g.nty, ty = m.tile - (m.tile / g.nty) * g.nty;
     int X0 = tx * kTile, Y0 = ty * kTile;
     int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
+    const int k = blockIdx.y * kBlock + threadIdx.x;
+    int lx = k >> kTileShift, ly = k & (kTile - 1);
+    if (lx >= TW || ly >= TH) return;
     const int2 kk = ACC == kAccFix ? tile_k[m.tile] : make_int2(0, 0);
-    for (int k = threadIdx.x; k < kTilePix; k += kBlock) {
-        int lx = k >> kTileShift, ly = k & (kTile - 1);
-        if (lx >= TW || ly >= TH) continue;
-        unsigned long long s0 = 0, s1 = 0;  // +0.0 in fp64 as well
-        for (int j = 0; j < m.nslab; ++j) {  // fixed slab order: deterministic
-            const unsigned long long* src = slabs + (long long)(m.slab0 + j) * NOUT * kTilePix;
-            s0 = acc_sum<ACC>(s0, src[k]);
-            if (NOUT == 2) s1 = acc_sum<ACC>(s1, src[kTilePix + k]);
+    const unsigned long long* src = slabs + (long long)m.slab0 * NOUT * kTilePix + k;
+    unsigned long long s0 = 0, s1 = 0;  // +0.0 in fp64 as well
+    int j = 0;
+    for (; j + kMergeBatch <= m.nslab; j += kMergeBatch) {
+        unsigned long long b0[kMergeBatch], b1[kMergeBatch];
+#pragma unroll
+        for (int q = 0; q < kMergeBatch; ++q) {
+            const unsigned long long* p = src + (long long)(j + q) * NOUT * kTilePix;
+            b0[q] = p[0];
+            b1[q] = NOUT == 2 ? p[kTilePix] : 0ull;
         }
-        long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
-        emit_pixel<NOUT, ACC>(o, s0, s1, kk.x, kk.y, out0, out1, flags);
+#pragma unroll
+        for (int q = 0; q < kMergeBatch; ++q) {  // fixed slab order: deterministic
+            s0 = acc_sum<ACC>(s0, b0[q]);
+            if (NOUT == 2) s1 = acc_sum<ACC>(s1, b1[q]);
+        }
     }
+    for (; j < m.nslab; ++j) {
+        const unsigned long long* p = src + (long long)j * NOUT * kTilePix;
+        s0 = acc_sum<ACC>(s0, p[0]);
+        if (NOUT == 2) s1 = acc_sum<ACC>(s1, p[kTilePix]);
+    }
+    long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
+    emit_pixel<NOUT, ACC>(o, s0, s1, kk.x, kk.y, out0, out1, flags);
 }
 
 // ----------------------------------------------------------------------------------
@@ -1437,7 +1456,7 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
         }
         if (ck.n_merges > 0) {
             StageMark m(ws, kSMerge, sd);
-            hipLaunchKernelGGL((k_merge<NOUT, ACC>), dim3(ck.n_merges), dim3(kBlock), 0, sd, g,
+            hipLaunchKernelGGL((k_merge<NOUT, ACC>), dim3(ck.n_merges, kTilePix / kBlock), dim3(kBlock), 0, sd, g,
                                merges, (const unsigned long long*)slabs, (const int2*)ws.tile_k.p,
                                o0, o1, dflags);
             ASP_LAUNCHED();

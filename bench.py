@@ -8,7 +8,9 @@ SURVEY.md §8(d)).  Inputs are generated on the device and resident in HBM befor
 timed region.  With N ranks the particles are Z-slab sharded (equal counts) and one RCCL
 reduce sums the two component maps on rank 0 (strong scaling: total work fixed).
 
-One "step" = one full map: binning + deposit + (N > 1) RCCL reduce + ratio.
+One "step" = one full map: binning + deposit + (N > 1) RCCL reduce + ratio.  With N > 1
+the component maps are double-buffered so the reduce of map i runs on RCCL's stream while
+map i + 1 is binned and deposited (``--no-pipeline``: one map at a time).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       torchrun --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
@@ -53,6 +55,8 @@ def parse():
     ap.add_argument("--cube", type=int, default=512, help="cube edge (voxels), --workload cube")
     ap.add_argument("--chunks", type=int, default=None,
                     help="particle chunks of the scatter/deposit pipeline (default: library's)")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
+                    help="N > 1: wait for each map's collective before the next map")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args()
 
@@ -258,21 +262,41 @@ def main():
         log(f"[rank {rank}] data ready: {n_local} particles in {time.time() - t0:.1f}s")
 
     ratio = args.map == "weighted"
-    # both component maps in one allocation: N > 1 sums them with ONE RCCL collective
-    maps = torch.empty((2 if a1 is not None else 1, G, G), dtype=torch.float32, device=dev)
-    out0 = maps[0]
-    out1 = maps[1] if a1 is not None else None
+    # both component maps in one allocation: N > 1 sums them with ONE RCCL collective.
+    # N > 1 double-buffers them: the collective of map i (RCCL's stream) overlaps the
+    # binning + deposit of map i + 1 (compute stream); map i + 2 reuses map i's buffer
+    # only after its collective (stream-ordered wait).
+    nbuf = 2 if (world > 1 and args.pipeline) else 1
+    bufs = [torch.empty((2 if a1 is not None else 1, G, G), dtype=torch.float32, device=dev)
+            for _ in range(nbuf)]
+    pending = [None]
+    it = [0]
 
     def step():
+        maps = bufs[it[0] % nbuf]
+        it[0] += 1
+        o0, o1 = maps[0], (maps[1] if a1 is not None else None)
         if world > 1:
-            return project2d_sharded(u, v, h, a0, a1, image_size=(G, G), extent=ext,
-                                     kernel=args.kernel, ratio=ratio, op=args.op, out0=out0,
-                                     out1=out1, deterministic=args.deterministic)
-        return project2d(u, v, h, a0, a1, image_size=(G, G), extent=ext, kernel=args.kernel,
-                         ratio=ratio, out0=out0, out1=out1, deterministic=args.deterministic)
+            p = project2d_sharded(u, v, h, a0, a1, image_size=(G, G), extent=ext,
+                                  kernel=args.kernel, ratio=ratio, op=args.op, out0=o0,
+                                  out1=o1, deterministic=args.deterministic,
+                                  async_op=nbuf > 1)
+            if nbuf > 1:
+                if pending[0] is not None:
+                    pending[0].wait()  # map i - 1: stream-ordered, the host does not block
+                pending[0] = p
+            return
+        project2d(u, v, h, a0, a1, image_size=(G, G), extent=ext, kernel=args.kernel,
+                  ratio=ratio, out0=o0, out1=o1, deterministic=args.deterministic)
+
+    def drain():
+        if pending[0] is not None:
+            pending[0].wait()
+            pending[0] = None
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     _lib.profile(local, True)
     if world > 1:
@@ -281,10 +305,13 @@ def main():
     t = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t
+    last = bufs[(it[0] - 1) % nbuf]
+    out0, out1 = last[0], (last[1] if a1 is not None else None)
     prof = _lib.profile_read(local)
     _lib.profile(local, False)
     st = stats(local)
@@ -334,7 +361,8 @@ def main():
                                + (f", Z-slab x{world} + RCCL {args.op}" if world > 1 else ""),
                    "particles": args.n, "grid": G, "kernel": args.kernel, "h_law": args.h_law,
                    "map": args.map, "parallelism": f"zslab{world}" if world > 1 else "single",
-                   "accumulation": "int64 fixed point" if args.deterministic else "fp64"},
+                   "accumulation": "int64 fixed point" if args.deterministic else "fp64",
+                   "collective_overlap": nbuf > 1},
         "particles_per_s": pps,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -79,6 +79,22 @@ def _worker(rank, world, port, q):
                                        kernel="cubic", op=op, projector=_oracle_projector,
                                        out0=maps[0], out1=maps[1])
             res["fused_" + op] = (o0.numpy().copy(), o1.numpy().copy())
+        # pipelined as bench.py runs N > 1: async collectives, double-buffered maps, map
+        # i's collective completed (wait) only after map i + 1 has been projected
+        bufs = [torch.full((2, G, G), float("nan")) for _ in range(2)]
+        pend = None
+        for i in range(3):
+            b = bufs[i % 2]
+            p = project2d_sharded(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3],
+                                  image_size=(G, G), extent=EXT, chunk_size=16, kernel="cubic",
+                                  op="allreduce", projector=_oracle_projector, out0=b[0],
+                                  out1=b[1], async_op=True)
+            if pend is not None:
+                pend.wait()
+            pend = p
+        o0, o1 = pend.wait()
+        assert o0.data_ptr() == bufs[0][0].data_ptr()
+        res["pipelined"] = (o0.numpy().copy(), o1.numpy().copy(), bufs[1][0].numpy().copy())
         res["n_local"] = int(keep.sum())
         q.put((rank, res))
     finally:
@@ -114,6 +130,10 @@ def test_zslab_sharded_sum_world2():
     for r in range(world):
         np.testing.assert_allclose(out[r]["fused_allreduce"][0], full0, atol=tol, rtol=0)
         np.testing.assert_allclose(out[r]["allreduce"][0], full0, atol=tol, rtol=0)
+        np.testing.assert_allclose(out[r]["pipelined"][0], full0, atol=tol, rtol=0)
+        np.testing.assert_allclose(out[r]["pipelined"][1], full1, atol=1e-5 * np.abs(full1).max(),
+                                   rtol=0)
+        np.testing.assert_allclose(out[r]["pipelined"][2], full0, atol=tol, rtol=0)
         rows = slice(r * G // world, (r + 1) * G // world)
         np.testing.assert_allclose(out[r]["reduce_scatter"][0], full0[rows], atol=tol, rtol=0)
     # the slabs really are partial maps: neither rank alone holds the full map
