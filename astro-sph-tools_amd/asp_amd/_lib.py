@@ -31,7 +31,8 @@ ASP_ERR_UNSUPPORTED = -4
 # Every symbol include/asp.h declares (tests check the library exports all of them).
 EXPORTS = ("asp_version", "asp_last_error", "asp_device_count", "asp_project2d",
            "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges", "asp_pixel_neighbours", "asp_ratio",
-           "asp_profile", "asp_profile_read", "asp_last_stats", "asp_release")
+           "asp_profile", "asp_profile_stages", "asp_profile_read", "asp_last_stats",
+           "asp_release")
 
 STAGES = ("memset", "count", "colscan", "tilescan", "scatter", "scale", "deposit", "merge",
           "wide", "ratio", "cube_count", "cube_colscan", "cube_tilescan", "cube_scatter",
@@ -87,12 +88,13 @@ def lib():
                                        _i64, C.c_int64, _i64, _i32, C.c_int64, _i64, C.c_int32]
     L.asp_ratio.argtypes = [_f, _f, C.c_int64, C.c_int32, C.c_void_p]
     L.asp_profile.argtypes = [C.c_int32, C.c_int32]
+    L.asp_profile_stages.argtypes = [C.c_int32, C.c_uint32]
     L.asp_profile_read.argtypes = [C.c_int32, _d, _i64, C.c_int32]
     L.asp_last_stats.argtypes = [C.c_int32, _i64, C.c_int32]
     L.asp_release.argtypes = [C.c_int32]
     for name in ("asp_project2d", "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges",
-                 "asp_pixel_neighbours", "asp_ratio", "asp_profile", "asp_profile_read", "asp_last_stats",
-                 "asp_release"):
+                 "asp_pixel_neighbours", "asp_ratio", "asp_profile", "asp_profile_stages",
+                 "asp_profile_read", "asp_last_stats", "asp_release"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L
@@ -136,9 +138,16 @@ def last_stats(device: int = 0):
             "records_per_item": s[5], "merges": s[6], "slabs": s[7], "chunks": s[8]}
 
 
-def profile(device: int = 0, enable: bool = True):
-    """Start (and reset) / stop per-stage HIP-event timing inside the library."""
-    check(lib().asp_profile(device, 1 if enable else 0))
+def profile(device: int = 0, enable: bool = True, stages=None):
+    """Start (and reset) / stop per-stage HIP-event timing inside the library; ``stages``
+    (names of STAGES) limits the events to those stages."""
+    if stages is None or not enable:
+        check(lib().asp_profile(device, 1 if enable else 0))
+    else:
+        mask = 0
+        for s in stages:
+            mask |= 1 << STAGES.index(s)
+        check(lib().asp_profile_stages(device, mask))
 
 
 def profile_read(device: int = 0):

@@ -27,19 +27,24 @@ enum Ctr {
 
 // ----------------------------------------------------------------------------------
 // K2a: per tile, exclusive prefix of hist over blocks (in place); tile totals.
-// 64 tiles per workgroup (one per lane), the 4 waves split the block range.  Blocks come
+// 64 tiles per workgroup (one per lane), the kColscanWaves waves split the block range
+// (a latency-bound walk down 64 columns of hist: more waves, shorter walks).  Blocks come
 // in chunks of cb (blockIdx.y = chunk): the prefix restarts at every chunk and chunk c's
 // totals go to tile_total[c * ntiles + t] (one chunk: cb >= nblk, gridDim.y = 1).
 // ----------------------------------------------------------------------------------
-static __global__ __launch_bounds__(kBlock) void k_colscan(int* __restrict__ hist, int nblk, int ntiles,
-                                                    int* __restrict__ tile_total, int cb) {
-    __shared__ int part[4][64];
+constexpr int kColscanWaves = 16;
+constexpr int kColscanBlock = 64 * kColscanWaves;
+static __global__ __launch_bounds__(kColscanBlock) void k_colscan(int* __restrict__ hist, int nblk,
+                                                           int ntiles,
+                                                           int* __restrict__ tile_total, int cb) {
+    __shared__ int part[kColscanWaves][64];
     int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int t = blockIdx.x * 64 + lane;
     int c0 = (int)min((long long)nblk, (long long)blockIdx.y * cb);
     int cn = min(nblk - c0, cb);
     tile_total += (long long)blockIdx.y * ntiles;
-    int b0 = c0 + (int)((long long)cn * w / 4), b1 = c0 + (int)((long long)cn * (w + 1) / 4);
+    int b0 = c0 + (int)((long long)cn * w / kColscanWaves);
+    int b1 = c0 + (int)((long long)cn * (w + 1) / kColscanWaves);
     int s = 0;
     if (t < ntiles) {
         int b = b0;
@@ -66,7 +71,7 @@ static __global__ __launch_bounds__(kBlock) void k_colscan(int* __restrict__ his
     if (t < ntiles) {
         if (off)
             for (int b = b0; b < b1; ++b) hist[(long long)b * ntiles + t] += off;
-        if (w == 3) tile_total[t] = off + s;
+        if (w == kColscanWaves - 1) tile_total[t] = off + s;
     }
 }
 
@@ -103,6 +108,9 @@ static __device__ __forceinline__ void tile_items(int cs, int cl, int ch, int ch
     if (ks + kl == 0) ks = 1;  // empty tile: one zero item writes the zeros
 }
 
+constexpr int kScanPer = 16;  // max tiles per scan thread held in registers (<= 16384 tiles)
+
+template <int PER>  // tiles per thread held in registers: ntiles <= PER * kScanThreads
 static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     const int* __restrict__ tile_total, const int* __restrict__ morton, int ntiles, int nstream,
     long long* __restrict__ tile_start, Item* __restrict__ items, Merge* __restrict__ merges,
@@ -110,14 +118,24 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     __shared__ long long s_rec[kScanThreads], s_item[kScanThreads], s_slab[kScanThreads],
         s_merge[kScanThreads];
     int tid = threadIdx.x;
-    int per = (ntiles + kScanThreads - 1) / kScanThreads;
+    int per = (ntiles + kScanThreads - 1) / kScanThreads;  // <= kScanPer (host-checked)
     int r0 = min(ntiles, tid * per), r1 = min(ntiles, r0 + per);
-    auto large = [&](int t) { return nstream == 2 ? tile_total[t + ntiles] : 0; };
+    // this thread's tiles, their small- and large-record counts: all loads issued up front
+    // (two dependent rounds: morton, then the totals) and kept in registers
+    int tt[PER], cs_[PER], cl_[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) tt[q] = r0 + q < r1 ? morton[r0 + q] : 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        bool in = r0 + q < r1;
+        cs_[q] = in ? tile_total[tt[q]] : 0;
+        cl_[q] = in && nstream == 2 ? tile_total[tt[q] + ntiles] : 0;
+    }
     long long loc = 0, wloc = 0;  // all records; stream-1 records
-    for (int r = r0; r < r1; ++r) {
-        int t = morton[r];
-        loc += tile_total[t] + large(t);
-        wloc += large(t);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        loc += cs_[q] + cl_[q];
+        wloc += cl_[q];
     }
     s_rec[tid] = loc;
     s_item[tid] = wloc;
@@ -126,15 +144,17 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     block_scan_ll(s_item, tid);
     long long total = s_rec[kScanThreads - 1];
     long long total1 = s_item[kScanThreads - 1];
-    long long base = s_rec[tid] - loc;
+    const long long base0 = s_rec[tid] - loc;
+    long long base = base0;
     int ch = (int)max((long long)kMinItemRecords,
                       (total - total1 + kTargetItems - 1) / kTargetItems);
     int chl = (int)max((long long)kMinItemRecords1, (total1 + kTargetItems1 - 1) / kTargetItems1);
     __syncthreads();
     long long nit = 0, nsl = 0, nmg = 0;
-    for (int r = r0; r < r1; ++r) {
-        int t = morton[r];
-        int cs = tile_total[t], cl = large(t);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (r0 + q >= r1) continue;
+        int t = tt[q], cs = cs_[q], cl = cl_[q];
         tile_start[t] = base;
         if (nstream == 2) tile_start[t + ntiles] = base + cs;
         base += cs + cl;
@@ -154,13 +174,16 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     block_scan_ll(s_slab, tid);
     block_scan_ll(s_merge, tid);
     long long ib = s_item[tid] - nit, sb = s_slab[tid] - nsl, mb = s_merge[tid] - nmg;
-    for (int r = r0; r < r1; ++r) {
-        int t = morton[r];
-        int cs = tile_total[t], cl = large(t);
+    base = base0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (r0 + q >= r1) continue;
+        int t = tt[q], cs = cs_[q], cl = cl_[q];
         int ks, kl;
         tile_items(cs, cl, ch, chl, ks, kl);
         int k = ks + kl;
-        long long s0 = tile_start[t];
+        long long s0 = base;
+        base += cs + cl;
         for (int j = 0; j < k; ++j) {
             Item it;
             bool lg = j >= ks;

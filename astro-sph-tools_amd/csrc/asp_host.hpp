@@ -47,9 +47,14 @@ struct Workspace {
     // HIP-event profiling (asp_profile): per-stage start/stop events of the last call,
     // folded into the running sums at the next call or at asp_profile_read.
     bool prof = false;
-    hipEvent_t ev[kStages][kMarks][2] = {};
-    int ev_live[kStages] = {};  // marks recorded in the last call (a stage may launch
-                                // once per particle chunk)
+    unsigned prof_mask = 0u;  // stages timed (bit k = stage k)
+    // Two event sets, used by alternate calls: a call folds the set of the call two back,
+    // which has completed by then (the previous call's counter read-back waited for it),
+    // so profiling never makes the host wait for the GPU to drain between calls.
+    hipEvent_t ev[2][kStages][kMarks][2] = {};
+    int ev_live[2][kStages] = {};  // marks recorded per set (a stage may launch once per
+                                   // particle chunk)
+    int pset = 0;                  // the set the current call records into
     double stage_ms[kStages] = {};
     long long stage_n[kStages] = {};
     Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
@@ -63,6 +68,8 @@ struct Workspace {
     hipStream_t side = nullptr;
     hipEvent_t chunk_ev[kMarks] = {};
     hipEvent_t done_ev = nullptr;
+    hipEvent_t scan_ev = nullptr;  // 2-D pipeline: binning scans done (st)
+    hipEvent_t cnt_ev = nullptr;   // ... and their counters copied to the host (side)
 };
 
 inline int ensure_side(Workspace& ws) {
@@ -71,39 +78,53 @@ inline int ensure_side(Workspace& ws) {
     for (int c = 0; c < kMarks; ++c)
         ASP_HIP(hipEventCreateWithFlags(&ws.chunk_ev[c], hipEventDisableTiming));
     ASP_HIP(hipEventCreateWithFlags(&ws.done_ev, hipEventDisableTiming));
+    ASP_HIP(hipEventCreateWithFlags(&ws.scan_ev, hipEventDisableTiming));
+    ASP_HIP(hipEventCreateWithFlags(&ws.cnt_ev, hipEventDisableTiming));
     return ASP_OK;
 }
 
 inline Workspace g_ws[64];
 
-inline int prof_fold(Workspace& ws) {
+inline int prof_fold_set(Workspace& ws, int set) {
     for (int k = 0; k < kStages; ++k) {
-        for (int j = 0; j < ws.ev_live[k]; ++j) {
-            ASP_HIP(hipEventSynchronize(ws.ev[k][j][1]));
+        for (int j = 0; j < ws.ev_live[set][k]; ++j) {
+            ASP_HIP(hipEventSynchronize(ws.ev[set][k][j][1]));
             float ms = 0.0f;
-            ASP_HIP(hipEventElapsedTime(&ms, ws.ev[k][j][0], ws.ev[k][j][1]));
+            ASP_HIP(hipEventElapsedTime(&ms, ws.ev[set][k][j][0], ws.ev[set][k][j][1]));
             ws.stage_ms[k] += ms;
             ws.stage_n[k] += 1;
         }
-        ws.ev_live[k] = 0;
+        ws.ev_live[set][k] = 0;
     }
     return ASP_OK;
 }
 
-// Stage bracket: record start/stop events around a launch when profiling.
+// At the start of a call: switch sets, folding what the call two back recorded there.
+inline int prof_next(Workspace& ws) {
+    ws.pset ^= 1;
+    return prof_fold_set(ws, ws.pset);
+}
+
+// Everything recorded so far (asp_profile_read).
+inline int prof_fold(Workspace& ws) {
+    int rc = prof_fold_set(ws, ws.pset ^ 1);
+    return rc != ASP_OK ? rc : prof_fold_set(ws, ws.pset);
+}
+
 struct StageMark {
     Workspace& ws;
     int k;
     hipStream_t st;
     bool on;
     StageMark(Workspace& w, int stage, hipStream_t s)
-        : ws(w), k(stage), st(s), on(w.prof && w.ev_live[stage] < kMarks) {
-        if (on) (void)hipEventRecord(ws.ev[k][ws.ev_live[k]][0], st);
+        : ws(w), k(stage), st(s),
+          on(w.prof && ((w.prof_mask >> stage) & 1u) && w.ev_live[w.pset][stage] < kMarks) {
+        if (on) (void)hipEventRecord(ws.ev[ws.pset][k][ws.ev_live[ws.pset][k]][0], st);
     }
     void done() {
         if (on) {
-            (void)hipEventRecord(ws.ev[k][ws.ev_live[k]][1], st);
-            ws.ev_live[k] += 1;
+            (void)hipEventRecord(ws.ev[ws.pset][k][ws.ev_live[ws.pset][k]][1], st);
+            ws.ev_live[ws.pset][k] += 1;
         }
     }
 };

@@ -175,7 +175,11 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long per_block,
     Grid g, const int* __restrict__ hist, const long long* __restrict__ tile_start,
     float4* __restrict__ recs, unsigned* __restrict__ cmx, int* __restrict__ wide_list,
-    int* __restrict__ ctr, int blk0, int grp) {
+    int* __restrict__ ctr, int blk0, int grp, long long rec_cap, int wide_cap) {
+    // Speculative launch (enqueued before the host has read the counters): the record and
+    // wide-list buffers were sized by an earlier call; if this call needs more, every
+    // workgroup leaves at once and the host relaunches after growing them.
+    if (ctr[cRecs] > rec_cap || ctr[cWideCount] > wide_cap) return;
     // absolute record cursors, regular runs then large runs (2 * ntiles)
     extern __shared__ __attribute__((aligned(16))) int cur[];
     // per-wave staging for the paired record stores (NOUT == 2): 64 records x 32 B
@@ -1359,6 +1363,7 @@ static bool make_grid(double x_min, double x_max, double y_min, double y_max, in
 
 constexpr int kMaxBinBlocks = 1024;  // count / scatter workgroups (hist rows)
 constexpr int kMaxTiles = 4096;  // K1/K3 LDS: 2 cursors + per-tile max (16 B/tile at 2 maps)
+static_assert(kMaxTiles <= kScanThreads * 4, "k_tilescan holds <= kScanPer tiles per thread");
 
 // The particles are cut into nch chunks (contiguous runs of count workgroups).  Every
 // chunk has its own tile-sorted record region, work list and slabs, so chunk c can be
@@ -1391,13 +1396,37 @@ constexpr int kChunks = ASP_CHUNKS;
 static inline size_t item_cap(const Grid& g) { return (size_t)2 * g.ntiles + kTargetItems + kTargetItems1 + 16; }
 static inline size_t merge_cap(const Grid& g) { return (size_t)g.ntiles + 16; }
 
+// One chunk's scatter (K3) on stream st.  rec_cap / wide_cap: the capacities the kernel
+// checks against the device counters (speculative launch; see project2d).
+template <int KID, int NOUT, int ACC>
+static int launch_scatter(const Grid& g, Workspace& ws, const Plan& pl, int c, const float* u,
+                          const float* v, const float* h, const float* a0, const float* a1,
+                          long long rec_cap, int wide_cap, hipStream_t st) {
+    int* dc = (int*)ws.counters.p;
+    const Chunk& ck = pl.ch[c];
+    float4* recs = (float4*)ws.recs.p + ck.rec0 * NOUT;
+    StageMark m(ws, kSScatter, st);
+    size_t lds = (size_t)g.nstream * g.ntiles * sizeof(int) +
+                 (NOUT == 2 ? (size_t)(kScatterBlock / 64) * 128 * sizeof(float4) : 0) +
+                 (ACC == kAccFix ? (size_t)g.ntiles * NOUT * sizeof(unsigned) : 0);
+    hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC>), dim3((unsigned)ck.nblk_s), dim3(kScatterBlock),
+                       lds, st, u, v, h, a0, a1, pl.n, pl.per_block * pl.grp, g,
+                       (const int*)ws.hist.p,
+                       (const long long*)ws.tile_start.p + (long long)c * 2 * g.ntiles, recs,
+                       (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc, (int)ck.blk0, pl.grp,
+                       rec_cap, wide_cap);
+    ASP_LAUNCHED();
+    m.done();
+    return ASP_OK;
+}
+
 // K3..K7 for one kernel / map count.  Scatters run on the caller's stream st; with several
 // chunks the deposits run on the workspace's side stream, each behind its chunk's scatter
 // (one event per chunk), and st waits for the side stream at the end.
 template <int KID, int NOUT, int ACC>
 static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u,
                     const float* v, const float* h, const float* a0, const float* a1, float* o0,
-                    float* o1, int flags, hipStream_t st) {
+                    float* o1, int flags, hipStream_t st, bool pre_scattered) {
     int* dc = (int*)ws.counters.p;
     const bool ratio = (flags & ASP_F_RATIO) != 0;
     const bool fuse_ratio = ratio && pl.n_wide == 0;
@@ -1412,19 +1441,9 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
         const Merge* merges = (const Merge*)ws.merges.p + c * mcap;
         int dflags = ((flags & ASP_F_ACCUMULATE) || c > 0 ? kFlagAccumulate : 0) |
                      (fuse_ratio && c == pl.nch - 1 ? kFlagRatio : 0);
-        {
-            StageMark m(ws, kSScatter, st);
-            size_t lds = (size_t)g.nstream * g.ntiles * sizeof(int) +
-                         (NOUT == 2 ? (size_t)(kScatterBlock / 64) * 128 * sizeof(float4) : 0) +
-                         (ACC == kAccFix ? (size_t)g.ntiles * NOUT * sizeof(unsigned) : 0);
-            hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC>), dim3((unsigned)ck.nblk_s), dim3(kScatterBlock),
-                               lds, st, u, v, h, a0, a1, pl.n, pl.per_block * pl.grp, g,
-                               (const int*)ws.hist.p,
-                               (const long long*)ws.tile_start.p + (long long)c * 2 * g.ntiles, recs,
-                               (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc, (int)ck.blk0, pl.grp);
-            ASP_LAUNCHED();
-            m.done();
-        }
+        if (!(c == 0 && pre_scattered))
+            ASP_TRY((launch_scatter<KID, NOUT, ACC>(g, ws, pl, c, u, v, h, a0, a1, 0x7fffffffLL,
+                                                    0x7fffffff, st)));
         if (piped) {
             ASP_HIP(hipEventRecord(ws.chunk_ev[c], st));
             ASP_HIP(hipStreamWaitEvent(sd, ws.chunk_ev[c], 0));
@@ -1557,7 +1576,7 @@ static int project2d(const float* u, const float* v, const float* h, const float
                 ASP_HIP(hipMemcpyAsync(d1, out1, npix * sizeof(float), hipMemcpyHostToDevice, st));
         }
     }
-    if (ws.prof) ASP_TRY(prof_fold(ws));
+    if (ws.prof) ASP_TRY(prof_next(ws));
 
     Plan pl{};
     pl.n = n;
@@ -1616,7 +1635,7 @@ static int project2d(const float* u, const float* v, const float* h, const float
         }
         {
             StageMark m(ws, kSColscan, st);
-            hipLaunchKernelGGL(k_colscan, dim3((g.nstream * g.ntiles + 63) / 64, pl.nch), dim3(kBlock),
+            hipLaunchKernelGGL(k_colscan, dim3((g.nstream * g.ntiles + 63) / 64, pl.nch), dim3(kColscanBlock),
                                0, st, (int*)ws.hist.p, (int)pl.nblk, g.nstream * g.ntiles,
                                (int*)ws.tile_total.p, (int)pl.cb);
             ASP_LAUNCHED();
@@ -1624,7 +1643,7 @@ static int project2d(const float* u, const float* v, const float* h, const float
         }
         for (int c = 0; c < pl.nch; ++c) {
             StageMark m(ws, kSTilescan, st);
-            hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(kScanThreads), 0, st,
+            hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
                                (const int*)ws.tile_total.p + (long long)c * g.nstream * g.ntiles,
                                (const int*)ws.morton.p, g.ntiles, g.nstream,
                                (long long*)ws.tile_start.p + (long long)c * 2 * g.ntiles,
@@ -1633,10 +1652,33 @@ static int project2d(const float* u, const float* v, const float* h, const float
             ASP_LAUNCHED();
             m.done();
         }
-        // One small read-back sizes the record / slab buffers.
+        // One small read-back sizes the record / slab buffers.  With buffers
+        // left by an earlier call, the scatter is enqueued BEFORE the host waits for it
+        // (speculatively: it checks the counters against those capacities itself), so the
+        // GPU does not idle across the host round trip.
+        // The copy runs on the side stream, so the scatter behind it on st need not wait
+        // for the copy's own latency.
+        ASP_TRY(ensure_side(ws));
+        ASP_HIP(hipEventRecord(ws.scan_ev, st));
+        ASP_HIP(hipStreamWaitEvent(ws.side, ws.scan_ev, 0));
         ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, (size_t)pl.nch * cNum * sizeof(int),
-                               hipMemcpyDeviceToHost, st));
-        ASP_HIP(hipStreamSynchronize(st));
+                               hipMemcpyDeviceToHost, ws.side));
+        ASP_HIP(hipEventRecord(ws.cnt_ev, ws.side));
+        const long long rec_cap = (long long)std::min<size_t>(ws.recs.cap / (nout * sizeof(float4)), 0x7fffffff);
+        const int wide_cap = (int)std::min<size_t>(ws.wide.cap / sizeof(int), 0x7fffffff);
+        const bool spec = pl.nch == 1 && ws.recs.p && ws.wide.p && getenv("ASP_NO_SPECULATE") == nullptr;
+        if (spec) {
+            pl.ch[0].rec0 = 0;
+#define ASP_SC(K, N, A) \
+    launch_scatter<K, N, A>(g, ws, pl, 0, du, dv, dh, da0, da1, rec_cap, wide_cap, st)
+#define ASP_SC2(K, A) (nout == 1 ? ASP_SC(K, 1, A) : ASP_SC(K, 2, A))
+#define ASP_SC3(A) (kid == 0 ? ASP_SC2(0, A) : kid == 1 ? ASP_SC2(1, A) : ASP_SC2(2, A))
+            ASP_TRY(det ? ASP_SC3(kAccFix) : ASP_SC3(kAccF64));
+#undef ASP_SC3
+#undef ASP_SC2
+#undef ASP_SC
+        }
+        ASP_HIP(hipEventSynchronize(ws.cnt_ev));
         pl.n_items = pl.n_slabs = pl.n_merges = 0;
         pl.n_recs = 0;
         for (int c = 0; c < pl.nch; ++c) {
@@ -1658,12 +1700,14 @@ static int project2d(const float* u, const float* v, const float* h, const float
         pl.n_wide = ws.h_counters[cWideCount];
         if (pl.n_recs >= 0x7fffffffLL)
             return fail(ASP_ERR_UNSUPPORTED, "more than 2^31 particle-tile records");
+        const bool pre = spec && pl.n_recs <= rec_cap && pl.n_wide <= wide_cap;
+        if (spec && !pre) ASP_HIP(hipStreamSynchronize(st));  // its (no-op) scatter is done
         ASP_TRY(ensure(ws.recs, (size_t)pl.n_recs * nout * sizeof(float4)));
         ASP_TRY(ensure(ws.wide, (size_t)pl.n_wide * sizeof(int)));
         ASP_TRY(ensure(ws.slabs, (size_t)pl.n_slabs * nout * kTilePix * sizeof(long long)));
         int rc;
 #define ASP_TAIL(K, N, A) \
-    run_tail<K, N, A>(g, ws, pl, du, dv, dh, da0, da1, d0, d1, flags, st)
+    run_tail<K, N, A>(g, ws, pl, du, dv, dh, da0, da1, d0, d1, flags, st, pre)
 #define ASP_TAIL2(K, A) (nout == 1 ? ASP_TAIL(K, 1, A) : ASP_TAIL(K, 2, A))
 #define ASP_TAIL3(A) (kid == 0 ? ASP_TAIL2(0, A) : kid == 1 ? ASP_TAIL2(1, A) : ASP_TAIL2(2, A))
         rc = det ? ASP_TAIL3(kAccFix) : ASP_TAIL3(kAccF64);
@@ -1885,24 +1929,30 @@ int asp_ratio(float* out0, const float* out1, int64_t n, int32_t device, void* s
     return ASP_OK;
 }
 
-int asp_profile(int32_t device, int32_t enable) {
+int asp_profile_stages(int32_t device, uint32_t stage_mask) {
     t_err.clear();
     int ndev = asp_device_count();
     if (device < 0 || device >= ndev) return fail(ASP_ERR_INVALID, "bad device");
     ASP_HIP(hipSetDevice(device));
     Workspace& ws = g_ws[device];
     std::lock_guard<std::mutex> lock(ws.mu);
-    if (enable && !ws.ev[0][0][0])
-        for (int k = 0; k < kStages; ++k)
-            for (int j = 0; j < kMarks; ++j)
-                for (int e = 0; e < 2; ++e) ASP_HIP(hipEventCreate(&ws.ev[k][j][e]));
+    if (stage_mask && !ws.ev[0][0][0][0])
+        for (int q = 0; q < 2; ++q)
+            for (int k = 0; k < kStages; ++k)
+                for (int j = 0; j < kMarks; ++j)
+                    for (int e = 0; e < 2; ++e) ASP_HIP(hipEventCreate(&ws.ev[q][k][j][e]));
     for (int k = 0; k < kStages; ++k) {
         ws.stage_ms[k] = 0.0;
         ws.stage_n[k] = 0;
-        ws.ev_live[k] = 0;
+        ws.ev_live[0][k] = ws.ev_live[1][k] = 0;
     }
-    ws.prof = enable != 0;
+    ws.prof = stage_mask != 0u;
+    ws.prof_mask = stage_mask;
     return ASP_OK;
+}
+
+int asp_profile(int32_t device, int32_t enable) {
+    return asp_profile_stages(device, enable ? 0xffffffffu : 0u);
 }
 
 int asp_profile_read(int32_t device, double* ms_sum, int64_t* launches, int32_t nstages) {

@@ -39,6 +39,7 @@ constexpr int kBX = 16, kBY = 16, kBZ = 32;  // brick edge (voxels); z fastest
 constexpr int kBXs = 4, kBYs = 4, kBZs = 5;
 constexpr int kBrickVox = kBX * kBY * kBZ;   // 8192 -> 64 KiB of fp64 accumulators
 constexpr int kMaxBricks = 16384;            // C1/C3 LDS: one int per brick (64 KiB)
+static_assert(kMaxBricks <= kScanThreads * kScanPer, "k_tilescan holds <= kScanPer bricks per thread");
 constexpr int k3Block = 512;                 // count / scatter / deposit workgroup
 constexpr int kSmallVox = 32;                // boxes up to this many voxels: lane-per-record
 
@@ -455,7 +456,7 @@ static int project3d(const float* x, const float* y, const float* z, const float
         if (acc)
             ASP_HIP(hipMemcpyAsync(dout, out, nvox * sizeof(float), hipMemcpyHostToDevice, st));
     }
-    if (ws.prof) ASP_TRY(prof_fold(ws));
+    if (ws.prof) ASP_TRY(prof_next(ws));
     long long n_recs = 0;
     int n_items = 0, n_merges = 0, n_slabs = 0;
     if (n == 0) {
@@ -488,14 +489,20 @@ static int project3d(const float* x, const float* y, const float* z, const float
         }
         {
             StageMark m(ws, kS3Colscan, st);
-            hipLaunchKernelGGL(k_colscan, dim3((g.nb + 63) / 64), dim3(kBlock), 0, st,
+            hipLaunchKernelGGL(k_colscan, dim3((g.nb + 63) / 64), dim3(kColscanBlock), 0, st,
                                (int*)ws.hist.p, (int)nblk, g.nb, (int*)ws.tile_total.p, (int)nblk);
             ASP_LAUNCHED();
             m.done();
         }
         {
             StageMark m(ws, kS3Tilescan, st);
-            hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(kScanThreads), 0, st,
+            if (g.nb <= 4 * kScanThreads)
+                hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
+                               (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1,
+                               (long long*)ws.tile_start.p, (Item*)ws.items.p,
+                               (Merge*)ws.merges.p, dc);
+            else
+                hipLaunchKernelGGL(k_tilescan<kScanPer>, dim3(1), dim3(kScanThreads), 0, st,
                                (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1,
                                (long long*)ws.tile_start.p, (Item*)ws.items.p,
                                (Merge*)ws.merges.p, dc);

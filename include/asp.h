@@ -165,6 +165,10 @@ int asp_last_stats(int32_t device, int64_t *stats, int32_t nstats);
  * 14 deposit, 15 merge; 16 band (2-D row-band deposit of non-small records).
  */
 int asp_profile(int32_t device, int32_t enable);
+/* As asp_profile(device, 1), but events only around the stages whose bit is set in
+ * `stage_mask` (bit k = stage k; 0 stops).  Each event pair costs the stream a few
+ * microseconds, so a timed run marks only the kernel it reports (bench.py). */
+int asp_profile_stages(int32_t device, uint32_t stage_mask);
 int asp_profile_read(int32_t device, double *ms_sum, int64_t *launches, int32_t nstages);
 
 /* Release the cached device workspace of `device` (-1: all devices). */

@@ -432,3 +432,25 @@ def test_chunked_pipeline(gpu, oracle, chunks, monkeypatch):
     ref, _ = oracle.project_scatter(cl[:, 0], cl[:, 1], hc, Ac, None, (512, 512), 64,
                                     -1.0, 1.0, -1.0, 1.0)
     assert_map_close(img, ref)
+
+
+def test_speculative_scatter_grow_and_reuse(gpu, oracle, monkeypatch):
+    """The scatter is enqueued before the host reads the record count, against the buffers
+    an earlier call left (project2d): a call needing MORE records / wide
+    slots than those buffers hold must fall back (kernel leaves, host grows, relaunches),
+    one needing fewer must reuse them.  Same bit-exact bar either way."""
+    from asp_amd.device import stats
+    from asp_amd.tools.projections import create_image, indicator_kernel
+    monkeypatch.setenv("ASP_WIDE_TILES", "16")
+    G, ext = 512, (-4.0, 4.0, -4.0, 4.0)
+    for n, seed, wide in ((20_000, 31, 0), (400_000, 32, 0), (60_000, 33, 0), (90_000, 34, 40),
+                          (700_000, 35, 60), (30_000, 36, 0)):
+        p = plummer_f32(n, seed=seed, h_law="pixel", grid=G)
+        h = p["h"]
+        h[:wide] = np.float32(2.0)  # 2h = half the extent: > 16 of the 8 x 8 tiles -> wide
+        cnt = create_image(p["pos"], h, np.ones(n), (G, G), 64, 2, *ext,
+                           kernel_func=indicator_kernel)
+        want, _ = oracle.project_scatter(p["pos"][:, 0], p["pos"][:, 1], h, np.ones(n), None,
+                                         (G, G), 64, *ext, kernel="indicator")
+        assert np.array_equal(cnt, want), (n, seed)
+        assert stats(0)["records"] >= n // 2 and stats(0)["wide"] >= 0.9 * wide  # some miss the map

@@ -6,6 +6,6 @@ for n in 12500000 25000000 50000000 100000000; do
   timeout -k 10 200 python bench.py --cpu-baseline off --quiet --n $n --steps 20 > gpurun_out/ns/n$n.json 2> gpurun_out/ns/n$n.err || { echo "n=$n failed"; tail -5 gpurun_out/ns/n$n.err; exit 1; }
   python3 - $n <<'PY'
 import json,sys; d=json.load(open(f"gpurun_out/ns/n{sys.argv[1]}.json"))
-print(sys.argv[1], d["ms_per_step"], d["output_ok"], {k: round(v["ms_per_launch"]*v["launches"]/d["steps"],3) for k,v in d["stages"].items() if v["launches"]})
+print(sys.argv[1], d["ms_per_step"], d["output_ok"], {k: round(v["ms_per_launch"],3) for k,v in d["stages"].items()})
 PY
 done
