@@ -86,7 +86,10 @@ static __global__ __launch_bounds__(kColscanBlock) void k_colscan(int* __restric
 // independently: each stream aims at its own item count.
 // ----------------------------------------------------------------------------------
 constexpr int kScanThreads = 1024;
-constexpr int kTargetItems = 2048;
+#ifndef ASP_TARGET_ITEMS
+#define ASP_TARGET_ITEMS 2048
+#endif
+constexpr int kTargetItems = ASP_TARGET_ITEMS;  // regular items per map (split granularity)
 constexpr int kMinItemRecords = 2048;
 constexpr int kTargetItems1 = 4096;    // mode-1 items (a record there costs ~10-1000x)
 constexpr int kMinItemRecords1 = 256;

@@ -211,6 +211,27 @@ __device__ __forceinline__ float kernel_shape(float q) {
     }
 }
 
+// Error band of a record: thr = (2h)^2 in fp32 and the band around it
+// inside which the fp32 decision is not trusted (+inf: every pair goes to fp64).
+__device__ __forceinline__ void rec_band(const Grid& g, float h, float& thr, float& band) {
+    float D = 2.0f * h;
+    float Da = fabsf(D);
+    thr = D * D;
+    float eps = 0x1p-22f * (g.mg + Da);
+    band = 4.0f * Da * eps + 2.0f * eps * eps + 0x1p-20f * Da * Da;
+    // Negative h narrows the chunk cull below the disc: decide every pair in fp64.
+    if (h < 0.0f || !__builtin_isfinite(band)) band = __builtin_inff();
+}
+
+// thr -/+ band rounded: the band bounds the decision error with a >= 2x margin and its
+// 2^-20 D^2 term alone exceeds these two roundings (2^-24 thr each).
+__device__ __forceinline__ void set_band(Prep& P, float thr, float band) {
+    P.lo = thr - band;
+    P.hi = thr + band;
+    P.thr = thr;
+    P.band = band;
+}
+
 template <int KID, int ACC = kAccF64>
 __device__ __forceinline__ bool prep_record(const Grid& g, float u, float v, float h, float a0,
                                             float a1, int k0, int k1, Prep& P) {
@@ -218,19 +239,9 @@ __device__ __forceinline__ bool prep_record(const Grid& g, float u, float v, flo
     P.u = u;
     P.v = v;
     P.h = h;
-    float D = 2.0f * h;
-    float Da = fabsf(D);
-    float thr = D * D;
-    float eps = 0x1p-22f * (g.mg + Da);
-    float band = 4.0f * Da * eps + 2.0f * eps * eps + 0x1p-20f * Da * Da;
-    // Negative h narrows the chunk cull below the disc: decide every pair in fp64.
-    if (h < 0.0f || !__builtin_isfinite(band)) band = __builtin_inff();
-    // thr -/+ band rounded: the band bounds the decision error with a >= 2x margin and
-    // its 2^-20 D^2 term alone exceeds these two roundings (2^-24 thr each).
-    P.lo = thr - band;
-    P.hi = thr + band;
-    P.thr = thr;
-    P.band = band;
+    float thr, band;
+    rec_band(g, h, thr, band);
+    set_band(P, thr, band);
     P.hinv = __builtin_amdgcn_rcpf(h);  // value path only (fp32 tolerance)
     if constexpr (ACC == kAccFix) {
         P.s0 = (float)ldexp(term_coef<KID>(a0, h), k0);
@@ -279,12 +290,24 @@ __device__ __forceinline__ unsigned long long f2fix(float f) {
 }
 
 // Add one term to an LDS tile accumulator word.
+#ifndef ASP_ABLATE_ACC
+#define ASP_ABLATE_ACC 0  // diagnostic builds only (wrong maps): 1 = no LDS add, 2 = the fp64
+                          // term's bits added with ds_add_u64, 3 = fp32 term, ds_add_u32
+#endif
 template <int ACC>
 __device__ __forceinline__ void acc_add(unsigned long long* a, float t) {
+#if ASP_ABLATE_ACC == 1
+    asm volatile("" ::"v"(t), "v"(a));
+#elif ASP_ABLATE_ACC == 2
+    atomicAdd(a, (unsigned long long)__double_as_longlong((double)t));
+#elif ASP_ABLATE_ACC == 3
+    atomicAdd((unsigned*)a, __float_as_uint(t));
+#else
     if constexpr (ACC == kAccFix)
         atomicAdd(a, f2fix(t));
     else
         atomicAdd((double*)a, (double)t);
+#endif
 }
 
 // Accumulator word -> map value.

@@ -150,6 +150,15 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
     for (int t = threadIdx.x; t < g.nstream * g.ntiles; t += kCountBlock) row[t] = lh[t];
 }
 
+// A record's candidate box clipped to tile (tx, ty), tile-local, one byte per bound:
+// x0 | x1 << 8 | y0 << 16 | y1 << 24 (carried as the bits of a float).
+__device__ __forceinline__ float tile_box(const Box& b, int tx, int ty) {
+    int X0 = tx * kTile, Y0 = ty * kTile;
+    unsigned x0 = max(b.x0, X0) - X0, x1 = min(b.x1, X0 + kTile - 1) - X0;
+    unsigned y0 = max(b.y0, Y0) - Y0, y1 = min(b.y1, Y0 + kTile - 1) - Y0;
+    return __uint_as_float(x0 | (x1 << 8) | (y0 << 16) | (y1 << 24));
+}
+
 template <int NOUT, int NT>
 __device__ __forceinline__ void load_props(const float* __restrict__ a0,
                                            const float* __restrict__ a1, long long base,
@@ -165,9 +174,12 @@ __device__ __forceinline__ void load_props(const float* __restrict__ a0,
 
 // ----------------------------------------------------------------------------------
 // K3: scatter records into their tiles' runs.  Same particle partition as K1.
-// Record layout: NOUT == 1 -> float4 {u, v, h, a0};  NOUT == 2 -> 2 x float4
-// {u, v, h, a0}, {a1, 0, 0, 0}.  Also the per-(block, tile) max |c| (fp32 bits) of the
-// records it inserted, the fixed-point bound of K3b.
+// Record layout: NOUT == 1 -> float4 {u, v, h, a0};  NOUT == 2 -> the PREPARED record,
+// 2 x float4 {u, v, h, c0}, {c1, thr, band, box} (prep2_record): the deposit's per-record
+// set-up (candidate box, clip, error band, fp64 kernel normalisation) is done here, where
+// the store-bound scatter has VALU to spare, instead of in the VALU-bound deposit.  Also
+// the per-(block, tile) max |c| (fp32 bits) of the records it inserted, the fixed-point
+// bound of K3b.
 // ----------------------------------------------------------------------------------
 template <int KID, int NOUT, int ACC>
 __global__ __launch_bounds__(kScatterBlock) void k_scatter(
@@ -202,8 +214,14 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     // the scattered stores.
     float pu[kUnroll], pv[kUnroll], ph[kUnroll], pa0[kUnroll], pa1[kUnroll];
     int first_slot[kUnroll];
+    // the prepared fields of every particle's first record (the paired store's payload)
+    float first_c0[kUnroll], first_c1[kUnroll], first_thr[kUnroll], first_band[kUnroll],
+        first_box[kUnroll];
 #pragma unroll
-    for (int k = 0; k < kUnroll; ++k) first_slot[k] = -1;
+    for (int k = 0; k < kUnroll; ++k) {
+        first_slot[k] = -1;
+        first_c0[k] = first_c1[k] = first_thr[k] = first_band[k] = first_box[k] = 0.0f;
+    }
     load_batch<kScatterBlock>(u, v, h, p0, p1, pu, pv, ph);
     load_props<NOUT, kScatterBlock>(a0, a1, p0, p1, pa0, pa1);
     for (long long base = p0; base < p1; base += kStep) {
@@ -215,10 +233,14 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             long long p = base + threadIdx.x + (long long)k * kScatterBlock;
             Box b;
             if (!footprint(g, pu[k], pv[k], ph[k], b)) continue;
+            // NOUT == 2: the prepared record's fields (prep2_record); the fixed-point
+            // bound is taken over the same fp32 coefficients the deposit scales
+            float cf0 = NOUT == 2 ? (float)term_coef<KID>(pa0[k], ph[k]) : 0.0f;
+            float cf1 = NOUT == 2 ? (float)term_coef<KID>(pa1[k], ph[k]) : 0.0f;
             unsigned c0 = 0u, c1 = 0u;
             if constexpr (ACC == kAccFix) {
-                c0 = __float_as_uint(fabsf((float)term_coef<KID>(pa0[k], ph[k])));
-                if (NOUT == 2) c1 = __float_as_uint(fabsf((float)term_coef<KID>(pa1[k], ph[k])));
+                c0 = __float_as_uint(fabsf(NOUT == 2 ? cf0 : (float)term_coef<KID>(pa0[k], ph[k])));
+                if (NOUT == 2) c1 = __float_as_uint(fabsf(cf1));
             }
             int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
             int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
@@ -230,8 +252,15 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                 }
                 continue;
             }
-            float4 r0 = make_float4(pu[k], pv[k], ph[k], pa0[k]);
-            float4 r1 = make_float4(pa1[k], 0.0f, 0.0f, 0.0f);
+            float thr = 0.0f, band = 0.0f;
+            if constexpr (NOUT == 2) rec_band(g, ph[k], thr, band);
+            float4 r0 = make_float4(pu[k], pv[k], ph[k], NOUT == 2 ? cf0 : pa0[k]);
+            if constexpr (NOUT == 2) {
+                first_c0[k] = cf0;
+                first_c1[k] = cf1;
+                first_thr[k] = thr;
+                first_band[k] = band;
+            }
             bool mb = g.nstream == 2 && b.y1 - b.y0 + 1 >= g.band_cols;
             for (int tx = tx0; tx <= tx1; ++tx)
                 for (int ty = ty0; ty <= ty1; ++ty) {
@@ -245,11 +274,13 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                     slot = (int)p;  // diagnostic: coalesced destinations, same bytes
 #endif
                     if constexpr (NOUT == 2) {
+                        float bp = tile_box(b, tx, ty);
                         if (tx == tx0 && ty == ty0) {
                             first_slot[k] = slot;  // written by the paired store below
+                            first_box[k] = bp;
                         } else {
                             put_rec(&recs[2 * (long long)slot], r0);
-                            put_rec(&recs[2 * (long long)slot + 1], r1);
+                            put_rec(&recs[2 * (long long)slot + 1], make_float4(cf1, thr, band, bp));
                         }
                     } else {
                         put_rec(&recs[slot], r0);
@@ -264,8 +295,8 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             int lane = threadIdx.x & 63;
 #pragma unroll
             for (int k = 0; k < kUnroll; ++k) {
-                st[2 * lane] = make_float4(pu[k], pv[k], ph[k], pa0[k]);
-                st[2 * lane + 1] = make_float4(pa1[k], 0.0f, 0.0f, 0.0f);
+                st[2 * lane] = make_float4(pu[k], pv[k], ph[k], first_c0[k]);
+                st[2 * lane + 1] = make_float4(first_c1[k], first_thr[k], first_band[k], first_box[k]);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -424,16 +455,35 @@ __device__ __forceinline__ bool clip(Box& b, int X0, int Y0, int TW, int TH) {
     return b.x0 <= b.x1 && b.y0 <= b.y1;
 }
 
-template <int NOUT>
-__device__ __forceinline__ void load_rec(const float4* recs, long long i, float& u, float& v,
-                                         float& h, float& a0, float& a1) {
+// A record -> the pair loop's state, clipped to the tile (X0, Y0, TW, TH).  NOUT == 1:
+// raw {u, v, h, a0}, prepared here.  NOUT == 2: the scatter's prepared record
+// {u, v, h, c0}, {c1, thr, band, box}; only 1/h and the tile's fixed-point scale remain
+// (ldexp of the fp32 coefficient: exact, the scale is a power of two).  False: no pair.
+template <int KID, int NOUT, int ACC>
+__device__ __forceinline__ bool rec_prep(const Grid& g, const float4& r0, const float4& r1,
+                                         int X0, int Y0, int TW, int TH, int2 kk, Prep& P) {
     if constexpr (NOUT == 1) {
-        float4 r = recs[i];
-        u = r.x; v = r.y; h = r.z; a0 = r.w; a1 = 0.0f;
+        return prep_record<KID, ACC>(g, r0.x, r0.y, r0.z, r0.w, 0.0f, kk.x, kk.y, P) &&
+               clip(P.b, X0, Y0, TW, TH);
     } else {
-        float4 r = recs[2 * i];
-        float4 s = recs[2 * i + 1];
-        u = r.x; v = r.y; h = r.z; a0 = r.w; a1 = s.x;
+        P.u = r0.x;
+        P.v = r0.y;
+        P.h = r0.z;
+        set_band(P, r1.y, r1.z);
+        P.hinv = __builtin_amdgcn_rcpf(r0.z);
+        if constexpr (ACC == kAccFix) {
+            P.s0 = ldexpf(r0.w, kk.x);
+            P.s1 = ldexpf(r1.x, kk.y);
+        } else {
+            P.s0 = r0.w;
+            P.s1 = r1.x;
+        }
+        unsigned bp = __float_as_uint(r1.w);
+        P.b.x0 = X0 + (int)(bp & 255u);
+        P.b.x1 = X0 + (int)((bp >> 8) & 255u);
+        P.b.y0 = Y0 + (int)((bp >> 16) & 255u);
+        P.b.y1 = Y0 + (int)(bp >> 24);
+        return true;
     }
 }
 
@@ -687,8 +737,8 @@ __device__ __forceinline__ void band_item(const Grid& g, const float4* __restric
         if (base + 64 + lane < it.count) load_rec4<NOUT>(recs, it.start + base + 64 + lane, n0, n1);
         Prep P;
         bool hit = base + lane < it.count &&
-                   prep_record<KID, ACC>(g, r0.x, r0.y, r0.z, r0.w, r1.x, kk.x, kk.y, P) &&
-                   clip(P.b, X0, Y0, TW, TH) && P.b.x0 - X0 <= rb0 + 7 && P.b.x1 - X0 >= rb0;
+                   rec_prep<KID, NOUT, ACC>(g, r0, r1, X0, Y0, TW, TH, kk, P) &&
+                   P.b.x0 - X0 <= rb0 + 7 && P.b.x1 - X0 >= rb0;
         r0 = n0;
         r1 = n1;
         unsigned long long m = __ballot(hit);
@@ -897,6 +947,12 @@ __device__ __forceinline__ bool small3_fast(const Prep& P, int bw, int bh, int X
 #define ASP_FAST3 1  // 0: diagnostic builds only, the unpacked 3 x 3 body with in-loop band pairs
 #endif
 
+#ifndef ASP_DEP_THREADS
+#define ASP_DEP_THREADS 512
+#endif
+// k_deposit workgroup: two per CU (64 KiB fp64 LDS tile each)
+constexpr int kDepThreads = ASP_DEP_THREADS;
+
 // Per-wave list of records deferred to the exact path (a pair in the error band).
 constexpr int kDeferCap = 128;
 
@@ -918,8 +974,7 @@ __device__ __forceinline__ void deferred(const Grid& g, const float4* __restrict
     float4 r0, r1 = make_float4(0.f, 0.f, 0.f, 0.f);
     load_rec4<NOUT>(recs, start + idx, r0, r1);
     Prep P;
-    if (!prep_record<KID, ACC>(g, r0.x, r0.y, r0.z, r0.w, r1.x, kk.x, kk.y, P)) return;
-    if (!clip(P.b, X0, Y0, TW, TH)) return;
+    if (!rec_prep<KID, NOUT, ACC>(g, r0, r1, X0, Y0, TW, TH, kk, P)) return;
     small_box<KID, NOUT, ACC, 4>(g, P, P.b.x1 - P.b.x0 + 1, P.b.y1 - P.b.y0 + 1, X0, Y0, xt, yt,
                                  acc0, acc1);
 }
@@ -929,7 +984,7 @@ __device__ __forceinline__ void deferred(const Grid& g, const float4* __restrict
 // tile (single-item tiles) or its int64 partial slab (split tiles).
 // ----------------------------------------------------------------------------------
 template <int KID, int NOUT, int ACC>
-__global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_deposit(
+__global__ __launch_bounds__(kDepThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_deposit(
     Grid g, const float4* __restrict__ recs, const Item* __restrict__ items,
     const int2* __restrict__ tile_k, unsigned long long* __restrict__ slabs,
     float* __restrict__ out0, float* __restrict__ out1, int flags) {
@@ -949,7 +1004,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
             // raw sums here, the ratio is still to be taken
             if constexpr (NOUT == 2) {
                 if (flags & kFlagRatio) {
-                    for (int k = threadIdx.x; k < kTilePix; k += kDepBlock) {
+                    for (int k = threadIdx.x; k < kTilePix; k += kDepThreads) {
                         int lx = k >> kTileShift, ly = k & (kTile - 1);
                         if (lx >= TW || ly >= TH) continue;
                         long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
@@ -960,7 +1015,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
             }
             return;
         }
-        for (int k = threadIdx.x; k < kTilePix; k += kDepBlock) {
+        for (int k = threadIdx.x; k < kTilePix; k += kDepThreads) {
             int lx = k >> kTileShift, ly = k & (kTile - 1);
             if (lx >= TW || ly >= TH) continue;
             long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
@@ -970,9 +1025,9 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
         return;
     }
     const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
-    tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
+    tile_prologue<NOUT, kDepThreads>(g, X0, Y0, acc, xt, yt);
     {
-        __shared__ int defer_lds[kDepBlock / 64][kDeferCap];
+        __shared__ int defer_lds[kDepThreads / 64][kDeferCap];
         int lane = threadIdx.x & 63;
         int* dlist = defer_lds[threadIdx.x >> 6];
         int ndef = 0;  // wave-uniform
@@ -980,13 +1035,13 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
         // (16 waves/CU x 64 lanes x 32 B x 2 in flight per CU).
         float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, q0 = r0, q1 = r0;
         if ((int)threadIdx.x < it.count) load_rec4<NOUT>(recs, it.start + threadIdx.x, r0, r1);
-        if ((int)threadIdx.x + kDepBlock < it.count)
-            load_rec4<NOUT>(recs, it.start + threadIdx.x + kDepBlock, q0, q1);
-        for (int base = 0; base < it.count; base += kDepBlock) {
+        if ((int)threadIdx.x + kDepThreads < it.count)
+            load_rec4<NOUT>(recs, it.start + threadIdx.x + kDepThreads, q0, q1);
+        for (int base = 0; base < it.count; base += kDepThreads) {
             int i = base + threadIdx.x;
             float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0;
-            if (i + 2 * kDepBlock < it.count)
-                load_rec4<NOUT>(recs, it.start + i + 2 * kDepBlock, n0, n1);
+            if (i + 2 * kDepThreads < it.count)
+                load_rec4<NOUT>(recs, it.start + i + 2 * kDepThreads, n0, n1);
             Prep P;
             P.b = Box{0, -1, 0, -1};
             bool live = false;
@@ -996,8 +1051,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
             continue;
     #endif
             if (i < it.count)
-                live = prep_record<KID, ACC>(g, r0.x, r0.y, r0.z, r0.w, r1.x, kk.x, kk.y, P) &&
-                       clip(P.b, X0, Y0, TW, TH);
+                live = rec_prep<KID, NOUT, ACC>(g, r0, r1, X0, Y0, TW, TH, kk, P);
             r0 = q0;
             r1 = q1;
             q0 = n0;
@@ -1055,10 +1109,10 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
     __syncthreads();
     if (it.slab >= 0) {  // split tile: exact partial sums, merged by K5
         unsigned long long* dst = slabs + (long long)it.slab * NOUT * kTilePix;
-        for (int k = threadIdx.x; k < NOUT * kTilePix; k += kDepBlock) dst[k] = acc[k];
+        for (int k = threadIdx.x; k < NOUT * kTilePix; k += kDepThreads) dst[k] = acc[k];
         return;
     }
-    for (int k = threadIdx.x; k < kTilePix; k += kDepBlock) {
+    for (int k = threadIdx.x; k < kTilePix; k += kDepThreads) {
         int lx = k >> kTileShift, ly = k & (kTile - 1);
         if (lx >= TW || ly >= TH) continue;
         long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly);
@@ -1459,7 +1513,7 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
         {
             StageMark m(ws, kSDeposit, sd);
             size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4;
-            hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(ck.n_items), dim3(kDepBlock), lds, sd, g,
+            hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(ck.n_items), dim3(kDepThreads), lds, sd, g,
                                (const float4*)recs, items, (const int2*)ws.tile_k.p, slabs, o0, o1,
                                dflags);
             ASP_LAUNCHED();
