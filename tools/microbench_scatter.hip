@@ -25,6 +25,7 @@ constexpr int T = 1024;
 template <int MODE>
 __global__ __launch_bounds__(T) void k(float4* __restrict__ recs, float* __restrict__ plane1,
                                        int K, int kshift, long long R, int B) {
+    const long long cap = (100000000LL + (1LL << 24)) * 2;  // float4 slots allocated
     const int lane = threadIdx.x & 63;
     const long long nb = R * K;  // records per workgroup
     const int b = blockIdx.x;
@@ -62,15 +63,17 @@ __global__ __launch_bounds__(T) void k(float4* __restrict__ recs, float* __restr
             int bb = MODE == 7 ? b >> 3 : b;
             long long RLn = (nj / 8) / KT + 1;  // lines per (workgroup, tile)
             long long ln = (long long)tile * ((long long)nbk * RLn + 3) + (long long)bb * RLn + cl % RLn;
-            recs[ln * 8 + (lane & 7)] = make_float4((float)j, 1.f, 2.f, 3.f);
+            if (ln * 8 + 8 <= cap) recs[ln * 8 + (lane & 7)] = make_float4((float)j, 1.f, 2.f, 3.f);
             continue;
         }
         float4 v0 = make_float4((float)j, (float)t, 1.f, 2.f);
         if constexpr (MODE == 2) {
             asm volatile("" ::"v"(v0.x), "v"((int)slot));
         } else if constexpr (MODE == 4) {
-            recs[slot] = v0;
-            plane1[slot] = 3.f;
+            if (slot < cap / 2) {
+                recs[slot] = v0;
+                plane1[slot] = 3.f;
+            }
         } else {
             // paired store: lanes 2i, 2i+1 write the halves of record i (32 lines / instr)
 #pragma unroll
@@ -79,7 +82,7 @@ __global__ __launch_bounds__(T) void k(float4* __restrict__ recs, float* __restr
                 long long s = __shfl(slot, src);
                 float4 val = (lane & 1) ? make_float4(3.f, 0.f, 0.f, 0.f)
                                         : make_float4(__shfl(v0.x, src), __shfl(v0.y, src), 1.f, 2.f);
-                recs[2 * s + (lane & 1)] = val;
+                if (2 * s + 2 <= cap) recs[2 * s + (lane & 1)] = val;
             }
         }
     }
