@@ -22,6 +22,13 @@ ASP_F_RATIO = 0x2
 ASP_F_ACCUMULATE = 0x4
 ASP_F_DETERMINISTIC = 0x8
 
+ASP_PB_WRAP = 0x1
+ASP_PB_SHIFT_ORIGIN = 0x2
+ASP_PB_SHIFT_CENTRE = 0x4
+ASP_PB_ORIGIN_IS_CENTRE = 0x8
+ASP_PB_IMAGES = 0x10
+ASP_PB_DISPLACEMENT = 0x20
+
 ASP_OK = 0
 ASP_ERR_INVALID = -1
 ASP_ERR_HIP = -2
@@ -32,7 +39,7 @@ ASP_ERR_UNSUPPORTED = -4
 EXPORTS = ("asp_version", "asp_last_error", "asp_device_count", "asp_project2d",
            "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges", "asp_pixel_neighbours", "asp_ratio",
            "asp_profile", "asp_profile_stages", "asp_profile_read", "asp_last_stats",
-           "asp_release")
+           "asp_release", "asp_stage_particles", "asp_periodic", "asp_wrapped_distance")
 
 STAGES = ("memset", "count", "colscan", "tilescan", "scatter", "scale", "deposit", "merge",
           "wide", "ratio", "cube_count", "cube_colscan", "cube_tilescan", "cube_scatter",
@@ -92,9 +99,17 @@ def lib():
     L.asp_profile_read.argtypes = [C.c_int32, _d, _i64, C.c_int32]
     L.asp_last_stats.argtypes = [C.c_int32, _i64, C.c_int32]
     L.asp_release.argtypes = [C.c_int32]
+    L.asp_stage_particles.argtypes = [_d, _d, _d, _d, C.c_int64, C.c_int32, _d, C.c_double,
+                                      C.c_int32, _f, _f, _f, _f, _f, C.c_int64, _i64, C.c_int32,
+                                      C.c_int32, C.c_void_p]
+    L.asp_periodic.argtypes = [C.c_int32, _d, C.c_int64, _d, C.c_int64, C.c_int64, C.c_double,
+                               C.c_int32, _d, C.c_int32, C.c_void_p]
+    L.asp_wrapped_distance.argtypes = [_d, C.c_int64, _d, C.c_int64, C.c_int64, C.c_double,
+                                       C.c_int32, _d, C.c_int32, C.c_void_p]
     for name in ("asp_project2d", "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges",
                  "asp_pixel_neighbours", "asp_ratio", "asp_profile", "asp_profile_stages",
-                 "asp_profile_read", "asp_last_stats", "asp_release"):
+                 "asp_profile_read", "asp_last_stats", "asp_release", "asp_stage_particles",
+                 "asp_periodic", "asp_wrapped_distance"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

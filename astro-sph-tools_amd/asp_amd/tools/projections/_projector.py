@@ -117,3 +117,40 @@ def create_weighted_image(positions, smoothing_lengths, weights, values, image_s
     r, _ = _run(u, v, h, wv, w, image_size, cs, (x_min, x_max, y_min, y_max), kid,
                 _lib.ASP_F_RATIO | det, device)
     return r.astype(dtype, copy=False)
+
+
+def create_periodic_image(positions, smoothing_lengths, particle_properties, image_size,
+                          chunk_size, projection_axis, box_width, centre=None,
+                          kernel_func=quartic_spline_kernel, *, origin_is_centre: bool = False,
+                          device: int = 0, dtype=np.float64, deterministic: bool = False):
+    """Map of a whole periodic box, footprints wrapping across its faces (SURVEY.md §8(f)
+    rank 2: the reference ships the box helpers, tools/_periodic_box_manipulations.py, but
+    its projector ignores periodicity).
+
+    Positions are moved with the reference's ``shift_centre(positions, centre, box_width,
+    origin_is_centre)`` when ``centre`` is given, else wrapped with ``calculate_periodic``
+    (fp64, on the device).  The image spans the box ``[lo, lo + L)`` on both projected axes
+    (``lo = 0``, or ``-L/2`` with ``origin_is_centre``) and each pixel is ``create_image``'s
+    sum over every periodic image of every particle (the staged copies of
+    ``asp_stage_particles``; same neighbour decisions, same kernels).
+    """
+    import torch
+
+    from ...device import project2d
+    from ...stage import stage_particles
+    cs = _check_chunk_size(chunk_size)
+    kid = kernel_id_of(kernel_func)
+    L = float(box_width)
+    nx, ny = int(image_size[0]), int(image_size[1])
+    if nx <= 0 or ny <= 0 or cs < 0:
+        return np.zeros((max(nx, 0), max(ny, 0)), dtype=dtype)
+    u, v, h, props = stage_particles(positions, smoothing_lengths, particle_properties,
+                                     projection_axis=projection_axis, box_width=L,
+                                     centre=centre, shift="wrap" if centre is None else "centre",
+                                     origin_is_centre=origin_is_centre, images=True,
+                                     device=device)
+    lo = -(L / 2) if origin_is_centre else 0.0
+    out, _ = project2d(u, v, h, props[0], image_size=(nx, ny), extent=(lo, lo + L, lo, lo + L),
+                       chunk_size=cs, kernel=kid, deterministic=deterministic)
+    torch.cuda.synchronize(u.device)
+    return out.cpu().numpy().astype(dtype, copy=False)

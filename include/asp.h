@@ -147,6 +147,62 @@ int asp_pixel_neighbours(const float *u, const float *v, const float *h, int64_t
  */
 int asp_ratio(float *out0, const float *out1, int64_t n, int32_t device, void *stream);
 
+/* Periodic-box operations: pb_flags of asp_stage_particles, op of asp_periodic. */
+#define ASP_PB_WRAP 0x1             /* make_periodic (_periodic_box_manipulations.py:36-48) */
+#define ASP_PB_SHIFT_ORIGIN 0x2     /* shift_origin (:54-57): x - origin, then wrapped       */
+#define ASP_PB_SHIFT_CENTRE 0x4     /* shift_centre (:63-69): x + (L/2 - centre), wrapped    */
+#define ASP_PB_ORIGIN_IS_CENTRE 0x8 /* the box is [-L/2, L/2) instead of [0, L)              */
+#define ASP_PB_IMAGES 0x10          /* asp_stage_particles: append periodic images           */
+#define ASP_PB_DISPLACEMENT 0x20    /* asp_periodic: calculate_wrapped_displacement (:10-20) */
+
+/*
+ * Snapshot -> projector staging.  Replaces the host-side step of
+ * create_image that takes the reader's arrays (io/data_structures/_SnapshotBase.py:599-725:
+ * positions (n, 3) float64 row-major, smoothing lengths and properties float64) to the
+ * float32 structure of arrays asp_project2d consumes, with the axis selection of
+ * _projector.py:38-46 (axis 0 = X -> (y, z), 1 = Y -> (x, z), 2 = Z -> (x, y)); the
+ * conversion (round to nearest, as NumPy's astype(float32)) runs on the device.
+ *   u, v, hf, a0f, a1f: DEVICE float32 outputs on `device` of capacity cap (hf, a0f, a1f
+ *   may be NULL, as may their inputs h, a0, a1).  Inputs are host pointers, copied in
+ *   chunks with copy and conversion overlapped, unless ASP_F_DEVICE_PTRS.
+ * Periodic box, pb_flags: at most one of ASP_PB_WRAP,
+ *   ASP_PB_SHIFT_ORIGIN, ASP_PB_SHIFT_CENTRE (centre = the new origin / centre, 3 values;
+ *   the reference helpers' fp64 arithmetic on the two projected coordinates), optionally
+ *   ASP_PB_ORIGIN_IS_CENTRE, and ASP_PB_IMAGES: every particle inside the box
+ *   [lo, lo + L)^2 (lo = 0, or -L/2) whose reach 2|h| (+ a 2^-20 margin) crosses a face
+ *   gets a copy one box width over (up to 3 per particle), appended after the n
+ *   originals in an unspecified order -- projecting the result over the box gives the
+ *   periodic map.  *n_out = n + images; if that exceeds cap the images beyond cap are
+ *   dropped and the call returns ASP_ERR_INVALID with *n_out set to the size needed.
+ */
+int asp_stage_particles(const double *positions, const double *h, const double *a0,
+                        const double *a1, int64_t n, int32_t axis, const double *centre,
+                        double box_width, int32_t pb_flags, float *u, float *v, float *hf,
+                        float *a0f, float *a1f, int64_t cap, int64_t *n_out, int32_t flags,
+                        int32_t device, void *stream);
+
+/*
+ * The periodic-box helpers of tools/_periodic_box_manipulations.py on the device, fp64,
+ * bit-identical to the reference: op = ASP_PB_WRAP (make_periodic / calculate_periodic,
+ * :36-48), ASP_PB_SHIFT_ORIGIN (shift_origin :54-57, b = new origin), ASP_PB_SHIFT_CENTRE
+ * (shift_centre :63-69, b = new centre), ASP_PB_DISPLACEMENT
+ * (calculate_wrapped_displacement :10-20, a = from, b = to).  out[i] for i < n; a and b
+ * repeat with periods pa and pb (NumPy broadcasting of a (3,) vector over (N, 3)).
+ * Device pointers, ordered on `stream`.
+ */
+int asp_periodic(int32_t op, const double *a, int64_t pa, const double *b, int64_t pb,
+                 int64_t n, double box_width, int32_t origin_is_centre, double *out,
+                 int32_t device, void *stream);
+
+/*
+ * calculate_wrapped_distance (_periodic_box_manipulations.py:22-34): per row of 3, the
+ * length (squared != 0: its square) of the wrapped displacement; from / to repeat with
+ * periods pf / pt (elements).  Device pointers, ordered on `stream`.
+ */
+int asp_wrapped_distance(const double *from, int64_t pf, const double *to, int64_t pt,
+                         int64_t rows, double box_width, int32_t squared, double *out,
+                         int32_t device, void *stream);
+
 /*
  * Statistics of the last asp_project2d call on `device` (inspection / roofline):
  * stats[0] = records binned (particle x GPU-tile insertions), stats[1] = work items,

@@ -196,3 +196,78 @@ def voxel_neighbours(x, y, z, h, cube_size, extent, voxels):
         if t >= 0:
             return offs, idx[:t]
         cap = -t
+
+
+# ---------------------------------------------------------------------------------------
+# Periodic box: NumPy restatement of the reference's helpers,
+# tools/_periodic_box_manipulations.py:10-72 (pinned by tests/golden/g8_periodic.npz, made
+# by running the reference's own function bodies), and of the periodic images the staging
+# pass appends (asp_stage_particles; build-defined, include/asp.h).
+# ---------------------------------------------------------------------------------------
+def pb_wrap(x, L, centred=False):
+    """make_periodic (:36-43): one wrap by L of the coordinates outside the box."""
+    x = np.array(x, dtype=np.float64)
+    lo = -(L / 2) if centred else 0.0
+    out = (x < lo) | (x >= lo + L)
+    s = np.sign(x + (L / 2) if centred else x)
+    return np.where(out, -s * L + x, x)
+
+
+def pb_shift(x, c, L, kind, centred=False):
+    """shift_origin (:54-57) / shift_centre (:63-69)."""
+    x = np.asarray(x, dtype=np.float64)
+    if kind == "origin" or centred:
+        return pb_wrap(x - c, L, centred)
+    return pb_wrap(x + ((L / 2) - c), L, False)
+
+
+def pb_displacement(frm, to, L):
+    """calculate_wrapped_displacement (:10-20)."""
+    d = np.asarray(to, np.float64) - np.asarray(frm, np.float64)
+    return np.where(np.abs(d) > L / 2, d - np.sign(d) * L, d)
+
+
+def pb_distance(frm, to, L, squared=False):
+    """calculate_wrapped_distance (:22-34)."""
+    d = pb_displacement(frm, to, L)
+    s = (d ** 2).sum(axis=1 if d.ndim > 1 else 0)
+    return s if squared else np.sqrt(s)
+
+
+def stage_particles(positions, h, props, axis, L=None, centre=None, shift=None,
+                    centred=False, images=False):
+    """What asp_stage_particles produces: (u, v, h, props) float32, the originals in input
+    order followed by the periodic images (the device appends those in an unspecified
+    order; compare them as a set)."""
+    pos = np.asarray(positions, np.float64).reshape(-1, 3)
+    a, b = AXIS_COLS[int(getattr(axis, "value", axis))]
+    x, y = pos[:, a], pos[:, b]
+    if shift == "wrap":
+        x, y = pb_wrap(x, L, centred), pb_wrap(y, L, centred)
+    elif shift in ("origin", "centre"):
+        c = np.asarray(centre, np.float64)
+        x, y = pb_shift(x, c[a], L, shift, centred), pb_shift(y, c[b], L, shift, centred)
+    hh = None if h is None else np.asarray(h, np.float64)
+    pp = [np.asarray(p, np.float64) for p in props]
+    cols = [x, y] + ([hh] if hh is not None else []) + pp
+    out = [c.astype(np.float32) for c in cols]
+    if not images:
+        return out
+    lo = -(L / 2) if centred else 0.0
+    R = 2.0 * np.abs(hh) * (1.0 + 2.0 ** -20) + 2.0 ** -20 * L
+    ok = (R > 0) & (R < L)
+
+    def direction(w):
+        inside = (w >= lo) & (w < lo + L) & ok
+        d = np.where(inside & (w - lo < R), 1, 0)
+        return np.where(inside & (d == 0) & ((lo + L) - w <= R), -1, d)
+
+    dx, dy = direction(x), direction(y)
+    extra = [[] for _ in cols]
+    for sx, sy, sel in ((dx, 0, dx != 0), (0, dy, dy != 0), (dx, dy, (dx != 0) & (dy != 0))):
+        sx = np.broadcast_to(sx, x.shape)[sel]
+        sy = np.broadcast_to(sy, y.shape)[sel]
+        shifted = [x[sel] + sx * L, y[sel] + sy * L] + [c[sel] for c in cols[2:]]
+        for k, c in enumerate(shifted):
+            extra[k].append(c)
+    return [np.concatenate([o] + [e.astype(np.float32) for e in ex]) for o, ex in zip(out, extra)]
