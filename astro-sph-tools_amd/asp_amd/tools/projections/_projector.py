@@ -22,24 +22,18 @@ import numbers
 import numpy as np
 
 from ... import _lib
-from ..._axes import AXIS_COLUMNS, axis_index
 from ._kernels import kernel_id_of, quartic_spline_kernel
 
 
-def _soa(positions, smoothing_lengths, particle_properties, projection_axis):
+def _lengths(positions, smoothing_lengths, *fields):
     pos = np.asarray(positions)
     if pos.ndim != 2 or pos.shape[1] != 3:
         raise ValueError(f"positions must have shape (N, 3), got {pos.shape}")
-    h = np.asarray(smoothing_lengths).reshape(-1)
-    A = np.asarray(particle_properties).reshape(-1)
     n = pos.shape[0]
-    if h.shape[0] != n or A.shape[0] != n:
-        raise ValueError(f"positions ({n}), smoothing_lengths ({h.shape[0]}) and "
-                         f"particle_properties ({A.shape[0]}) differ in length")
-    a, b = AXIS_COLUMNS[axis_index(projection_axis)]
-    f32 = np.float32
-    return (np.ascontiguousarray(pos[:, a], dtype=f32), np.ascontiguousarray(pos[:, b], dtype=f32),
-            np.ascontiguousarray(h, dtype=f32), np.ascontiguousarray(A, dtype=f32))
+    lens = [np.asarray(f).reshape(-1).shape[0] for f in (smoothing_lengths,) + fields]
+    if any(k != n for k in lens):
+        raise ValueError(f"positions ({n}), smoothing_lengths ({lens[0]}) and "
+                         f"particle_properties ({lens[1]}) differ in length")
 
 
 def _check_chunk_size(chunk_size):
@@ -51,20 +45,30 @@ def _check_chunk_size(chunk_size):
     return int(chunk_size)
 
 
-def _run(u, v, h, a0, a1, image_size, chunk_size, extent, kernel_id, flags, device):
+def _run(positions, smoothing_lengths, props, projection_axis, image_size, chunk_size,
+         extent, kernel_id, ratio, deterministic, device):
+    """Stage the reader's fp64 arrays on the device (asp_stage_particles: axis selection
+    and fp32 conversion in HBM, the host-side step of _projector.py:38-51) and project
+    them (asp_project2d).  Returns the float32 host map(s)."""
     nx, ny = int(image_size[0]), int(image_size[1])
     out0 = np.zeros((nx, ny), dtype=np.float32)
-    out1 = None if a1 is None else np.zeros((nx, ny), dtype=np.float32)
+    out1 = None if len(props) < 2 else np.zeros_like(out0)
     if nx <= 0 or ny <= 0 or chunk_size < 0:
         # empty image, or range(0, N, negative) -> no tiles -> all zeros (reference)
         return out0, out1
     _lib.require_gpu(device)
-    x_min, x_max, y_min, y_max = (float(np.asarray(e)) for e in extent)
-    P = _lib.ptr
-    _lib.check(_lib.lib().asp_project2d(
-        P(u), P(v), P(h), P(a0), P(a1), u.shape[0], x_min, x_max, y_min, y_max, nx, ny,
-        chunk_size, kernel_id, flags, P(out0), P(out1), device, None))
-    return out0, out1
+    import torch
+
+    from ...device import project2d
+    from ...stage import stage_particles
+    u, v, h, pp = stage_particles(positions, smoothing_lengths, *props,
+                                  projection_axis=projection_axis, device=device)
+    o0, o1 = project2d(u, v, h, pp[0], pp[1] if len(pp) > 1 else None, image_size=(nx, ny),
+                       extent=tuple(float(np.asarray(e)) for e in extent),
+                       chunk_size=chunk_size, kernel=kernel_id, ratio=ratio,
+                       deterministic=deterministic)
+    torch.cuda.synchronize(u.device)
+    return o0.cpu().numpy(), (o1.cpu().numpy() if o1 is not None else None)
 
 
 def create_image(positions: np.ndarray, smoothing_lengths: np.ndarray,
@@ -80,9 +84,9 @@ def create_image(positions: np.ndarray, smoothing_lengths: np.ndarray,
     """
     cs = _check_chunk_size(chunk_size)
     kid = kernel_id_of(kernel_func)
-    u, v, h, A = _soa(positions, smoothing_lengths, particle_properties, projection_axis)
-    flags = _lib.ASP_F_DETERMINISTIC if deterministic else 0
-    img, _ = _run(u, v, h, A, None, image_size, cs, (x_min, x_max, y_min, y_max), kid, flags,
+    _lengths(positions, smoothing_lengths, particle_properties)
+    img, _ = _run(positions, smoothing_lengths, [particle_properties], projection_axis,
+                  image_size, cs, (x_min, x_max, y_min, y_max), kid, False, deterministic,
                   device)
     return img.astype(dtype, copy=False)
 
@@ -102,20 +106,20 @@ def create_weighted_image(positions, smoothing_lengths, weights, values, image_s
     """
     cs = _check_chunk_size(chunk_size)
     kid = kernel_id_of(kernel_func)
-    u, v, h, w = _soa(positions, smoothing_lengths, weights, projection_axis)
+    _lengths(positions, smoothing_lengths, weights)
+    w = np.asarray(weights, dtype=np.float64).reshape(-1)
     vals = np.asarray(values, dtype=np.float64).reshape(-1)
-    if vals.shape[0] != u.shape[0]:
+    if vals.shape[0] != w.shape[0]:
         raise ValueError("values and positions differ in length")
-    wv = np.ascontiguousarray(np.asarray(weights, np.float64).reshape(-1) * vals, dtype=np.float32)
-    det = _lib.ASP_F_DETERMINISTIC if deterministic else 0
+    ext = (x_min, x_max, y_min, y_max)
     if return_components:
-        s0, s1 = _run(u, v, h, wv, w, image_size, cs, (x_min, x_max, y_min, y_max), kid, det,
-                      device)
+        s0, s1 = _run(positions, smoothing_lengths, [w * vals, w], projection_axis, image_size,
+                      cs, ext, kid, False, deterministic, device)
         with np.errstate(divide="ignore", invalid="ignore"):
             ratio = np.where(s1 != 0, s0.astype(np.float64) / s1, 0.0)
         return ratio.astype(dtype, copy=False), s0.astype(dtype), s1.astype(dtype)
-    r, _ = _run(u, v, h, wv, w, image_size, cs, (x_min, x_max, y_min, y_max), kid,
-                _lib.ASP_F_RATIO | det, device)
+    r, _ = _run(positions, smoothing_lengths, [w * vals, w], projection_axis, image_size, cs,
+                ext, kid, True, deterministic, device)
     return r.astype(dtype, copy=False)
 
 

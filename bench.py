@@ -49,9 +49,11 @@ def parse():
                     help="PMC summary (tools/pmc_summary.py) for roofline.traffic")
     ap.add_argument("--deterministic", action="store_true",
                     help="int64 fixed-point accumulation (bitwise reproducible maps)")
-    ap.add_argument("--workload", default="map", choices=["map", "cube"],
+    ap.add_argument("--workload", default="map", choices=["map", "cube", "stage"],
                     help="map: the headline 2-D projection; cube: BASELINE configs[4], "
-                         "10^8 particles -> 512^3 density cube (not the driver's line)")
+                         "10^8 particles -> 512^3 density cube; stage: snapshot fp64 -> "
+                         "device fp32 SoA staging (SURVEY 8(f)); the last two are not the "
+                         "driver's line")
     ap.add_argument("--cube", type=int, default=512, help="cube edge (voxels), --workload cube")
     ap.add_argument("--chunks", type=int, default=None,
                     help="particle chunks of the scatter/deposit pipeline (default: library's)")
@@ -195,6 +197,69 @@ def run_cube(args, world, rank, local, dev):
         dist.destroy_process_group()
 
 
+def run_stage(args, dev):
+    """the reader's fp64 arrays (positions (N, 3), h, m, T) -> the
+    projector's fp32 SoA (u, v, h, m*T, m) in HBM with asp_stage_particles.  Device-resident
+    inputs are the timed rate (HBM-bound: 48 B read + 20 B written per particle); the host
+    path (PCIe-inclusive, chunked copies overlapped with conversion) and NumPy's host-side
+    conversion (what create_image did before, the CPU baseline) are timed on a bounded
+    sample of 2^24 particles."""
+    import numpy as np
+    import torch
+    from asp_amd.stage import stage_particles
+    n = args.n
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    pos = torch.rand((n, 3), generator=g, device=dev, dtype=torch.float64) * 8.0 - 4.0
+    h = torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 1e-3 + 1e-3
+    a0 = torch.rand(n, generator=g, device=dev, dtype=torch.float64)
+    a1 = torch.rand(n, generator=g, device=dev, dtype=torch.float64)
+    torch.cuda.synchronize()
+
+    def step():
+        return stage_particles(pos, h, a0, a1, projection_axis=2)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) / args.steps * 1e3
+    bytes_alg = n * (24 + 3 * 8 + 5 * 4)
+    m = min(n, 1 << 24)
+    hp = [x[:m].cpu().numpy() for x in (pos, h, a0, a1)]
+    stage_particles(*hp, projection_axis=2)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    stage_particles(*hp, projection_axis=2)
+    torch.cuda.synchronize()
+    host_s = time.perf_counter() - t
+    t = time.perf_counter()
+    f32 = [np.ascontiguousarray(hp[0][:, 0], np.float32), np.ascontiguousarray(hp[0][:, 1], np.float32)]
+    f32 += [np.ascontiguousarray(x, np.float32) for x in hp[1:]]
+    cpu_s = time.perf_counter() - t
+    res = {
+        "metric": "staged particles/s (snapshot fp64 -> device fp32 SoA)", "value": n / ms * 1e3,
+        "unit": "particles/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64->f32", "data": "synthetic uniform, generated in HBM",
+        "config": {"workload": f"stage: {n:.0e} particles, positions (N,3) + h + 2 fields",
+                   "particles": n},
+        "roofline": {"bound": "hbm", "kernel": "k_stage", "achieved": round(bytes_alg / ms / 1e6, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(bytes_alg / ms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_alg_per_launch": bytes_alg},
+        "host_path": {"particles": m, "seconds": round(host_s, 4),
+                      "GB_per_s_pcie_inclusive": round(m * 48 / host_s / 1e9, 2)},
+        "cpu_baseline": {"value": m / cpu_s, "unit": "particles/s", "cores": 1, "kind": "port",
+                         "sample": f"NumPy column select + astype(float32) of {m} particles "
+                                   "(the host-side conversion create_image performs)"},
+    }
+    print(json.dumps(res), flush=True)
+
+
 def output_check(out0, out1, a0, a1, ratio, world=1):
     """Size-independent sanity of the timed map (the parity proper is tests/): finite,
     non-negative component sums (W >= 0, m > 0), and for the mass-weighted map every pixel a
@@ -246,6 +311,8 @@ def main():
 
     if args.workload == "cube":
         return run_cube(args, world, rank, local, dev)
+    if args.workload == "stage":
+        return run_stage(args, dev)
     G, extent = args.grid, 4.0
     ext = (-extent, extent, -extent, extent)
     t0 = time.time()

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Copy one measurement session (tools_gpu_measure.sh -> gpurun_out/meas, prof_meas) into
+"""Copy one measurement session (tools/gpu/measure.sh -> gpurun_out/meas, prof_meas) into
 the tracked profiles/<round>/ directory, and cross-check the rocprofv3 kernel averages
 against the HIP-event stage times bench.py measured in its own run.
 

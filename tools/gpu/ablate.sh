@@ -1,6 +1,6 @@
 #!/bin/bash
 # diagnostic library variants (tools/ablate.sh) on the headline config
-# usage: tools_gpu_ablate.sh MACRO "k1 k2" [bench args]
+# usage: tools/gpu/ablate.sh MACRO "k1 k2" [bench args]
 cd "$GRAFT_REPO_ROOT" || exit 9
 m=$1; ks=$2; shift 2
 mkdir -p gpurun_out/ablate

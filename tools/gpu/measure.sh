@@ -18,4 +18,8 @@ rc=$?; echo "rocprof bench rc=$rc"
 [ $rc -ne 0 ] && exit $rc
 ASP_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --op allreduce > gpurun_out/meas/bench_2rank_gloo.json 2> gpurun_out/meas/bench_2rank_gloo.err
 rc=$?; echo "2-rank rehearsal rc=$rc"; tail -1 gpurun_out/meas/bench_2rank_gloo.json | cut -c1-300
+timeout -k 10 300 python bench.py --workload stage --steps 10 --warmup 2 > gpurun_out/meas/bench_stage.json 2> gpurun_out/meas/bench_stage.err
+rc=$?; echo "stage bench rc=$rc"; tail -1 gpurun_out/meas/bench_stage.json | cut -c1-300
+timeout -k 10 300 python bench.py --workload cube --steps 3 --warmup 1 > gpurun_out/meas/bench_cube.json 2> gpurun_out/meas/bench_cube.err
+rc=$?; echo "cube bench rc=$rc"; tail -1 gpurun_out/meas/bench_cube.json | cut -c1-300
 exit 0
