@@ -57,6 +57,7 @@ struct Workspace {
     int pset = 0;                  // the set the current call records into
     double stage_ms[kStages] = {};
     long long stage_n[kStages] = {};
+    Buf knn[7];  // asp_knn_smoothing_lengths
     Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
         wide, slabs, morton, aux[6];
     int* h_counters = nullptr;  // pinned

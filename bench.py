@@ -49,7 +49,7 @@ def parse():
                     help="PMC summary (tools/pmc_summary.py) for roofline.traffic")
     ap.add_argument("--deterministic", action="store_true",
                     help="int64 fixed-point accumulation (bitwise reproducible maps)")
-    ap.add_argument("--workload", default="map", choices=["map", "cube", "stage"],
+    ap.add_argument("--workload", default="map", choices=["map", "cube", "stage", "knn"],
                     help="map: the headline 2-D projection; cube: BASELINE configs[4], "
                          "10^8 particles -> 512^3 density cube; stage: snapshot fp64 -> "
                          "device fp32 SoA staging (SURVEY 8(f)); the last two are not the "
@@ -260,6 +260,51 @@ def run_stage(args, dev):
     print(json.dumps(res), flush=True)
 
 
+def run_knn(args, dev):
+    """h = distance to the 32nd nearest neighbour (the reference's
+    scipy KDTree query, io/SWIFT/_SnapshotSWIFT.py:62-83) for N Plummer particles, inputs
+    in HBM.  CPU baseline: scipy KDTree build + query (one thread, as the reference calls
+    it) on a bounded random sample."""
+    import numpy as np
+    import torch
+    from asp_amd.knn import knn_smoothing_lengths
+    from asp_amd.plummer import plummer_torch
+    d = plummer_torch(args.n, seed=0, h_law="pixel", extent=4.0, grid=64, device=dev)
+    pos = torch.stack([d["x"], d["y"], d["z"]], dim=1).double().contiguous()
+    del d
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        knn_smoothing_lengths(pos, 32)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        h = knn_smoothing_lengths(pos, 32)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) / args.steps * 1e3
+    ok = bool(torch.isfinite(h).all().item()) and float(h.min().item()) > 0
+    res = {
+        "metric": "k-NN smoothing lengths/s (k = 32, fp64, bit-exact vs scipy KDTree)",
+        "value": args.n / ms * 1e3, "unit": "particles/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic Plummer sphere (a=1, seed 0) generated in HBM",
+        "config": {"workload": f"knn: {args.n:.0e} particles, k = 32", "particles": args.n},
+        "output_ok": ok,
+    }
+    if args.cpu_baseline != "off":
+        from scipy.spatial import KDTree
+        m = min(args.n, 1 << 20)
+        sample = pos[torch.randperm(args.n, device=dev)[:m]].cpu().numpy()
+        t = time.perf_counter()
+        KDTree(sample).query(sample, k=32)
+        cpu_s = time.perf_counter() - t
+        res["cpu_baseline"] = {"value": m / cpu_s, "unit": "particles/s", "cores": 1,
+                               "kind": "reference",
+                               "sample": f"scipy KDTree build + query(k=32) of {m} random "
+                                         f"particles of the set (the reference's call)"}
+    print(json.dumps(res), flush=True)
+
+
 def output_check(out0, out1, a0, a1, ratio, world=1):
     """Size-independent sanity of the timed map (the parity proper is tests/): finite,
     non-negative component sums (W >= 0, m > 0), and for the mass-weighted map every pixel a
@@ -313,6 +358,8 @@ def main():
         return run_cube(args, world, rank, local, dev)
     if args.workload == "stage":
         return run_stage(args, dev)
+    if args.workload == "knn":
+        return run_knn(args, dev)
     G, extent = args.grid, 4.0
     ext = (-extent, extent, -extent, extent)
     t0 = time.time()

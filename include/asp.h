@@ -204,6 +204,19 @@ int asp_wrapped_distance(const double *from, int64_t pf, const double *to, int64
                          int32_t device, void *stream);
 
 /*
+ * Smoothing lengths from the k-th nearest neighbour: replaces
+ * the scipy KDTree query of io/SWIFT/_SnapshotSWIFT.py:62-83 (dark matter: h = distance to
+ * the k-th nearest particle, the particle itself counted, k = 32 there):
+ *   h[i] = sqrt(d2_(k)),  d2 = ((x_i - x_j)^2 + (y_i - y_j)^2) + (z_i - z_j)^2  (fp64),
+ * d2_(k) the k-th smallest over all j, j = i included -- scipy's Euclidean distance, so
+ * the result is bit-identical to the reference's; +inf when n < k (scipy's value for a
+ * missing neighbour).  positions (n, 3) float64 row-major, h float64; 1 <= k <= 64,
+ * n < 2^31.  Host pointers unless ASP_F_DEVICE_PTRS (then ordered on `stream`).
+ */
+int asp_knn_smoothing_lengths(const double *positions, int64_t n, int32_t k, double *h,
+                              int32_t flags, int32_t device, void *stream);
+
+/*
  * Statistics of the last asp_project2d call on `device` (inspection / roofline):
  * stats[0] = records binned (particle x GPU-tile insertions), stats[1] = work items,
  * stats[2] = wide particles, stats[3] = GPU tile edge (pixels), stats[4] = GPU tiles,
