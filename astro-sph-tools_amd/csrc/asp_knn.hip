@@ -8,17 +8,18 @@
 // +inf when n < k (scipy's value for a missing neighbour).
 //
 // MI355X layout: particles sorted along a 63-bit Morton curve (21 bits per axis over the
-// bounding cube; rocPRIM radix sort), positions gathered into sorted fp64 SoA so that the
-// particles a thread scans are contiguous and shared with its neighbours in the wave
-// (L1/L2 hits).  Per particle (one thread):
-//   1. an upper bound R on the k-th distance from the finest Morton cell around it that
-//      holds k + 1 particles (any k points bound the k-th nearest distance from above);
-//   2. every cell of the Morton level whose cell edge is >= R that the ball of radius R
-//      (plus one quantum of slack) touches -- at most 3 per axis, each a contiguous
-//      key range found by binary search -- own cell first, cells whose box lies beyond
-//      the current k-th distance skipped;
-//   3. a register top-k (the k smallest d2 seen; replace-the-maximum), exact in fp64.
-// The k-th smallest d2 over a superset of the ball is the exact answer.
+// bounding cube; rocPRIM radix sort), positions gathered into sorted fp64 SoA.  One wave
+// takes 64 consecutive particles of the curve (k_knn_wave):
+//   1. the curve window of W = 128 entries either side is streamed once per wave through
+//      LDS (coalesced), every lane testing every entry; candidates below a lane's k-th
+//      distance so far are buffered in registers and merged into its register top-k a
+//      few at a time (the O(k) insertion does not run per candidate for the whole wave);
+//   2. each lane then checks its ball (radius = its k-th distance so far) against the
+//      cells of edge >= half that radius: cells whose Morton key range lies inside the
+//      window's span are complete; any other cell the ball reaches is scanned by the
+//      lane (binary-searched key range, minus the window).
+// The k-th smallest d2 over a superset of the ball is the exact answer.  (k_knn: the
+// one-lane-per-particle form, kept as a diagnostic; DESIGN.md §12 has the measurements.)
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -26,6 +27,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/asp.h"
@@ -201,17 +203,13 @@ __device__ __forceinline__ long long lower_bound(const unsigned long long* __res
     return lo;
 }
 
+// The whole search for particle i by one lane: returns its k-th smallest d2.
 template <int K>
-__global__ __launch_bounds__(kKnnBlock) void k_knn(const double* __restrict__ xs,
-                                                   const double* __restrict__ ys,
-                                                   const double* __restrict__ zs,
-                                                   const unsigned long long* __restrict__ keys,
-                                                   const int* __restrict__ idx, long long n, int k,
-                                                   const KGrid* __restrict__ g,
-                                                   double* __restrict__ h) {
-    long long i = (long long)blockIdx.x * kKnnBlock + threadIdx.x;
-    if (i >= n) return;
-    const KGrid G = *g;
+__device__ __forceinline__ double knn_thread(long long i, const double* __restrict__ xs,
+                                             const double* __restrict__ ys,
+                                             const double* __restrict__ zs,
+                                             const unsigned long long* __restrict__ keys,
+                                             long long n, int k, const KGrid& G) {
     const double x = xs[i], y = ys[i], z = zs[i];
     TopK<K> T;
     T.init(k);
@@ -290,7 +288,152 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn(const double* __restrict__ xs
                     }
         }
     }
-    h[idx[i]] = sqrt(T.mx);
+    return T.mx;
+}
+
+template <int K>
+__global__ __launch_bounds__(kKnnBlock) void k_knn(const double* __restrict__ xs,
+                                                   const double* __restrict__ ys,
+                                                   const double* __restrict__ zs,
+                                                   const unsigned long long* __restrict__ keys,
+                                                   const int* __restrict__ idx, long long n,
+                                                   int k, const KGrid* __restrict__ g,
+                                                   double* __restrict__ h) {
+    long long i = (long long)blockIdx.x * kKnnBlock + threadIdx.x;
+    if (i >= n) return;
+    const KGrid G = *g;
+    h[idx[i]] = sqrt(knn_thread<K>(i, xs, ys, zs, keys, n, k, G));
+}
+
+// ----------------------------------------------------------------------------------
+// Wave-cooperative search: one wave takes 64 consecutive particles of the Morton order
+// (spatially compact).
+//   1. The curve window [base - W, base + 64 + W) is streamed ONCE per wave: 64 coalesced
+//      loads into LDS per chunk, each lane testing the 64 entries against its own
+//      particle (LDS broadcast reads).  Candidates below a lane's current k-th distance go
+//      to a small register buffer, merged into the top-k when some lane's buffer is full,
+//      so the O(k) insertion runs a few times per chunk, not per candidate for the wave.
+//   2. Each lane then checks its ball (radius = its k-th distance so far, plus slack)
+//      against the cells of the level with edge >= that radius: a cell whose key range
+//      lies strictly inside the window's key span is complete already; any other cell the
+//      ball reaches is scanned by the lane alone (binary-searched range minus the window).
+// Exact: every particle within the final k-th distance is in the window or in a scanned
+// cell.  Far from jumps of the curve the window covers the whole ball and step 2 scans
+// nothing.
+// ----------------------------------------------------------------------------------
+constexpr int kBufSlots = 8;
+constexpr int kWinHalf = 128;  // W: curve window each side of the wave (swept: 64-512)
+constexpr int kCellFine = 1;   // verification cells >= half the ball radius (swept: 0-3)
+
+template <int K>
+struct Cand {
+    TopK<K> T;
+    double buf[kBufSlots];
+    int cnt;
+    __device__ __forceinline__ void push(double d) {  // d < T.mx already
+#pragma unroll
+        for (int q = 0; q < kBufSlots; ++q)
+            if (q == cnt) buf[q] = d;
+        ++cnt;
+    }
+    __device__ __forceinline__ void flush() {
+#pragma unroll
+        for (int q = 0; q < kBufSlots; ++q)
+            if (q < cnt) T.insert(buf[q]);
+        cnt = 0;
+    }
+};
+
+template <int K>
+__device__ __forceinline__ void wave_scan(long long a, long long b, const double* __restrict__ xs,
+                                          const double* __restrict__ ys,
+                                          const double* __restrict__ zs, double* lx, double* ly,
+                                          double* lz, int lane, double x, double y, double z,
+                                          Cand<K>& C) {
+    for (long long c = a; c < b; c += 64) {
+        const int m = (int)min(64LL, b - c);
+        if (lane < m) {
+            lx[lane] = xs[c + lane];
+            ly[lane] = ys[c + lane];
+            lz[lane] = zs[c + lane];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int q = 0; q < m; ++q) {
+            double d = dist2(x, y, z, lx[q], ly[q], lz[q]);
+            if (d < C.T.mx) C.push(d);
+            if (__builtin_amdgcn_ballot_w64(C.cnt == kBufSlots)) C.flush();
+        }
+        __builtin_amdgcn_wave_barrier();  // the chunk is rewritten next
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict__ xs,
+                                                        const double* __restrict__ ys,
+                                                        const double* __restrict__ zs,
+                                                        const unsigned long long* __restrict__ keys,
+                                                        const int* __restrict__ idx, long long n,
+                                                        int k, const KGrid* __restrict__ g,
+                                                        double* __restrict__ h, int diag,
+                                                        int whalf, int fine) {
+    __shared__ double sx[kKnnBlock / 64][64], sy[kKnnBlock / 64][64], sz[kKnnBlock / 64][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long long base = ((long long)blockIdx.x * (kKnnBlock / 64) + wv) * 64;
+    if (base >= n) return;  // wave-uniform
+    const long long i = base + lane;
+    const bool act = i < n;
+    const long long ic = act ? i : n - 1;  // idle lanes shadow the last particle, write nothing
+    const KGrid G = *g;
+    const double x = xs[ic], y = ys[ic], z = zs[ic];
+    Cand<K> C;
+    C.T.init(k);
+    C.cnt = 0;
+    const long long win0 = max(0LL, base - whalf), win1 = min(n, base + 64 + whalf);
+    wave_scan<K>(win0, win1, xs, ys, zs, sx[wv], sy[wv], sz[wv], lane, x, y, z, C);
+    C.flush();
+    if (act && n >= k && diag == 0) {
+        // key span the window covers completely (open at the ends of the array)
+        const unsigned long long klo = win0 == 0 ? 0ULL : keys[win0] + 1;
+        const unsigned long long khi = win1 == n ? ~0ULL : keys[win1 - 1];
+        const double R = sqrt(C.T.mx) * (1.0 + 0x1p-40);
+        int e;
+        frexp(R * G.scale + 1.0, &e);  // cell edge 2^shift >= R + 1 quantum ...
+        const int shift = max(0, min(e, kQBits) - fine), sh3 = 3 * shift;  // ... / 2^fine
+        const double c3[3] = {x, y, z};
+        long long ca[3], cb[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            ca[a] = max(0LL, quant(c3[a] - R, G.lo[a], G.scale) - 1) >> shift;
+            cb[a] = min(kQMax, quant(c3[a] + R, G.lo[a], G.scale) + 1) >> shift;
+        }
+        for (long long cx = ca[0]; cx <= cb[0]; ++cx)
+            for (long long cy = ca[1]; cy <= cb[1]; ++cy)
+                for (long long cz = ca[2]; cz <= cb[2]; ++cz) {
+                    unsigned long long p = morton3(cx, cy, cz);
+                    unsigned long long k0 = sh3 >= 63 ? 0ULL : p << sh3;
+                    unsigned long long k1 = sh3 >= 63 ? ~0ULL : (p + 1) << sh3;  // exclusive
+                    if (k0 >= klo && k1 <= khi) continue;  // inside the window already
+                    const long long cc[3] = {cx, cy, cz};
+                    double md = 0.0;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        double clo = G.lo[a] + (double)(cc[a] << shift) * G.quantum - G.quantum;
+                        double chi = G.lo[a] + (double)((cc[a] + 1) << shift) * G.quantum + G.quantum;
+                        double d = c3[a] < clo ? clo - c3[a] : (c3[a] > chi ? c3[a] - chi : 0.0);
+                        md += d * d;
+                    }
+                    if (md * (1.0 - 0x1p-40) > C.T.mx) continue;
+                    long long j0 = lower_bound(keys, n, k0);
+                    long long j1 = sh3 >= 63 ? n : lower_bound(keys + j0, n - j0, k1) + j0;
+                    for (long long j = j0; j < min(j1, win0); ++j)
+                        C.T.insert(dist2(x, y, z, xs[j], ys[j], zs[j]));
+                    for (long long j = max(j0, win1); j < j1; ++j)
+                        C.T.insert(dist2(x, y, z, xs[j], ys[j], zs[j]));
+                }
+    }
+    if (act) h[idx[i]] = sqrt(C.T.mx);
 }
 
 static int knn(const double* pos, long long n, int k, double* h, int flags, int device,
@@ -347,14 +490,31 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     hipLaunchKernelGGL(k_gather, dim3(grid), dim3(kKnnBlock), 0, st, dpos, (long long)n,
                        (const int*)iout, xs, ys, zs);
     ASP_LAUNCHED();
+    // diagnostics only: ASP_KNN_THREAD = one lane per particle throughout;
+    // ASP_KNN_DIAG = 1: the window pass alone (wrong results, timing)
+    const bool per_thread = getenv("ASP_KNN_THREAD") != nullptr;
+    const int diag = getenv("ASP_KNN_DIAG") ? atoi(getenv("ASP_KNN_DIAG")) : 0;
+    const int whalf = getenv("ASP_KNN_WINDOW") ? atoi(getenv("ASP_KNN_WINDOW")) : kWinHalf;
+    const int fine = getenv("ASP_KNN_FINE") ? atoi(getenv("ASP_KNN_FINE")) : kCellFine;
+#define ASP_KNN(KN)                                                                               \
+    do {                                                                                          \
+        if (per_thread)                                                                           \
+            hipLaunchKernelGGL(k_knn<KN>, dim3(grid), dim3(kKnnBlock), 0, st, (const double*)xs,  \
+                               (const double*)ys, (const double*)zs,                              \
+                               (const unsigned long long*)kout, (const int*)iout, (long long)n,   \
+                               k, (const KGrid*)dg, dh);                                          \
+        else                                                                                      \
+            hipLaunchKernelGGL(k_knn_wave<KN>, dim3((unsigned)((n + 255) / 256)),                  \
+                               dim3(kKnnBlock), 0, st, (const double*)xs, (const double*)ys,      \
+                               (const double*)zs, (const unsigned long long*)kout,                \
+                               (const int*)iout, (long long)n, k, (const KGrid*)dg, dh, diag, whalf,  \
+                               fine);    \
+    } while (0)
     if (k <= 32)
-        hipLaunchKernelGGL(k_knn<32>, dim3(grid), dim3(kKnnBlock), 0, st, (const double*)xs,
-                           (const double*)ys, (const double*)zs, (const unsigned long long*)kout,
-                           (const int*)iout, (long long)n, k, (const KGrid*)dg, dh);
+        ASP_KNN(32);
     else
-        hipLaunchKernelGGL(k_knn<64>, dim3(grid), dim3(kKnnBlock), 0, st, (const double*)xs,
-                           (const double*)ys, (const double*)zs, (const unsigned long long*)kout,
-                           (const int*)iout, (long long)n, k, (const KGrid*)dg, dh);
+        ASP_KNN(64);
+#undef ASP_KNN
     ASP_LAUNCHED();
     if (!dev) {
         ASP_HIP(hipMemcpyAsync(h, dh, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st));
