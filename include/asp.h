@@ -217,6 +217,25 @@ int asp_knn_smoothing_lengths(const double *positions, int64_t n, int32_t k, dou
                               int32_t flags, int32_t device, void *stream);
 
 /*
+ * Ionisation-table interpolation: replaces the scipy
+ * RegularGridInterpolator of data_structures/_IonisationTable.py:44-58 (linear,
+ * bounds_error=False, fill_value=-inf; the HM01 tables of
+ * io/ionisation_tables/_HM01.py:61-92 are 3-D over (log10 n_H, log10 T, redshift)).
+ * table: (n0, n1, n2) float64 C-order on strictly ascending axes g0, g1, g2; points:
+ * (n, 3) rows, or (n, 2) rows with `zvalue` inserted at axis `zaxis` (ncol = 2;
+ * evaluate_at_redshift, :54-58).  out[i] = the interpolated value, bit-identical to scipy
+ * 1.15's linear evaluation (fill outside the table, NaN for NaN input);
+ * mode 1: out[i] = (a0[i] * a1[i]) * value, mode 2: (a0[i] * a1[i]) * 10^value -- the ion
+ * masses m * X_element * f_ion that feed asp_project2d for an ion column map.  Device
+ * pointers, ordered on `stream`.
+ */
+int asp_table_interp3(const double *table, int32_t n0, int32_t n1, int32_t n2,
+                      const double *g0, const double *g1, const double *g2,
+                      const double *points, int32_t ncol, int32_t zaxis, double zvalue,
+                      int64_t n, double fill, int32_t mode, const double *a0, const double *a1,
+                      double *out, int32_t device, void *stream);
+
+/*
  * Statistics of the last asp_project2d call on `device` (inspection / roofline):
  * stats[0] = records binned (particle x GPU-tile insertions), stats[1] = work items,
  * stats[2] = wide particles, stats[3] = GPU tile edge (pixels), stats[4] = GPU tiles,

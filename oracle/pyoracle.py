@@ -271,3 +271,49 @@ def stage_particles(positions, h, props, axis, L=None, centre=None, shift=None,
         for k, c in enumerate(shifted):
             extra[k].append(c)
     return [np.concatenate([o] + [e.astype(np.float32) for e in ex]) for o, ex in zip(out, extra)]
+
+
+def table_interp3(table, grids, points, fill=-np.inf):
+    """Linear interpolation of a 3-D table (IonisationTableBase.__call__,
+    data_structures/_IonisationTable.py:44-52 -> scipy 1.15 RegularGridInterpolator with
+    bounds_error=False, fill_value=-inf), restated in NumPy with scipy's operation order
+    (_rgi.py: find_indices, _evaluate_linear, then fill, then NaN):
+      i_d = largest i with g_d[i] <= x_d, clamped to [0, n_d - 2];
+      y_d = (x_d - g_d[i_d]) / (g_d[i_d + 1] - g_d[i_d]);
+      v = 0; for the 8 corners (last axis fastest): v = v + t[corner] * ((w0 * w1) * w2)."""
+    t = np.asarray(table, np.float64)
+    P = np.asarray(points, np.float64).reshape(-1, 3)
+    idx, y = [], []
+    for d in range(3):
+        g = np.asarray(grids[d], np.float64)
+        x = P[:, d]
+        i = np.clip(np.searchsorted(g, x, side="right") - 1, 0, g.size - 2)
+        with np.errstate(invalid="ignore"):
+            y.append((x - g[i]) / (g[i + 1] - g[i]))
+        idx.append(i)
+    v = np.zeros(P.shape[0])
+    for a in (0, 1):
+        for b in (0, 1):
+            for e in (0, 1):
+                w0 = y[0] if a else 1 - y[0]
+                w1 = y[1] if b else 1 - y[1]
+                w2 = y[2] if e else 1 - y[2]
+                with np.errstate(invalid="ignore"):
+                    v = v + t[idx[0] + a, idx[1] + b, idx[2] + e] * ((w0 * w1) * w2)
+    oob = np.zeros(P.shape[0], bool)
+    for d in range(3):
+        g = np.asarray(grids[d], np.float64)
+        oob |= (P[:, d] < g[0]) | (P[:, d] > g[-1])
+    v[oob] = fill
+    v[np.isnan(P).any(axis=1)] = np.nan
+    return v
+
+
+def table_at_redshift(table, grids, points2, z, zaxis=2, fill=-np.inf):
+    """IonisationTableBase.evaluate_at_redshift (_IonisationTable.py:54-58): the constant z
+    inserted as column `zaxis`, then table_interp3."""
+    P2 = np.asarray(points2, np.float64)
+    P = np.empty((P2.shape[0], 3))
+    P[:, np.arange(3) != zaxis] = P2
+    P[:, zaxis] = z
+    return table_interp3(table, grids, P, fill)
