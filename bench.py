@@ -49,7 +49,7 @@ def parse():
                     help="PMC summary (tools/pmc_summary.py) for roofline.traffic")
     ap.add_argument("--deterministic", action="store_true",
                     help="int64 fixed-point accumulation (bitwise reproducible maps)")
-    ap.add_argument("--workload", default="map", choices=["map", "cube", "stage", "knn"],
+    ap.add_argument("--workload", default="map", choices=["map", "cube", "stage", "knn", "ion"],
                     help="map: the headline 2-D projection; cube: BASELINE configs[4], "
                          "10^8 particles -> 512^3 density cube; stage: snapshot fp64 -> "
                          "device fp32 SoA staging (SURVEY 8(f)); the last two are not the "
@@ -305,6 +305,87 @@ def run_knn(args, dev):
     print(json.dumps(res), flush=True)
 
 
+def run_ion(args, dev):
+    """per-particle ion masses m * X * 10^f_ion(log10 n_H, log10 T, z)
+    for an ion column map -- the reference's IonisationTableBase.evaluate_at_redshift
+    (data_structures/_IonisationTable.py:54-58, scipy RegularGridInterpolator) fused with
+    the mass product, inputs in HBM.  Table: HM01-shaped 41 x 141 x 49 fp64 (synthetic
+    values; the HDF5 tables are not in the repo).  Algorithmic bytes per particle: 16 (n_H,
+    T) + 16 (m, X) + 8 (out) = 40 B; the table stays in cache.  CPU baseline: the
+    reference's call (scipy RGI at a redshift, one thread) on a bounded sample."""
+    import numpy as np
+    import torch
+    from asp_amd.ionisation import IonisationTable, ion_masses
+    n = args.n
+    rng = np.random.default_rng(0)
+    shape = (41, 141, 49)
+    axes = [np.linspace(-8.0, 0.0, shape[0]), np.linspace(2.0, 9.0, shape[1]),
+            np.concatenate([np.linspace(0.0, 1.0, 21), np.linspace(1.1, 9.0, 28)])]
+    table = rng.uniform(-12.0, 0.0, shape)
+    tab = IonisationTable(table, *axes, redshift_input_index=2)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    state = torch.rand((n, 2), generator=g, device=dev, dtype=torch.float64)
+    state[:, 0] = state[:, 0] * 9.0 - 8.5          # a few points outside the table -> -inf
+    state[:, 1] = state[:, 1] * 7.0 + 2.0
+    m = torch.rand(n, generator=g, device=dev, dtype=torch.float64) + 0.5
+    X = torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 0.2 + 0.6
+    z = 2.25
+    torch.cuda.synchronize()
+
+    def step():
+        return tab._run(state, 2, z, 2, m, X)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) / args.steps * 1e3
+    bytes_alg = n * 40
+    k = min(n, 1 << 16)
+    chk = out[:k].cpu().numpy()
+    s_h = state[:k].cpu().numpy()
+    from scipy.interpolate import RegularGridInterpolator
+    rgi = RegularGridInterpolator(axes, table, bounds_error=False, fill_value=-np.inf)
+    P = np.empty((k, 3))
+    P[:, :2] = s_h
+    P[:, 2] = z
+    want = (m[:k].cpu().numpy() * X[:k].cpu().numpy()) * 10.0 ** rgi(P)
+    ok = bool(np.allclose(chk, want, rtol=4.5e-16, atol=0))
+    res = {
+        "metric": "ion masses/s (m * X * f_ion from a 3-D ionisation table, fp64)",
+        "value": n / ms * 1e3, "unit": "particles/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic gas states and HM01-shaped table (41x141x49), generated in HBM",
+        "config": {"workload": f"ion: {n:.0e} particles, HM01-shaped table at z = {z}",
+                   "particles": n},
+        "roofline": {"bound": "hbm", "kernel": "k_table_slab", "achieved": round(bytes_alg / ms / 1e6, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(bytes_alg / ms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_alg_per_launch": bytes_alg},
+        "output_ok": ok,
+    }
+    if args.cpu_baseline != "off":
+        c = min(n, 1 << 22)
+        s_c = state[:c].cpu().numpy()
+        mc, Xc = m[:c].cpu().numpy(), X[:c].cpu().numpy()
+        t = time.perf_counter()
+        Pc = np.empty((c, 3))
+        Pc[:, :2] = s_c
+        Pc[:, 2] = z
+        (mc * Xc) * 10.0 ** rgi(Pc)
+        cpu_s = time.perf_counter() - t
+        res["cpu_baseline"] = {"value": c / cpu_s, "unit": "particles/s", "cores": 1,
+                               "kind": "reference",
+                               "sample": f"scipy RegularGridInterpolator at a redshift (the "
+                                         f"reference's call) + mass product on {c} particles"}
+    print(json.dumps(res), flush=True)
+
+
 def output_check(out0, out1, a0, a1, ratio, world=1):
     """Size-independent sanity of the timed map (the parity proper is tests/): finite,
     non-negative component sums (W >= 0, m > 0), and for the mass-weighted map every pixel a
@@ -358,6 +439,8 @@ def main():
         return run_cube(args, world, rank, local, dev)
     if args.workload == "stage":
         return run_stage(args, dev)
+    if args.workload == "ion":
+        return run_ion(args, dev)
     if args.workload == "knn":
         return run_knn(args, dev)
     G, extent = args.grid, 4.0

@@ -94,3 +94,22 @@ def test_ion_masses_and_column_map(gpu, oracle, table, g9):
     img = create_image(pos, h, got, (128, 128), 32, 2, 0.0, 1.0, 0.0, 1.0)
     ref = oracle.create_image(pos, h, want, (128, 128), 32, 2, 0.0, 1.0, 0.0, 1.0)
     assert_map_close(img, ref)
+
+
+@pytest.mark.parametrize("zaxis", [0, 1, 2])
+def test_at_redshift_any_axis_matches_restatement(gpu, oracle, zaxis):
+    """The fixed axis anywhere (axis 2 goes through the LDS slab kernel, 0 / 1 through the
+    global one), on a random table, random states and an HM01-sized slab."""
+    from asp_amd.ionisation import IonisationTable
+    rng = np.random.default_rng(100 + zaxis)
+    shape = (41, 141, 49)
+    grids = [np.cumsum(rng.uniform(0.05, 0.2, k)) for k in shape]
+    t = rng.uniform(-10.0, 0.0, shape)
+    tab = IonisationTable(t, *grids, redshift_input_index=zaxis)
+    free = [d for d in range(3) if d != zaxis]
+    P = np.stack([rng.uniform(grids[d][0] - 0.1, grids[d][-1] + 0.1, 300000) for d in free], 1)
+    for z in (grids[zaxis][7], 0.5 * (grids[zaxis][3] + grids[zaxis][4]), grids[zaxis][-1],
+              grids[zaxis][-1] + 1.0, np.nan):
+        got = tab.evaluate_at_redshift(P, float(z))
+        want = oracle.table_at_redshift(t, grids, P, float(z), zaxis=zaxis)
+        assert np.array_equal(bits(got), bits(want)), (zaxis, z)
