@@ -38,10 +38,24 @@ namespace asp {
 constexpr int kBX = 16, kBY = 16, kBZ = 32;  // brick edge (voxels); z fastest
 constexpr int kBXs = 4, kBYs = 4, kBZs = 5;
 constexpr int kBrickVox = kBX * kBY * kBZ;   // 8192 -> 64 KiB of fp64 accumulators
+#ifndef ASP_CUBE_PAD
+#define ASP_CUBE_PAD 1
+#endif
+// LDS accumulator rows padded to kBZP doubles: a 32-double (256-B) row stride puts the same
+// k of adjacent columns in the same LDS bank, and lanes walk adjacent columns
+constexpr int kBZP = kBZ + ASP_CUBE_PAD;
+constexpr int kBrickLds = kBX * kBY * kBZP;
+__device__ __forceinline__ int lds_vox(int v) {  // dense brick index -> padded LDS index
+    return (v >> kBZs) * kBZP + (v & (kBZ - 1));
+}
 constexpr int kMaxBricks = 16384;            // C1/C3 LDS: one int per brick (64 KiB)
 static_assert(kMaxBricks <= kScanThreads * kScanPer, "k_tilescan holds <= kScanPer bricks per thread");
 constexpr int k3Block = 512;                 // count / scatter / deposit workgroup
-constexpr int kSmallVox = 32;                // boxes up to this many voxels: lane-per-record
+#ifndef ASP_CUBE_LANE_COLS
+#define ASP_CUBE_LANE_COLS 30
+#endif
+constexpr int kLaneCols = ASP_CUBE_LANE_COLS;  // boxes up to this many (i, j) columns:
+                                               // lane-per-record, wider: a wave per record
 
 struct Grid3 {
     double x_min, y_min, z_min;
@@ -50,6 +64,7 @@ struct Grid3 {
     int nx, ny, nz;
     int k_lo, nzl;           // output planes [k_lo, k_lo + nzl)
     int nbx, nby, nbz, nb;   // bricks over the output slab
+    int lane_cols;           // deposit: boxes up to this many columns lane-per-record
 };
 
 struct Box3 {
@@ -179,22 +194,59 @@ __global__ __launch_bounds__(k3Block) void k3_scatter(
 struct Rec3 {
     double x, y, z, thr;  // fp64 copies of the fp32 inputs; thr = (2h)^2 in fp64
     float hinv, s;        // 1 / h, a * norm(h)
+    float kc;             // brick-local plane coordinate of z, (z - z_min) / pz - K0
     Box3 b;               // clipped to the brick, brick-local indices
 };
 
-template <int KID>
-__device__ __forceinline__ void pair3(const Rec3& R, int li, int lj, int lk, const double* xt,
-                                      const double* yt, const double* zt, double* acc) {
-    // .pyx:30-31 extended to 3-D; the oracle's voxel_pass, operation for operation
+// One (i, j) column of a record's box.  The oracle's test is
+//   r2 = dx * dx + dy * dy + dz * dz  <  (2h)^2      (voxel_pass, left to right in fp64)
+// so s = dx * dx + dy * dy is the same intermediate for every k of the column, and only
+// the k with |dz| <= sqrt(thr - s) can pass.  That range is widened to a superset (the
+// rounding of s + dz^2 allows |dz|^2 up to thr - s + ~2 eps thr; 8 eps thr is added, and
+// axis_cells adds its 2^-40 relative + 2^-20 cell margin) and each k in it gets the exact
+// test, so neighbour sets stay bit-exact while the box corners outside the sphere
+// (about half of a box at physical h) are never visited.
+// the candidate planes [a, b] (brick-local) of column (li, lj); s = its dx^2 + dy^2.
+// The half-width sqrt(thr - s + 2^-49 thr) / pz is formed in fp32: its relative error
+// (< 2^-21) and that of kc (< 2^-24 of 512 planes) stay far inside the margin of
+// 2^-10 plane + 2^-18 relative, so [a, b] remains a superset of the passing planes.
+__device__ __forceinline__ bool column_range(const Grid3& g, const Rec3& R, int li, int lj,
+                                             const double* xt, const double* yt, double& s,
+                                             int& a, int& b) {
     double dx = R.x - xt[li];
     double dy = R.y - yt[lj];
+    s = dx * dx + dy * dy;
+    if (!(s < R.thr)) return false;  // s + dz * dz >= s >= thr for every k
+    float rz = __builtin_amdgcn_sqrtf((float)((R.thr - s) + R.thr * 0x1p-49)) * (float)g.ipz;
+    rz = rz * (1.0f + 0x1p-18f) + 0x1p-10f;
+    float fa = fmaxf(ceilf(R.kc - rz), (float)R.b.k0);
+    float fb = fminf(floorf(R.kc + rz), (float)R.b.k1);
+    if (!(fa <= fb)) return false;
+    a = (int)fa;
+    b = (int)fb;
+    return true;
+}
+
+template <int KID>
+__device__ __forceinline__ void voxel3(const Rec3& R, double s, int li, int lj, int lk,
+                                       const double* zt, double* acc) {
     double dz = R.z - zt[lk];
-    double r2 = dx * dx + dy * dy + dz * dz;
+    double r2 = s + dz * dz;
     if (r2 < R.thr) {
         float q = __builtin_amdgcn_sqrtf((float)r2) * R.hinv;
         float w = kernel_shape<KID>(q);
-        atomicAdd(&acc[(li * kBY + lj) * kBZ + lk], (double)(R.s * w));
+        atomicAdd(&acc[(li * kBY + lj) * kBZP + lk], (double)(R.s * w));
     }
+}
+
+template <int KID>
+__device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, int lj, int K0,
+                                        const double* xt, const double* yt, const double* zt,
+                                        double* acc) {
+    double s;
+    int a, b;
+    if (!column_range(g, R, li, lj, xt, yt, s, a, b)) return;
+    for (int lk = a; lk <= b; ++lk) voxel3<KID>(R, s, li, lj, lk, zt, acc);
 }
 
 template <int KID>
@@ -203,7 +255,7 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
                                                       double* __restrict__ slabs,
                                                       float* __restrict__ out, int accumulate) {
     extern __shared__ __attribute__((aligned(16))) double acc[];
-    double* xt = acc + kBrickVox;
+    double* xt = acc + kBrickLds;
     double* yt = xt + kBX;
     double* zt = yt + kBY;
     const Item it = items[blockIdx.x];
@@ -225,7 +277,7 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         }
         return;
     }
-    for (int v = threadIdx.x; v < kBrickVox; v += k3Block) acc[v] = 0.0;
+    for (int v = threadIdx.x; v < kBrickLds; v += k3Block) acc[v] = 0.0;
     if (threadIdx.x < kBX) xt[threadIdx.x] = g.x_min + (double)(I0 + (int)threadIdx.x) * g.px;
     else if (threadIdx.x < kBX + kBY)
         yt[threadIdx.x - kBX] = g.y_min + (double)(J0 + (int)threadIdx.x - kBX) * g.py;
@@ -262,16 +314,16 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
             R.thr = t * t;
             R.hinv = 1.0f / r0.w;
             R.s = (float)term_coef<KID>(r1.x, r0.w);
+            R.kc = (float)((R.z - g.z_min) * g.ipz - (double)K0);
         }
         r0 = n0;
         r1 = n1;
-        int bw = R.b.i1 - R.b.i0 + 1, bh = R.b.j1 - R.b.j0 + 1, bd = R.b.k1 - R.b.k0 + 1;
-        bool small = live && bw * bh * bd <= kSmallVox;
+        int bw = R.b.i1 - R.b.i0 + 1, bh = R.b.j1 - R.b.j0 + 1;
+        bool small = live && bw * bh <= g.lane_cols;
         if (small) {
             for (int li = R.b.i0; li <= R.b.i1; ++li)
                 for (int lj = R.b.j0; lj <= R.b.j1; ++lj)
-                    for (int lk = R.b.k0; lk <= R.b.k1; ++lk)
-                        pair3<KID>(R, li, lj, lk, xt, yt, zt, acc);
+                    column3<KID>(g, R, li, lj, K0, xt, yt, zt, acc);
         }
         unsigned long long big = __ballot(live && !small);
         while (big) {
@@ -284,36 +336,29 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
             Q.thr = __shfl(R.thr, l);
             Q.hinv = bcast(R.hinv, l);
             Q.s = bcast(R.s, l);
+            Q.kc = bcast(R.kc, l);
             Q.b.i0 = bcast(R.b.i0, l);
             Q.b.j0 = bcast(R.b.j0, l);
             Q.b.k0 = bcast(R.b.k0, l);
-            int qw = bcast(bw, l), qh = bcast(bh, l), qd = bcast(bd, l);
-            // Lanes walk the flattened box (k fastest) in steps of 64 with a mixed-radix
-            // increment: no division inside the loop.
-            int plane = qh * qd, vol = qw * plane;
-            int dk = 64 % qd, dj = (64 / qd) % qh, di = 64 / plane;
-            int ci = lane / plane, rr = lane - ci * plane;
-            int cj = rr / qd, ck = rr - cj * qd;
-            for (int v = lane; v < vol; v += 64) {
-                pair3<KID>(Q, Q.b.i0 + ci, Q.b.j0 + cj, Q.b.k0 + ck, xt, yt, zt, acc);
-                ck += dk;
-                if (ck >= qd) { ck -= qd; ++cj; }
-                cj += dj;
-                if (cj >= qh) { cj -= qh; ++ci; }
-                ci += di;
+            Q.b.k1 = bcast(R.b.k1, l);
+            int qw = bcast(bw, l), qh = bcast(bh, l);
+            // lanes take the box's (i, j) columns
+            for (int c = lane; c < qw * qh; c += 64) {
+                int ci = c / qh, cj = c - ci * qh;
+                column3<KID>(g, Q, Q.b.i0 + ci, Q.b.j0 + cj, K0, xt, yt, zt, acc);
             }
         }
     }
     __syncthreads();
     if (it.slab >= 0) {
         double* dst = slabs + (long long)it.slab * kBrickVox;
-        for (int v = threadIdx.x; v < kBrickVox; v += k3Block) dst[v] = acc[v];
+        for (int v = threadIdx.x; v < kBrickVox; v += k3Block) dst[v] = acc[lds_vox(v)];
         return;
     }
     for (int v = threadIdx.x; v < kBrickVox; v += k3Block) {
         long long o = out_index(v);
         if (o < 0) continue;
-        float val = (float)acc[v];
+        float val = (float)acc[lds_vox(v)];
         out[o] = accumulate ? out[o] + val : val;
     }
 }
@@ -402,6 +447,8 @@ static bool make_grid3(const double* ext, int nx, int ny, int nz, int k_lo, int 
     g.nbz = (g.nzl + kBZ - 1) / kBZ;
     long long nb = (long long)g.nbx * g.nby * g.nbz;
     g.nb = nb > kMaxBricks ? -1 : (int)nb;
+    g.lane_cols = kLaneCols;
+    if (const char* e = getenv("ASP_CUBE_LANE_COLS")) g.lane_cols = std::max(0, atoi(e));
     return true;
 }
 
@@ -529,7 +576,7 @@ static int project3d(const float* x, const float* y, const float* z, const float
         }
         {
             StageMark m(ws, kS3Deposit, st);
-            size_t lds = (size_t)kBrickVox * sizeof(double) + (kBX + kBY + kBZ) * sizeof(double);
+            size_t lds = (size_t)kBrickLds * sizeof(double) + (kBX + kBY + kBZ) * sizeof(double);
             auto kern = kid == 0 ? k3_deposit<0> : kid == 1 ? k3_deposit<1> : k3_deposit<2>;
             hipLaunchKernelGGL(kern, dim3(n_items), dim3(k3Block), lds, st, g,
                                (const float4*)ws.recs.p, (const Item*)ws.items.p,
