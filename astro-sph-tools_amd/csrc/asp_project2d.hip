@@ -44,7 +44,10 @@
 
 namespace asp {
 
-constexpr int kCountBlock = 512;  // count workgroup
+#ifndef ASP_COUNT_BLOCK
+#define ASP_COUNT_BLOCK 512
+#endif
+constexpr int kCountBlock = ASP_COUNT_BLOCK;  // count workgroup
 #ifndef ASP_SCATTER_BLOCK
 #define ASP_SCATTER_BLOCK 1024
 #endif
