@@ -34,6 +34,7 @@ enum Ctr {
 // ----------------------------------------------------------------------------------
 constexpr int kColscanWaves = 16;
 constexpr int kColscanBlock = 64 * kColscanWaves;
+constexpr int kColscanRows = 64;  // rows per wave held in registers (1024 blocks / 16 waves)
 static __global__ __launch_bounds__(kColscanBlock) void k_colscan(int* __restrict__ hist, int nblk,
                                                            int ntiles,
                                                            int* __restrict__ tile_total, int cb) {
@@ -46,22 +47,38 @@ static __global__ __launch_bounds__(kColscanBlock) void k_colscan(int* __restric
     int b0 = c0 + (int)((long long)cn * w / kColscanWaves);
     int b1 = c0 + (int)((long long)cn * (w + 1) / kColscanWaves);
     int s = 0;
+    // <= kColscanRows rows per wave (nblk <= 1024): one load of every row into registers,
+    // the exclusive prefix there, one store with the other waves' offset added
+    const bool regs = b1 - b0 <= kColscanRows;
+    int c[kColscanRows];
     if (t < ntiles) {
-        int b = b0;
-        for (; b + 8 <= b1; b += 8) {
-            int c[8];
+        if (regs) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) c[k] = hist[(long long)(b + k) * ntiles + t];
+            for (int k = 0; k < kColscanRows; ++k)
+                c[k] = b0 + k < b1 ? hist[(long long)(b0 + k) * ntiles + t] : 0;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                hist[(long long)(b + k) * ntiles + t] = s;
-                s += c[k];
+            for (int k = 0; k < kColscanRows; ++k) {
+                int x = c[k];
+                c[k] = s;
+                s += x;
             }
-        }
-        for (; b < b1; ++b) {
-            int c = hist[(long long)b * ntiles + t];
-            hist[(long long)b * ntiles + t] = s;
-            s += c;
+        } else {
+            int b = b0;
+            for (; b + 8 <= b1; b += 8) {
+                int cc[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) cc[k] = hist[(long long)(b + k) * ntiles + t];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    hist[(long long)(b + k) * ntiles + t] = s;
+                    s += cc[k];
+                }
+            }
+            for (; b < b1; ++b) {
+                int cc = hist[(long long)b * ntiles + t];
+                hist[(long long)b * ntiles + t] = s;
+                s += cc;
+            }
         }
     }
     part[w][lane] = s;
@@ -69,8 +86,13 @@ static __global__ __launch_bounds__(kColscanBlock) void k_colscan(int* __restric
     int off = 0;
     for (int k = 0; k < w; ++k) off += part[k][lane];
     if (t < ntiles) {
-        if (off)
+        if (regs) {
+#pragma unroll
+            for (int k = 0; k < kColscanRows; ++k)
+                if (b0 + k < b1) hist[(long long)(b0 + k) * ntiles + t] = c[k] + off;
+        } else if (off) {
             for (int b = b0; b < b1; ++b) hist[(long long)b * ntiles + t] += off;
+        }
         if (w == kColscanWaves - 1) tile_total[t] = off + s;
     }
 }
@@ -94,13 +116,32 @@ constexpr int kMinItemRecords = 2048;
 constexpr int kTargetItems1 = 4096;    // mode-1 items (a record there costs ~10-1000x)
 constexpr int kMinItemRecords1 = 256;
 
+// Inclusive scan of s[0 .. kScanThreads) in place: wave scans (DPP/permute shuffles), one
+// wave scans the 16 wave totals; three block barriers instead of 2 log2(1024).
 static __device__ __forceinline__ void block_scan_ll(long long* s, int tid) {
-    for (int o = 1; o < kScanThreads; o <<= 1) {
-        long long x = tid >= o ? s[tid - o] : 0;
-        __syncthreads();
-        s[tid] += x;
-        __syncthreads();
+    __shared__ long long part[kScanThreads / 64];
+    const int lane = tid & 63, w = tid >> 6;
+    long long x = s[tid];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        long long y = __shfl_up(x, o);
+        if (lane >= o) x += y;
     }
+    if (lane == 63) part[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        long long q = lane < kScanThreads / 64 ? part[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < kScanThreads / 64; o <<= 1) {
+            long long y = __shfl_up(q, o);
+            if (lane >= o) q += y;
+        }
+        if (lane < kScanThreads / 64) part[lane] = q;
+    }
+    __syncthreads();
+    if (w > 0) x += part[w - 1];
+    s[tid] = x;
+    __syncthreads();
 }
 
 // items of one tile: regular ones of ch records, large ones of chl records
