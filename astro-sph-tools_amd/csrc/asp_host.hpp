@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -140,7 +142,15 @@ inline int ensure(Buf& b, size_t bytes) {
         b.cap = 0;
     }
     size_t want = bytes + bytes / 4;
-    hipError_t e = hipMalloc(&b.p, want);
+    hipError_t e = hipErrorOutOfMemory;
+    if (want >= (size_t(1) << 28) && getenv("ASP_CONTIG") && atoi(getenv("ASP_CONTIG")))
+        e = hipExtMallocWithFlags(&b.p, want, hipDeviceMallocContiguous);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        e = hipMalloc(&b.p, want);
+    } else if (getenv("ASP_DEBUG_ALLOC")) {
+        fprintf(stderr, "[asp] contiguous ");
+    }
     if (e != hipSuccess) {
         e = hipMalloc(&b.p, bytes);
         want = bytes;
@@ -151,6 +161,8 @@ inline int ensure(Buf& b, size_t bytes) {
                                        hipGetErrorString(e));
     }
     b.cap = want;
+    if (want >= (size_t(1) << 28) && getenv("ASP_DEBUG_ALLOC"))
+        fprintf(stderr, "[asp] hipMalloc %zu B at %p\n", want, b.p);
     return ASP_OK;
 }
 
