@@ -45,7 +45,7 @@
 namespace asp {
 
 #ifndef ASP_COUNT_BLOCK
-#define ASP_COUNT_BLOCK 512
+#define ASP_COUNT_BLOCK 256
 #endif
 constexpr int kCountBlock = ASP_COUNT_BLOCK;  // count workgroup
 #ifndef ASP_SCATTER_BLOCK
@@ -79,7 +79,7 @@ __device__ __forceinline__ int tile_column(const Grid& g, const Box& b, bool may
 }
 constexpr int kUnroll = 2;        // particles in flight per thread in scatter
 #ifndef ASP_COUNT_UNROLL
-#define ASP_COUNT_UNROLL 4
+#define ASP_COUNT_UNROLL 8
 #endif
 constexpr int kCountUnroll = ASP_COUNT_UNROLL;  // ... and in count
 // Particles per loop iteration of a count / scatter workgroup (a "batch").
