@@ -561,12 +561,20 @@ def main():
             traffic_src = pm[key].get("source")
     except (OSError, ValueError, KeyError):
         pass
+    # BASELINE.json configs: [1] 10^7 -> 2048^2 surface density, [2] 10^8 -> 4096^2
+    # weighted map (the metric's), [3] the same on 8 GPUs; anything else is a custom size
+    if args.n == 100_000_000 and G == 4096:
+        cfg_tag = "cfg4" if world > 1 else "cfg3"
+    elif args.n == 10_000_000 and G == 2048:
+        cfg_tag = "cfg2"
+    else:
+        cfg_tag = "custom"
     res = {
         "metric": METRIC, "value": round(mpix, 3), "unit": "Mpixels/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic Plummer sphere (a=1, M=1, seed 0) generated in HBM",
-        "config": {"workload": f"cfg3: {args.n:.0e} particles -> {G}^2 "
+        "config": {"workload": f"{cfg_tag}: {args.n:.0e} particles -> {G}^2 "
                                f"{'mass-weighted temperature' if ratio else 'surface density'} "
                                f"map, {args.kernel}, {args.h_law}-scale h, fp32"
                                + (f", Z-slab x{world} + RCCL {args.op}" if world > 1 else ""),
