@@ -1043,7 +1043,69 @@ __device__ __forceinline__ void deferred(const Grid& g, const float4* __restrict
 // K4: deposit one work item (a run of records of one tile) into LDS, then write the
 // tile (single-item tiles) or its int64 partial slab (split tiles).
 // ----------------------------------------------------------------------------------
-template <int KID, int NOUT, int ACC>
+// Gathered large records (GATHER): a batch's large-box records go to an LDS list (SoA,
+// one batch = kDepThreads records at most); after a block barrier every thread tests the
+// list against the 8 pixels it owns (row = tid / 8, columns 8 (tid % 8) ..), with the
+// same fp32 decision + fp64 band fallback as decide(), and keeps register sums, added to
+// its own LDS words once per batch: no per-pair atomics.  fp64 accumulation only.
+constexpr int kGFields = 10;  // u v h lo hi hinv s0 s1 box(x0|x1<<8|y0<<16|y1<<24, tile-local)
+constexpr size_t kGatherLds = (size_t)kGFields * kDepThreads * 4 + 2 * sizeof(int);
+
+template <int KID, int NOUT>
+__device__ __forceinline__ void gather_list(const Grid& g, const float* gl, int nl, int X0,
+                                            int Y0, int TW, int TH, const float* xt,
+                                            const float* yt, unsigned long long* acc0,
+                                            unsigned long long* acc1) {
+    const int row = threadIdx.x >> 3, col0 = (threadIdx.x & 7) * 8;
+    if (row >= TW || col0 >= TH) return;
+    const float X = xt[row];
+    float Yv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Yv[j] = yt[min(col0 + j, kTile - 1)];
+    double s0[8], s1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.0;
+    const float *gu = gl, *gv = gl + kDepThreads, *gh = gl + 2 * kDepThreads,
+                *glo = gl + 3 * kDepThreads, *ghi = gl + 4 * kDepThreads,
+                *ghv = gl + 5 * kDepThreads, *gs0 = gl + 6 * kDepThreads,
+                *gs1 = gl + 7 * kDepThreads;
+    const unsigned* gb = (const unsigned*)(gl + 8 * kDepThreads);
+    for (int e = 0; e < nl; ++e) {
+        unsigned bx = gb[e];
+        int x0 = bx & 255, x1 = (bx >> 8) & 255, y0 = (bx >> 16) & 255, y1 = bx >> 24;
+        if (row < x0 || row > x1 || col0 + 7 < y0 || col0 > y1) continue;
+        const float u = gu[e], v = gv[e], lo = glo[e], hi = ghi[e];
+        const float dx = u - X;
+        const float dx2 = dx * dx;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = col0 + j;
+            if (c < y0 || c > y1) continue;
+            float dy = v - Yv[j];
+            float r2 = dx2 + dy * dy;
+            bool in = r2 < lo;
+            if (r2 >= lo && r2 <= hi) in = exact_pair(g, u, v, gh[e], X0 + row, Y0 + c);
+            if (in) {
+                float w = kernel_shape<KID>(__builtin_amdgcn_sqrtf(r2) * ghv[e]);
+                s0[j] += (double)(gs0[e] * w);
+                if constexpr (NOUT == 2) s1[j] += (double)(gs1[e] * w);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (col0 + j >= TH) continue;
+        const int k = row * kTile + col0 + j;
+        double* a0 = (double*)&acc0[k];
+        *a0 += s0[j];
+        if constexpr (NOUT == 2) {
+            double* a1 = (double*)&acc1[k];
+            *a1 += s1[j];
+        }
+    }
+}
+
+template <int KID, int NOUT, int ACC, bool GATHER = false>
 __global__ __launch_bounds__(kDepThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_deposit(
     Grid g, const float4* __restrict__ recs, const Item* __restrict__ items,
     const int2* __restrict__ tile_k, unsigned long long* __restrict__ slabs,
@@ -1053,6 +1115,8 @@ __global__ __launch_bounds__(kDepThreads) __attribute__((amdgpu_waves_per_eu(4))
     unsigned long long* acc1 = acc + kTilePix;
     float* xt = (float*)(acc + NOUT * kTilePix);
     float* yt = xt + kTile;
+    float* gl = yt + kTile;                          // GATHER: the list (SoA)
+    int* gcnt = (int*)(gl + kGFields * kDepThreads);  // GATHER: two list counters
     const Item it = items[blockIdx.x];
     if (it.mode != 0) return;  // K4b's
     int tx = it.tile / g.nty, ty = it.tile - (it.tile / g.nty) * g.nty;
@@ -1085,6 +1149,7 @@ __global__ __launch_bounds__(kDepThreads) __attribute__((amdgpu_waves_per_eu(4))
         return;
     }
     const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
+    if (GATHER && threadIdx.x == 0) gcnt[0] = gcnt[1] = 0;  // the prologue's barrier orders it
     tile_prologue<NOUT, kDepThreads>(g, X0, Y0, acc, xt, yt);
     {
         __shared__ int defer_lds[kDepThreads / 64][kDeferCap];
@@ -1154,12 +1219,37 @@ __global__ __launch_bounds__(kDepThreads) __attribute__((amdgpu_waves_per_eu(4))
                     }
                 }
             }
-            unsigned long long big = __ballot(live && !small);
-            while (big) {
-                int l = __builtin_ctzll(big);
-                big &= big - 1;
-                Prep Q = bcast_prep(P, l);
-                sweep<KID, NOUT, ACC>(g, Q, X0, Y0, xt, yt, acc0, acc1, lane);
+            if constexpr (GATHER) {
+                // list counter of this batch: gcnt[parity]; the other one is reset here for
+                // the next batch (nobody touches it before the barrier that ends this one)
+                const int par = (base / kDepThreads) & 1;
+                if (live && !small) {
+                    int e = atomicAdd(&gcnt[par], 1);
+                    gl[e] = P.u;
+                    gl[kDepThreads + e] = P.v;
+                    gl[2 * kDepThreads + e] = P.h;
+                    gl[3 * kDepThreads + e] = P.lo;
+                    gl[4 * kDepThreads + e] = P.hi;
+                    gl[5 * kDepThreads + e] = P.hinv;
+                    gl[6 * kDepThreads + e] = P.s0;
+                    gl[7 * kDepThreads + e] = P.s1;
+                    gl[8 * kDepThreads + e] = __uint_as_float(
+                        (unsigned)(P.b.x0 - X0) | ((unsigned)(P.b.x1 - X0) << 8) |
+                        ((unsigned)(P.b.y0 - Y0) << 16) | ((unsigned)(P.b.y1 - Y0) << 24));
+                }
+                __syncthreads();
+                const int nl = gcnt[par];
+                if (threadIdx.x == 0) gcnt[par ^ 1] = 0;
+                if (nl) gather_list<KID, NOUT>(g, gl, nl, X0, Y0, TW, TH, xt, yt, acc0, acc1);
+                __syncthreads();
+            } else {
+                unsigned long long big = __ballot(live && !small);
+                while (big) {
+                    int l = __builtin_ctzll(big);
+                    big &= big - 1;
+                    Prep Q = bcast_prep(P, l);
+                    sweep<KID, NOUT, ACC>(g, Q, X0, Y0, xt, yt, acc0, acc1, lane);
+                }
             }
         }
         if (ndef > 0)
@@ -1573,9 +1663,16 @@ static int run_tail(const Grid& g, Workspace& ws, const Plan& pl, const float* u
         {
             StageMark m(ws, kSDeposit, sd);
             size_t lds = (size_t)NOUT * kTilePix * 8 + 2 * kTile * 4;
-            hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(ck.n_items), dim3(kDepThreads), lds, sd, g,
-                               (const float4*)recs, items, (const int2*)ws.tile_k.p, slabs, o0, o1,
-                               dflags);
+            // ASP_GATHER=1: gathered large records (fp64 accumulation)
+            const bool gather = getenv("ASP_GATHER") && atoi(getenv("ASP_GATHER")) == 1;
+            if (ACC == kAccF64 && gather)
+                hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC, true>), dim3(ck.n_items), dim3(kDepThreads),
+                                   lds + kGatherLds, sd, g, (const float4*)recs, items,
+                                   (const int2*)ws.tile_k.p, slabs, o0, o1, dflags);
+            else
+                hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(ck.n_items), dim3(kDepThreads), lds, sd, g,
+                                   (const float4*)recs, items, (const int2*)ws.tile_k.p, slabs, o0, o1,
+                                   dflags);
             ASP_LAUNCHED();
             m.done();
         }
