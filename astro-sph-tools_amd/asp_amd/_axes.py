@@ -46,3 +46,24 @@ def axis_index(projection_axis) -> int:
     except (TypeError, ValueError):
         return 2
     return i if i in (0, 1) else 2
+
+
+def reference_axes(projection_axis):
+    """(pixel axis, cull axis) exactly as the reference derives them from ANY value.
+
+    The cull (_projector.py:38-46) compares ``projection_axis == CoordinateAxes.X`` / ``.Y``
+    -- true only for the enum members -- and otherwise culls on the Z columns; the pixel
+    function (_projector.py:63, _pixel_calculations.pyx:20-28) tests
+    ``str(projection_axis).encode()`` against ``b'x'`` / ``b'y'``.  Enum members (this
+    package's or the reference's own class) give the same axis twice; an int always means
+    Z; the str "x" culls on (x, y) but tests distances on (y, z).
+    """
+    from enum import Enum
+    name = getattr(projection_axis, "name", None)
+    cull = "XYZ".index(name) if isinstance(projection_axis, Enum) and name in ("X", "Y") else 2
+    try:
+        tag = str(projection_axis).encode()
+    except Exception:  # noqa: BLE001 -- the reference would raise here as well
+        raise TypeError(f"projection_axis {projection_axis!r} has no str()") from None
+    pixel = {b"x": 0, b"y": 1}.get(tag, 2)
+    return pixel, cull

@@ -17,8 +17,8 @@ def kernel_id(kernel) -> int:
         return kernel
     if isinstance(kernel, str):
         return _KERNEL_NAMES[kernel]
-    from .tools.projections._kernels import kernel_id_of
-    return kernel_id_of(kernel)
+    from .tools.projections._kernels import native_kernel_id
+    return native_kernel_id(kernel)
 
 
 def _check(t, name, n=None, device=None):
@@ -72,6 +72,89 @@ def project2d(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
         P(u), P(v), P(h), P(a0), P(a1), n, x_min, x_max, y_min, y_max, nx, ny, int(chunk_size),
         kernel_id(kernel), flags, P(out0), P(out1), dev.index or 0, stream))
     return out0, (out1 if a1 is not None else None)
+
+
+def _f64_arg(a, name, n, shape_tail=()):
+    """A float64 input of create_image: a contiguous host array (NumPy / unyt) or a
+    float64 device tensor; returns (object keeping it alive, ctypes pointer, on_device)."""
+    import numpy as np
+    if hasattr(a, "is_cuda") and a.is_cuda:
+        import torch
+        if a.dtype != torch.float64:
+            raise ValueError(f"{name} must be float64")
+        a = a.contiguous()
+        if tuple(a.shape) != (n,) + shape_tail:
+            raise ValueError(f"{name} has shape {tuple(a.shape)}, expected {(n,) + shape_tail}")
+        return a, _lib.ptr(a, _lib._d), True
+    x = np.ascontiguousarray(np.asarray(a), dtype=np.float64)
+    if shape_tail == () and x.ndim != 1:
+        x = x.reshape(-1)
+    if x.shape != (n,) + shape_tail:
+        raise ValueError(f"{name} has shape {x.shape}, expected {(n,) + shape_tail}")
+    return x, _lib.ptr(x, _lib._d), False
+
+
+def project2d_f64(positions, h, a0, a1=None, *, projection_axis=2, image_size, extent,
+                  chunk_size: int = 64, kernel="cubic", ratio: bool = False,
+                  accumulate: bool = False, out0=None, out1=None, device: int = 0,
+                  stream=None, deterministic: bool = False):
+    """asp_project2d_f64: the reader's float64 arrays (positions (N, 3), h, a0[, a1]) --
+    host NumPy arrays or float64 device tensors -- projected with the reference's fp64
+    decisions on those values.  ``projection_axis``: an axis (int 0/1/2, enum, "x") or a
+    (pixel axis, cull axis) pair (asp_amd._axes.reference_axes).  Returns float32 maps: device tensors for device inputs
+    (or the given ``out0``/``out1``), NumPy arrays for host inputs."""
+    import numpy as np
+    import torch
+    from ._axes import axis_index
+    if isinstance(projection_axis, tuple):  # (pixel axis, cull axis): reference_axes()
+        axis = int(projection_axis[0])
+        if int(projection_axis[1]) != axis:
+            axis |= (int(projection_axis[1]) + 1) << 4  # ASP_AXIS_CULL
+    else:
+        axis = axis_index(projection_axis)
+    n = int(positions.shape[0])
+    keep = []
+    pos, ppos, on_dev = _f64_arg(positions, "positions", n, (3,))
+    keep.append(pos)
+    ptrs = [ppos]
+    for arr, name in ((h, "smoothing_lengths"), (a0, "a0"), (a1, "a1")):
+        if arr is None:
+            ptrs.append(None)
+            continue
+        x, px, d = _f64_arg(arr, name, n)
+        if d != on_dev:
+            raise ValueError("positions and fields must all be host arrays or all device tensors")
+        keep.append(x)
+        ptrs.append(px)
+    nx, ny = int(image_size[0]), int(image_size[1])
+    nout = 1 if a1 is None else 2
+    flags = (_lib.ASP_F_RATIO if ratio else 0) | (_lib.ASP_F_ACCUMULATE if accumulate else 0) | \
+        (_lib.ASP_F_DETERMINISTIC if deterministic else 0)
+    if on_dev:
+        dev = pos.device
+        device = dev.index or 0
+        flags |= _lib.ASP_F_DEVICE_PTRS
+        if out0 is None:
+            out0 = torch.empty((nx, ny), dtype=torch.float32, device=dev)
+        if nout == 2 and out1 is None:
+            out1 = torch.empty((nx, ny), dtype=torch.float32, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+    else:
+        _lib.require_gpu(device)
+        if out0 is None:
+            out0 = np.zeros((nx, ny), dtype=np.float32)
+        if nout == 2 and out1 is None:
+            out1 = np.zeros((nx, ny), dtype=np.float32)
+    for t in (out0, out1):
+        if t is not None and (t.dtype not in (np.float32, torch.float32) or int(np.prod(t.shape)) != nx * ny):
+            raise ValueError("outputs must be float32 (nx, ny) arrays")
+    x_min, x_max, y_min, y_max = (float(np.asarray(e)) for e in extent)
+    _lib.check(_lib.lib().asp_project2d_f64(
+        ptrs[0], ptrs[1], ptrs[2], ptrs[3], n, axis, x_min, x_max, y_min, y_max, nx, ny,
+        int(chunk_size), kernel_id(kernel), flags, _lib.ptr(out0), _lib.ptr(out1),
+        int(device), stream))
+    return out0, (out1 if nout == 2 else None)
 
 
 def project3d(x, y, z, h, a, *, cube_size, extent, kernel="cubic", planes=None,

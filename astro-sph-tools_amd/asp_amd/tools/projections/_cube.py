@@ -20,7 +20,7 @@ from __future__ import annotations
 import numpy as np
 
 from ... import _lib
-from ._kernels import kernel_id_of, quartic_spline_kernel
+from ._kernels import native_kernel_id, quartic_spline_kernel
 
 
 def create_cube(positions: np.ndarray, smoothing_lengths: np.ndarray,
@@ -38,7 +38,7 @@ def create_cube(positions: np.ndarray, smoothing_lengths: np.ndarray,
     if h.shape[0] != n or A.shape[0] != n:
         raise ValueError(f"positions ({n}), smoothing_lengths ({h.shape[0]}) and "
                          f"particle_properties ({A.shape[0]}) differ in length")
-    kid = kernel_id_of(kernel_func)
+    kid = native_kernel_id(kernel_func)
     nx, ny, nz = (int(c) for c in cube_size)
     k_lo, k_hi = (0, nz) if planes is None else (int(planes[0]), int(planes[1]))
     if min(nx, ny, nz) <= 0 or k_hi <= k_lo:

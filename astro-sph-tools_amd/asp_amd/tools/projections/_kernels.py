@@ -6,8 +6,9 @@ array, evaluated ON THE GPU (asp_kernel_eval).  Despite its name the reference k
 the M4 cubic spline with support 2h and 3-D normalisation 1/(pi h^3); that is kept.
 
 The kernel objects also carry the C-ABI kernel id, which is how ``create_image``
-recognises them and runs the whole projection natively.  Arbitrary Python callables
-cannot run on the device; ``create_image`` rejects them (no silent CPU path).
+recognises them and runs the whole projection natively.  Any other callable (the
+reference's own compiled kernel included) goes through the plugin path: neighbour pairs
+from the device, the callable evaluated on the host (_plugin.py).
 """
 from __future__ import annotations
 
@@ -71,14 +72,22 @@ indicator_kernel = SPHKernel(
 KERNELS = {k.kernel_id: k for k in (quartic_spline_kernel, wendland_c2_kernel, indicator_kernel)}
 
 
-def kernel_id_of(kernel_func) -> int:
+def kernel_id_of(kernel_func):
+    """The C-ABI kernel id of one of this package's kernels, or None for any other
+    callable (it then runs through the plugin path, _plugin.project_callable)."""
     kid = getattr(kernel_func, "kernel_id", None)
     if isinstance(kernel_func, SPHKernel) and kid in KERNELS:
         return kid
-    name = getattr(kernel_func, "__name__", "")
-    # the reference's own compiled kernel object, passed through unchanged
-    if name == "quartic_spline_kernel":
-        return _lib.ASP_KERNEL_CUBIC_SPLINE
-    raise TypeError(
-        f"kernel_func {kernel_func!r} cannot run on the GPU; use quartic_spline_kernel, "
-        "wendland_c2_kernel or indicator_kernel from asp_amd.tools.projections")
+    if not callable(kernel_func):
+        raise TypeError(f"kernel_func {kernel_func!r} is not callable")
+    return None
+
+
+def native_kernel_id(kernel_func) -> int:
+    """kernel_id_of for the paths with no plugin (device arrays, cubes, periodic maps)."""
+    kid = kernel_id_of(kernel_func)
+    if kid is None:
+        raise TypeError(f"kernel_func {kernel_func!r} cannot run on the GPU here; use "
+                        "quartic_spline_kernel, wendland_c2_kernel or indicator_kernel "
+                        "(create_image accepts any callable)")
+    return kid

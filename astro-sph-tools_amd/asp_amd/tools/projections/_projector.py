@@ -9,11 +9,12 @@ corner ``(x_min + xi*dx, y_min + yi*dy)`` with ``dy = (y_max - y_min)/Nx`` (refe
 quirk S2); the value is the sum of ``A_p W(r_p, h_p)`` over particles passing the
 reference's cull of the ``chunk_size`` tile holding the pixel and ``r_p^2 < (2h_p)^2``.
 
-Differences, all documented in DESIGN.md §6: values accumulate in float32 on the GPU
-(upcast on return; neighbour sets are decided with the reference's fp64 arithmetic
-and are identical); ``kernel_func`` must be one of this package's kernels (Python
-callables cannot run on the device -> TypeError); ``x_max > x_min`` and
-``y_max > y_min`` are required (ValueError); non-finite particle inputs are excluded.
+Differences, all documented in DESIGN.md §6: values are sums of float32 terms on the GPU
+(upcast on return); neighbour sets are decided with the reference's fp64 arithmetic on
+the caller's own fp64 values and are identical; an arbitrary ``kernel_func`` is evaluated
+on the host over device-produced neighbour pairs, in batches (it must be element-wise);
+``x_max > x_min`` and ``y_max > y_min`` are required (ValueError); non-finite particle
+inputs are excluded.
 """
 from __future__ import annotations
 
@@ -22,7 +23,8 @@ import numbers
 import numpy as np
 
 from ... import _lib
-from ._kernels import kernel_id_of, quartic_spline_kernel
+from ..._axes import reference_axes
+from ._kernels import kernel_id_of, native_kernel_id, quartic_spline_kernel
 
 
 def _lengths(positions, smoothing_lengths, *fields):
@@ -47,9 +49,9 @@ def _check_chunk_size(chunk_size):
 
 def _run(positions, smoothing_lengths, props, projection_axis, image_size, chunk_size,
          extent, kernel_id, ratio, deterministic, device):
-    """Stage the reader's fp64 arrays on the device (asp_stage_particles: axis selection
-    and fp32 conversion in HBM, the host-side step of _projector.py:38-51) and project
-    them (asp_project2d).  Returns the float32 host map(s)."""
+    """The reader's fp64 arrays straight to asp_project2d_f64 (staging in HBM -- the
+    host-side step of _projector.py:38-51 -- and the projection with the reference's
+    fp64 decisions on the original values).  Returns the float32 host map(s)."""
     nx, ny = int(image_size[0]), int(image_size[1])
     out0 = np.zeros((nx, ny), dtype=np.float32)
     out1 = None if len(props) < 2 else np.zeros_like(out0)
@@ -57,18 +59,29 @@ def _run(positions, smoothing_lengths, props, projection_axis, image_size, chunk
         # empty image, or range(0, N, negative) -> no tiles -> all zeros (reference)
         return out0, out1
     _lib.require_gpu(device)
-    import torch
+    from ...device import project2d_f64
+    pos = np.asarray(positions)
+    if pos.ndim != 2 or pos.shape[1] != 3:
+        raise ValueError(f"positions must have shape (N, 3), got {pos.shape}")
+    return project2d_f64(pos, smoothing_lengths, props[0], props[1] if len(props) > 1 else None,
+                         projection_axis=reference_axes(projection_axis), image_size=(nx, ny),
+                         extent=tuple(float(np.asarray(e)) for e in extent),
+                         chunk_size=chunk_size, kernel=kernel_id, ratio=ratio,
+                         deterministic=deterministic, device=device, out0=out0, out1=out1)
 
-    from ...device import project2d
-    from ...stage import stage_particles
-    u, v, h, pp = stage_particles(positions, smoothing_lengths, *props,
-                                  projection_axis=projection_axis, device=device)
-    o0, o1 = project2d(u, v, h, pp[0], pp[1] if len(pp) > 1 else None, image_size=(nx, ny),
-                       extent=tuple(float(np.asarray(e)) for e in extent),
-                       chunk_size=chunk_size, kernel=kernel_id, ratio=ratio,
-                       deterministic=deterministic)
-    torch.cuda.synchronize(u.device)
-    return o0.cpu().numpy(), (o1.cpu().numpy() if o1 is not None else None)
+
+def _run_callable(positions, smoothing_lengths, props, projection_axis, image_size, chunk_size,
+                  extent, kernel_func, device):
+    nx, ny = int(image_size[0]), int(image_size[1])
+    if nx <= 0 or ny <= 0 or chunk_size < 0:
+        return [np.zeros((max(nx, 0), max(ny, 0))) for _ in props]
+    _lib.require_gpu(device)
+    from ._plugin import project_callable
+    pos = np.asarray(positions)
+    if pos.ndim != 2 or pos.shape[1] != 3:
+        raise ValueError(f"positions must have shape (N, 3), got {pos.shape}")
+    return project_callable(pos, smoothing_lengths, props, reference_axes(projection_axis),
+                            (nx, ny), chunk_size, extent, kernel_func, device=device)
 
 
 def create_image(positions: np.ndarray, smoothing_lengths: np.ndarray,
@@ -85,6 +98,11 @@ def create_image(positions: np.ndarray, smoothing_lengths: np.ndarray,
     cs = _check_chunk_size(chunk_size)
     kid = kernel_id_of(kernel_func)
     _lengths(positions, smoothing_lengths, particle_properties)
+    if kid is None:  # an arbitrary Python kernel: the plugin path (_plugin.py)
+        img, = _run_callable(positions, smoothing_lengths, [particle_properties],
+                             projection_axis, image_size, cs, (x_min, x_max, y_min, y_max),
+                             kernel_func, device)
+        return img.astype(dtype, copy=False)
     img, _ = _run(positions, smoothing_lengths, [particle_properties], projection_axis,
                   image_size, cs, (x_min, x_max, y_min, y_max), kid, False, deterministic,
                   device)
@@ -112,6 +130,14 @@ def create_weighted_image(positions, smoothing_lengths, weights, values, image_s
     if vals.shape[0] != w.shape[0]:
         raise ValueError("values and positions differ in length")
     ext = (x_min, x_max, y_min, y_max)
+    if kid is None:  # an arbitrary Python kernel: the plugin path (_plugin.py)
+        s0, s1 = _run_callable(positions, smoothing_lengths, [w * vals, w], projection_axis,
+                               image_size, cs, ext, kernel_func, device)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ratio = np.where(s1 != 0, s0 / s1, 0.0)
+        if return_components:
+            return ratio.astype(dtype, copy=False), s0.astype(dtype), s1.astype(dtype)
+        return ratio.astype(dtype, copy=False)
     if return_components:
         s0, s1 = _run(positions, smoothing_lengths, [w * vals, w], projection_axis, image_size,
                       cs, ext, kid, False, deterministic, device)
@@ -143,7 +169,7 @@ def create_periodic_image(positions, smoothing_lengths, particle_properties, ima
     from ...device import project2d
     from ...stage import stage_particles
     cs = _check_chunk_size(chunk_size)
-    kid = kernel_id_of(kernel_func)
+    kid = native_kernel_id(kernel_func)
     L = float(box_width)
     nx, ny = int(image_size[0]), int(image_size[1])
     if nx <= 0 or ny <= 0 or cs < 0:

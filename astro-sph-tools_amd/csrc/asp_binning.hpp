@@ -22,6 +22,7 @@ enum Ctr {
     cMerges = 6,    // split tiles (K2b)
     cWideMax0 = 7,  // max |c0| over wide particles, fp32 bits (K3)
     cWideMax1 = 8,  // max |c1| over wide particles, fp32 bits (K3)
+    cLarge = 9,     // records in the large stream (K2b)
     cNum = 16
 };
 
@@ -102,10 +103,10 @@ static __global__ __launch_bounds__(kColscanBlock) void k_colscan(int* __restric
 // adjacent tiles' records are adjacent in HBM), the deposit work list (also Morton
 // order: every tile gets >= 1 item, empty tiles a zero item) and the merge list.
 //
-// nstream = 2 (2-D map): column t + ntiles of tile_total holds tile t's NON-SMALL records
-// (clipped box wider than 4 x 4 pixels), stored right after its small-record run and
-// handed out in items of their own (Item::mode = 1, row-band deposit), chunked
-// independently: each stream aims at its own item count.
+// nstream = 2 (2-D map): column t + ntiles of tile_total holds tile t's LARGE records
+// (clipped box >= gather_min pixels on both axes), stored right after its small/mid-size
+// run and handed out in items of their own (Item::mode = 1, the gathered deposit K4g),
+// chunked independently: each stream aims at its own item count.
 // ----------------------------------------------------------------------------------
 constexpr int kScanThreads = 1024;
 #ifndef ASP_TARGET_ITEMS
@@ -257,6 +258,7 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
         ctr[cChunk] = ch;
         ctr[cSlabs] = (int)s_slab[kScanThreads - 1];
         ctr[cMerges] = (int)s_merge[kScanThreads - 1];
+        ctr[cLarge] = (int)min(total1, (long long)0x7fffffff);
     }
 }
 

@@ -9,8 +9,10 @@
 // Neighbour membership is decided EXACTLY as the reference decides it in fp64, at fp32
 // cost: the fp32 test r2_32 < thr_32 is trusted whenever |r2_32 - thr_32| exceeds a
 // rigorous per-record error band; pairs inside the band (~0.1 % near the 2h edge) are
-// re-decided by the reference's own fp64 arithmetic, including the chunk cull.  See
-// DESIGN.md §3 for the bound.
+// re-decided by the reference's own fp64 arithmetic, including the chunk cull.  The band
+// also covers the rounding of fp64 inputs to the fp32 working copies, so when the caller
+// hands over its fp64 arrays (Src64, asp_project2d_f64) the re-decision reads them and
+// the neighbour sets are the reference's on the fp64 inputs themselves.  DESIGN.md §3.
 //
 // Accumulation.  LDS fp32 atomics run ~8x slower than fp64 or integer
 // ones on gfx950 (tools/microbench_lds.hip), so tiles accumulate either
@@ -27,13 +29,12 @@
 namespace asp {
 
 constexpr int kBlock = 256;        // threads per workgroup for streaming kernels
-constexpr int kDepBlock = 512;     // deposit workgroup (8 waves; 2 per CU at 64 KiB LDS)
+constexpr int kDepBlock = 512;     // deposit workgroup (8 waves; 2 per CU)
 constexpr int kTile = 64;          // GPU tile edge in pixels
 constexpr int kTileShift = 6;
-#ifndef ASP_WIDE_TILES
-#define ASP_WIDE_TILES 256
-#endif
-constexpr int kWideTiles = ASP_WIDE_TILES;  // particles overlapping more tiles take the wide path
+constexpr int kRow = kTile + 1;    // LDS tile row stride in words (one pad word per row)
+constexpr int kTileWords = kTile * kRow;  // LDS words of one map's tile
+constexpr int kWideTilesDefault = 256;  // particles overlapping more tiles take the wide path
 constexpr int kScaleBits = 61;     // per-tile bound n_t * max|c| maps to <= 2^61
 constexpr int kAccF64 = 0;         // LDS fp64 accumulation
 constexpr int kAccFix = 1;         // LDS int64 fixed point (deterministic)
@@ -45,14 +46,32 @@ struct Grid {
     double psy_cull;  // (y_max - y_min) / ny                        _projector.py:35
     float xminf, yminf;   // fp32 copies for the candidate-box estimate
     float ipsx, ipsy;     // fp32 reciprocal pitches (pixel pitches)
-    float mg;         // bound on |corner coordinate| over the grid (error band)
+    float mg;         // bound on |corner coordinate| in the frame of any decision (band)
     int nx, ny, cs;
     int ncx, ncy;     // reference chunks per axis
     int ntx, nty, ntiles;  // GPU tiles
     int nonsquare;    // nx != ny: the y chunk cull is not implied by the r2 test
-    int band_cols;    // records spanning >= this many tile columns: row-band deposit
-    int nstream;      // 2: second record run per tile for them (histogram columns x 2)
+    int mixed;        // the cull reads other position columns than the pixel test (Src64)
     int wide_tiles;   // particles over more tiles than this take the wide path (K6)
+    int gather_min;   // records with clipped boxes >= this on both axes are gathered (K4)
+};
+
+// The caller's particle arrays, resident in HBM, read by particle index where the exact
+// values matter (fp64 re-decisions, tile-local coordinates): the fp64 arrays
+// (asp_project2d_f64: positions rows of `stride` doubles, u64 / v64 the columns of the
+// pixel test, cu64 / cv64 those of the chunk cull -- the same unless the reference's axis
+// spelling makes them differ, Grid::mixed; h64 contiguous), or, with u64 == nullptr,
+// the fp32 inputs u32 / v32 / h32 themselves (asp_project2d).
+struct Src64 {
+    const double* u64;
+    const double* v64;
+    const double* cu64;
+    const double* cv64;
+    const double* h64;
+    long long stride;
+    const float* u32;
+    const float* v32;
+    const float* h32;
 };
 
 struct Box {
@@ -61,13 +80,14 @@ struct Box {
 
 // Per-record state for the pair loop.
 struct Prep {
-    float u, v, h;
+    float u, v, h;  // u, v: tile-local in the deposits (corner tables in the same frame)
     float lo;    // fp32 r2 < lo: inside for sure;  lo <= r2 <= hi: decide in fp64;
     float hi;    // r2 > hi: outside  (lo, hi = (2h)^2 -/+ error band; +-inf: always fp64)
     float hinv;  // 1/h
     float s0, s1;  // a * norm(h) (kAccF64) or a * norm(h) * 2^k_tile (kAccFix)
     float thr;   // (2h)^2 in fp32
     float band;  // |r2 - thr| <= band: the fp32 decision is not trusted (inf: never)
+    int p;       // particle index (the fp64 re-decision reads the caller's arrays there)
     Box b;
 };
 
@@ -75,8 +95,8 @@ struct Item {       // one deposit work item: a run of records of one GPU tile
     long long start;
     int tile;
     int count;      // 0: empty tile (write zeros)
-    int slab;       // -1: the tile's only item (writes the map); >= 0: int64 partial slab
-    int mode;       // 0: regular records; 1: large records (2-D map, gathered)
+    int slab;       // -1: the tile's only item (writes the map); >= 0: partial slab
+    int mode;       // 0 (kept for the binning scans shared with the cube)
 };
 
 struct Merge {      // a tile split over several items: sum their slabs
@@ -132,18 +152,51 @@ __device__ __forceinline__ void chunk_range(double w, double h, double w_min, do
     c_hi = cmax;
 }
 
+// The fp64 values the reference sees for particle p: pixel-test coordinates (U, V),
+// cull coordinates (CU, CV) and h.
+struct Vals {
+    double U, V, CU, CV, H;
+};
+__device__ __forceinline__ Vals src_values(const Grid& g, const Src64& s, int p) {
+    Vals r;
+    if (s.u64) {
+        const long long o = (long long)p * s.stride;
+        r.U = s.u64[o];
+        r.V = s.v64[o];
+        r.H = s.h64[p];
+        r.CU = g.mixed ? s.cu64[o] : r.U;
+        r.CV = g.mixed ? s.cv64[o] : r.V;
+    } else {
+        r.U = r.CU = s.u32[p];
+        r.V = r.CV = s.v32[p];
+        r.H = s.h32[p];
+    }
+    return r;
+}
+// The exact fp64 value of particle p's pixel-test coordinate u (fp32 value u when the
+// fp32 inputs are the inputs) -- the source of tile-local coordinates.
+__device__ __forceinline__ double src_u(const Src64& s, int p, float u) {
+    return s.u64 ? s.u64[(long long)p * s.stride] : (double)u;
+}
+__device__ __forceinline__ double src_v(const Src64& s, int p, float v) {
+    return s.v64 ? s.v64[(long long)p * s.stride] : (double)v;
+}
+
 // Candidate pixel box of a particle: a superset of the pixels that can pass the exact
 // test.  fp32 estimate of (w - 2|h| - w_min) / pitch with a margin delta that bounds its
 // rounding error: at most ~6 roundings of 2^-24 relative to (|w| + |w_min| + 2|h|) / pitch
-// (w_min and 1/pitch to fp32, the difference, the product, the two offsets), so 2^-20
-// leaves a 2.7x margin; plus 2^-12 px so that a corner at exactly 2h stays a candidate.
-// (A wider margin makes more pixel-scale boxes 4 corners wide, which leave the fast 3 x 3
-// deposit.)  False when nothing can pass.
-__device__ __forceinline__ bool footprint(const Grid& g, float u, float v, float h, Box& b) {
+// (w_min and 1/pitch to fp32, the difference, the product, the two offsets) plus the
+// rounding of fp64 inputs to fp32 (2^-24 |w|, 2^-23 |h|), so 2^-20 leaves a 2x margin;
+// plus 2^-12 px so that a corner at exactly 2h stays a candidate.  Where the cull is not
+// implied by the disc -- the y axis of non-square images (S2), both axes when the cull
+// reads other columns (Grid::mixed) -- the range is clipped to the chunks whose cull
+// accepts the particle, computed exactly from the inputs (fp64 ones when given), so
+// every pixel of the box passes the cull.  False when nothing can pass.
+__device__ __forceinline__ bool footprint(const Grid& g, const Src64& s, int p, float u, float v,
+                                          float h, Box& b) {
     float hd = fabsf(2.0f * h);
     if (!(hd > 0.0f) || !__builtin_isfinite(hd)) {
         // h == 0: r2 < 0 never holds (S12).  Non-finite: excluded.
-        // |2h| overflowing fp32 only happens for non-finite h (|h| < 1.7e38).
         return false;
     }
     if (!__builtin_isfinite(u) || !__builtin_isfinite(v)) return false;
@@ -160,12 +213,19 @@ __device__ __forceinline__ bool footprint(const Grid& g, float u, float v, float
     b.x1 = (int)fx1;
     b.y0 = (int)fy0;
     b.y1 = (int)fy1;
-    if (g.nonsquare) {  // S2: the y cull pitch differs from the pixel pitch
+    if (g.nonsquare || g.mixed) {
+        const Vals x = src_values(g, s, p);
         int c0, c1;
-        chunk_range((double)v, (double)h, g.y_min, g.psy_cull, g.ny, g.cs, c0, c1);
+        chunk_range(x.CV, x.H, g.y_min, g.psy_cull, g.ny, g.cs, c0, c1);
         b.y0 = max(b.y0, c0 * g.cs);
         b.y1 = min(b.y1, min((c1 + 1) * g.cs, g.ny) - 1);
         if (b.y0 > b.y1) return false;
+        if (g.mixed) {
+            chunk_range(x.CU, x.H, g.x_min, g.psx, g.nx, g.cs, c0, c1);
+            b.x0 = max(b.x0, c0 * g.cs);
+            b.x1 = min(b.x1, min((c1 + 1) * g.cs, g.nx) - 1);
+            if (b.x0 > b.x1) return false;
+        }
     }
     return true;
 }
@@ -212,15 +272,20 @@ __device__ __forceinline__ float kernel_shape(float q) {
 }
 
 // Error band of a record: thr = (2h)^2 in fp32 and the band around it
-// inside which the fp32 decision is not trusted (+inf: every pair goes to fp64).
-__device__ __forceinline__ void rec_band(const Grid& g, float h, float& thr, float& band) {
+// inside which the fp32 decision is not trusted (+inf: every pair goes to fp64).  It
+// bounds the fp32 decision error in either frame: absolute corners (|X| <= M) or
+// tile-local ones (|X| <= 64 pitches), g.mg = the larger of the two bounds.
+__device__ __forceinline__ float rec_thr(float h) {
     float D = 2.0f * h;
-    float Da = fabsf(D);
-    thr = D * D;
-    float eps = 0x1p-22f * (g.mg + Da);
-    band = 4.0f * Da * eps + 2.0f * eps * eps + 0x1p-20f * Da * Da;
+    return D * D;
+}
+__device__ __forceinline__ float rec_band(const Grid& g, float h) {
+    float Da = fabsf(2.0f * h);
+    float eps = 0x1p-21f * (g.mg + Da);
+    float band = 4.0f * Da * eps + 2.0f * eps * eps + 0x1p-20f * Da * Da;
     // Negative h narrows the chunk cull below the disc: decide every pair in fp64.
     if (h < 0.0f || !__builtin_isfinite(band)) band = __builtin_inff();
+    return band;
 }
 
 // thr -/+ band rounded: the band bounds the decision error with a >= 2x margin and its
@@ -233,15 +298,15 @@ __device__ __forceinline__ void set_band(Prep& P, float thr, float band) {
 }
 
 template <int KID, int ACC = kAccF64>
-__device__ __forceinline__ bool prep_record(const Grid& g, float u, float v, float h, float a0,
-                                            float a1, int k0, int k1, Prep& P) {
-    if (!footprint(g, u, v, h, P.b)) return false;
+__device__ __forceinline__ bool prep_record(const Grid& g, const Src64& s, int p, float u,
+                                            float v, float h, float a0, float a1, int k0,
+                                            int k1, Prep& P) {
+    if (!footprint(g, s, p, u, v, h, P.b)) return false;
     P.u = u;
     P.v = v;
     P.h = h;
-    float thr, band;
-    rec_band(g, h, thr, band);
-    set_band(P, thr, band);
+    P.p = p;
+    set_band(P, rec_thr(h), rec_band(g, h));
     P.hinv = __builtin_amdgcn_rcpf(h);  // value path only (fp32 tolerance)
     if constexpr (ACC == kAccFix) {
         P.s0 = (float)ldexp(term_coef<KID>(a0, h), k0);
@@ -253,26 +318,27 @@ __device__ __forceinline__ bool prep_record(const Grid& g, float u, float v, flo
     return true;
 }
 
-// Reference decision in fp64 (.pyx:13-14, :20-31 and the chunk cull): the slow path.
-__device__ __forceinline__ bool exact_pair(const Grid& g, float u, float v, float h,
-                                                      int xi, int yi) {
-    double ud = u, vd = v, hd = h;
-    double dx = ud - corner_x(g, xi);
-    double dy = vd - corner_y(g, yi);
+// Reference decision in fp64 (.pyx:13-14, :20-31 and the chunk cull): the slow path, on
+// the caller's values of particle p.
+__device__ __forceinline__ bool exact_pair(const Grid& g, const Src64& s, int p, int xi, int yi) {
+    const Vals x = src_values(g, s, p);
+    double dx = x.U - corner_x(g, xi);
+    double dy = x.V - corner_y(g, yi);
     double r2 = dx * dx + dy * dy;
-    double t = 2.0 * hd;
-    return (r2 < t * t) && cull_pass(g, ud, vd, hd, xi, yi);
+    double t = 2.0 * x.H;
+    return (r2 < t * t) && cull_pass(g, x.CU, x.CV, x.H, xi, yi);
 }
 
-// The full decision for one (record, pixel) pair given the fp32 corner coordinates.
+// The full decision for one (record, pixel) pair given the fp32 corner coordinates in
+// the frame of (P.u, P.v) (tile-local in the deposits, absolute in k_neighbours).
 // Returns inclusion and the fp32 r2 used for the kernel value.
-__device__ __forceinline__ bool decide(const Grid& g, const Prep& P, int xi, int yi, float X,
-                                       float Y, float& r2) {
+__device__ __forceinline__ bool decide(const Grid& g, const Src64& s, const Prep& P, int xi,
+                                       int yi, float X, float Y, float& r2) {
     float dx = P.u - X;
     float dy = P.v - Y;
     r2 = dx * dx + dy * dy;
     bool in = r2 < P.lo;
-    if (r2 >= P.lo && r2 <= P.hi) in = exact_pair(g, P.u, P.v, P.h, xi, yi);
+    if (r2 >= P.lo && r2 <= P.hi) in = exact_pair(g, s, P.p, xi, yi);
     return in;
 }
 
@@ -290,24 +356,12 @@ __device__ __forceinline__ unsigned long long f2fix(float f) {
 }
 
 // Add one term to an LDS tile accumulator word.
-#ifndef ASP_ABLATE_ACC
-#define ASP_ABLATE_ACC 0  // diagnostic builds only (wrong maps): 1 = no LDS add, 2 = the fp64
-                          // term's bits added with ds_add_u64, 3 = fp32 term, ds_add_u32
-#endif
 template <int ACC>
 __device__ __forceinline__ void acc_add(unsigned long long* a, float t) {
-#if ASP_ABLATE_ACC == 1
-    asm volatile("" ::"v"(t), "v"(a));
-#elif ASP_ABLATE_ACC == 2
-    atomicAdd(a, (unsigned long long)__double_as_longlong((double)t));
-#elif ASP_ABLATE_ACC == 3
-    atomicAdd((unsigned*)a, __float_as_uint(t));
-#else
     if constexpr (ACC == kAccFix)
         atomicAdd(a, f2fix(t));
     else
         atomicAdd((double*)a, (double)t);
-#endif
 }
 
 // Accumulator word -> map value.

@@ -41,7 +41,7 @@ enum Stage {
     kSWide, kSRatio,
     // 3-D cube (asp_project3d)
     kS3Count = 10, kS3Colscan, kS3Tilescan, kS3Scatter, kS3Deposit, kS3Merge,
-    kSBand = 16  // 2-D row-band deposit of non-small records
+    kSGather = 16  // 2-D gathered deposit of the large-record stream
 };
 
 struct Workspace {
@@ -62,9 +62,11 @@ struct Workspace {
     Buf knn[7];  // asp_knn_smoothing_lengths
     Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
         wide, slabs, morton, aux[6];
+    Buf in64[4];     // asp_project2d_f64: the caller's fp64 arrays, resident for exact decisions
+    Buf tile_large;  // per 2-D tile: holds records gathered by the deposit's large path
+    Buf pairs[4];    // asp_pair_list
     int* h_counters = nullptr;  // pinned
     int morton_ntx = -1, morton_nty = -1;
-    Buf morton3;  // brick order of the 3-D cube
     int morton3_key[3] = {-1, -1, -1};
     long long stats[9] = {0};
     // Chunked 2-D pipeline: deposits run on a side stream, each behind its chunk's scatter.
@@ -73,6 +75,21 @@ struct Workspace {
     hipEvent_t done_ev = nullptr;
     hipEvent_t scan_ev = nullptr;  // 2-D pipeline: binning scans done (st)
     hipEvent_t cnt_ev = nullptr;   // ... and their counters copied to the host (side)
+    // End of the last call's GPU work on the workspace: the next call's stream waits for
+    // it, so calls on different streams never overwrite buffers still being read.
+    hipEvent_t last_ev = nullptr;
+    Buf morton3;  // brick order of the 3-D cube
+    std::vector<Buf*> all_bufs() {
+        std::vector<Buf*> v = {&hist, &cmx, &tile_total, &tile_start, &tile_k, &items, &merges,
+                               &counters, &recs, &wide, &slabs, &morton, &morton3, &tile_large};
+        for (auto& b : in) v.push_back(&b);
+        for (auto& b : out) v.push_back(&b);
+        for (auto& b : aux) v.push_back(&b);
+        for (auto& b : knn) v.push_back(&b);
+        for (auto& b : in64) v.push_back(&b);
+        for (auto& b : pairs) v.push_back(&b);
+        return v;
+    }
 };
 
 inline int ensure_side(Workspace& ws) {
@@ -87,6 +104,32 @@ inline int ensure_side(Workspace& ws) {
 }
 
 inline Workspace g_ws[64];
+
+inline int set_device(int device) {
+    int ndev = 0;
+    ASP_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(ASP_ERR_INVALID, "bad device");
+    ASP_HIP(hipSetDevice(device));
+    return ASP_OK;
+}
+
+// Cross-call ordering of the shared workspace (the caller holds ws.mu): a call's stream
+// first waits for the end of the previous call's work, and records the new end.
+inline int ws_begin(Workspace& ws, hipStream_t st) {
+    if (ws.last_ev) ASP_HIP(hipStreamWaitEvent(st, ws.last_ev, 0));
+    return ASP_OK;
+}
+inline int ws_end(Workspace& ws, hipStream_t st) {
+    if (!ws.last_ev) ASP_HIP(hipEventCreateWithFlags(&ws.last_ev, hipEventDisableTiming));
+    ASP_HIP(hipEventRecord(ws.last_ev, st));
+    return ASP_OK;
+}
+
+// asp_stage.hip: reader arrays on the device -> the projector's fp32 working copies
+// (axis selection of _projector.py:38-46, round to nearest), enqueued on st.
+int stage_device(const double* pos, const double* h, const double* a0, const double* a1,
+                 long long n, int axis, float* u, float* v, float* hf, float* a0f, float* a1f,
+                 hipStream_t st);
 
 inline int prof_fold_set(Workspace& ws, int set) {
     for (int k = 0; k < kStages; ++k) {
@@ -136,24 +179,16 @@ inline int ensure(Buf& b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return ASP_OK;
     if (b.p) {
-        hipError_t e = hipFree(b.p);
-        (void)e;
+        (void)hipFree(b.p);
         b.p = nullptr;
         b.cap = 0;
     }
-    size_t want = bytes + bytes / 4;
-    hipError_t e = hipErrorOutOfMemory;
-    if (want >= (size_t(1) << 28) && getenv("ASP_CONTIG") && atoi(getenv("ASP_CONTIG")))
-        e = hipExtMallocWithFlags(&b.p, want, hipDeviceMallocContiguous);
+    size_t want = bytes + bytes / 4;  // grow with slack: fewer re-allocations across calls
+    hipError_t e = hipMalloc(&b.p, want);
     if (e != hipSuccess) {
         (void)hipGetLastError();
-        e = hipMalloc(&b.p, want);
-    } else if (getenv("ASP_DEBUG_ALLOC")) {
-        fprintf(stderr, "[asp] contiguous ");
-    }
-    if (e != hipSuccess) {
-        e = hipMalloc(&b.p, bytes);
         want = bytes;
+        e = hipMalloc(&b.p, want);
     }
     if (e != hipSuccess) {
         b.p = nullptr;
@@ -161,8 +196,6 @@ inline int ensure(Buf& b, size_t bytes) {
                                        hipGetErrorString(e));
     }
     b.cap = want;
-    if (want >= (size_t(1) << 28) && getenv("ASP_DEBUG_ALLOC"))
-        fprintf(stderr, "[asp] hipMalloc %zu B at %p\n", want, b.p);
     return ASP_OK;
 }
 

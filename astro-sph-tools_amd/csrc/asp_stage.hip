@@ -116,20 +116,22 @@ __device__ __forceinline__ double stage_coord(const StageArgs& S, double x, int 
     return x;
 }
 
-// Periodic image direction on one axis: +1 (a copy at x + L) when the reach R crosses the
-// box's lower face, -1 (x - L) for the upper face; only particles inside the box.
-__device__ __forceinline__ int image_dir(double x, double R, double lo, double L) {
-    if (!(x >= lo && x < lo + L)) return 0;
-    if (x - lo < R) return 1;
-    if ((lo + L) - x <= R) return -1;
-    return 0;
+// Periodic image shifts on one axis: the k (copy at x + k L) whose reach [x + kL - R,
+// x + kL + R] meets the box [lo, lo + L); only particles inside the box get copies.  R
+// carries a 2^-20 L margin, far above the rounding of these fp64 expressions, so no copy
+// that can contribute is missed (an extra one would contribute nothing: the projection
+// decides every pair exactly).
+__device__ __forceinline__ void image_range(double x, double R, double lo, double L, int& k0,
+                                            int& k1) {
+    k0 = (int)floor((lo - x - R) / L) + 1;
+    k1 = (int)ceil((lo + L - x + R) / L) - 1;
 }
 
+constexpr int kMaxImageShift = 3;  // reach <= ~3 box widths per side (else an error)
+
 // Particles [i0, i1) (row i at index i - i0 of this chunk's arrays): outputs at index i;
-// periodic images appended at n + (claimed slot) while below cap.  The reach of an image
-// is 2|h| widened by a margin that covers the float32 rounding of the copy; extra images
-// add nothing (the projection decides every pair exactly), so the map is the sum over all
-// periodic images of every particle.
+// periodic images appended at n + (claimed slot) while below cap.  The map of the staged
+// set over the box is then the sum over all periodic images of every particle.
 __global__ __launch_bounds__(kStageBlock) void k_stage(
     StageArgs S, const double* __restrict__ pos, const double* __restrict__ h,
     const double* __restrict__ a0, const double* __restrict__ a1, long long i0, long long i1,
@@ -153,15 +155,18 @@ __global__ __launch_bounds__(kStageBlock) void k_stage(
         if (a1f) a1f[i] = (float)p1;
     }
     if (!S.images) return;
-    int dx = 0, dy = 0;
+    int kx0 = 0, kx1 = 0, ky0 = 0, ky1 = 0;
     if (live) {
-        double R = 2.0 * fabs(hd) * (1.0 + 0x1p-20) + 0x1p-20 * S.L;
-        if (R > 0.0 && R < S.L) {  // h == 0 or NaN: no images
-            dx = image_dir(x, R, S.lo, S.L);
-            dy = image_dir(y, R, S.lo, S.L);
+        const double R = 2.0 * fabs(hd) * (1.0 + 0x1p-20) + 0x1p-20 * S.L;
+        const bool inside = x >= S.lo && x < S.lo + S.L && y >= S.lo && y < S.lo + S.L;
+        if (inside && R > 0.0 && R <= kMaxImageShift * S.L) {  // h == 0 or NaN: none
+            image_range(x, R, S.lo, S.L, kx0, kx1);
+            image_range(y, R, S.lo, S.L, ky0, ky1);
+        } else if (inside && R > kMaxImageShift * S.L && R == R) {
+            atomicAdd(nimg + 1, 1ull);  // reach beyond the supported shifts: reported
         }
     }
-    int k = (dx != 0) + (dy != 0) + (dx != 0 && dy != 0);
+    const int k = (kx1 - kx0 + 1) * (ky1 - ky0 + 1) - 1;
     // one claim per wave; a lane's images follow those of the lanes below it
     unsigned long long m = __ballot(k > 0);
     if (!m) return;
@@ -178,27 +183,18 @@ __global__ __launch_bounds__(kStageBlock) void k_stage(
     base = __shfl(base, leader);
     if (k == 0) return;
     long long slot = n + (long long)base + before;
-    auto put = [&](double xx, double yy) {
-        if (slot < cap) {
-            u[slot] = (float)xx;
-            v[slot] = (float)yy;
-            if (hf) hf[slot] = (float)hd;
-            if (a0f) a0f[slot] = (float)p0;
-            if (a1f) a1f[slot] = (float)p1;
+    for (int kx = kx0; kx <= kx1; ++kx)
+        for (int ky = ky0; ky <= ky1; ++ky) {
+            if (kx == 0 && ky == 0) continue;
+            if (slot < cap) {
+                u[slot] = (float)(x + kx * S.L);
+                v[slot] = (float)(y + ky * S.L);
+                if (hf) hf[slot] = (float)hd;
+                if (a0f) a0f[slot] = (float)p0;
+                if (a1f) a1f[slot] = (float)p1;
+            }
+            ++slot;
         }
-        ++slot;
-    };
-    if (dx) put(x + dx * S.L, y);
-    if (dy) put(x, y + dy * S.L);
-    if (dx && dy) put(x + dx * S.L, y + dy * S.L);
-}
-
-static int set_device(int device) {
-    int ndev = 0;
-    ASP_HIP(hipGetDeviceCount(&ndev));
-    if (device < 0 || device >= ndev) return fail(ASP_ERR_INVALID, "bad device");
-    ASP_HIP(hipSetDevice(device));
-    return ASP_OK;
 }
 
 static unsigned grid_for(long long n) {
@@ -240,9 +236,10 @@ static int stage_particles(const double* pos, const double* h, const double* a0,
     ASP_TRY(set_device(device));
     Workspace& ws = g_ws[device];
     std::lock_guard<std::mutex> lock(ws.mu);
-    ASP_TRY(ensure(ws.aux[5], sizeof(unsigned long long)));
+    ASP_TRY(ws_begin(ws, st));
+    ASP_TRY(ensure(ws.aux[5], 2 * sizeof(unsigned long long)));
     unsigned long long* dimg = (unsigned long long*)ws.aux[5].p;
-    ASP_HIP(hipMemsetAsync(dimg, 0, sizeof(unsigned long long), st));
+    ASP_HIP(hipMemsetAsync(dimg, 0, 2 * sizeof(unsigned long long), st));
     if ((flags & ASP_F_DEVICE_PTRS) || n == 0) {
         if (n > 0) {
             hipLaunchKernelGGL(k_stage, dim3(grid_for(n)), dim3(kStageBlock), 0, st, S, pos, h, a0,
@@ -277,14 +274,34 @@ static int stage_particles(const double* pos, const double* h, const double* a0,
         ASP_HIP(hipEventRecord(ws.done_ev, ws.side));
         ASP_HIP(hipStreamWaitEvent(st, ws.done_ev, 0));
     }
-    unsigned long long nimg = 0;
-    ASP_HIP(hipMemcpyAsync(&nimg, dimg, sizeof(nimg), hipMemcpyDeviceToHost, st));
+    unsigned long long nimg[2] = {0, 0};
+    ASP_HIP(hipMemcpyAsync(nimg, dimg, sizeof(nimg), hipMemcpyDeviceToHost, st));
     ASP_HIP(hipStreamSynchronize(st));
-    *n_out = n + (long long)nimg;
+    ASP_TRY(ws_end(ws, st));
+    if (nimg[1])
+        return fail(ASP_ERR_UNSUPPORTED, std::to_string(nimg[1]) + " particles reach beyond " +
+                                             std::to_string(kMaxImageShift) +
+                                             " box widths (2|h| > 3 L): periodic images unsupported");
+    *n_out = n + (long long)nimg[0];
     if (*n_out > cap)
         return fail(ASP_ERR_INVALID, "periodic images exceed the output capacity (" +
                                          std::to_string(*n_out) + " > " + std::to_string(cap) +
                                          "); n_out holds the size needed");
+    return ASP_OK;
+}
+
+// Reader arrays already on the device -> fp32 working copies (no periodic options).
+int stage_device(const double* pos, const double* h, const double* a0, const double* a1,
+                 long long n, int axis, float* u, float* v, float* hf, float* a0f, float* a1f,
+                 hipStream_t st) {
+    if (n == 0) return ASP_OK;
+    StageArgs S{};
+    static const int cols[3][2] = {{1, 2}, {0, 2}, {0, 1}};  // _projector.py:38-46
+    S.a = cols[axis][0];
+    S.b = cols[axis][1];
+    hipLaunchKernelGGL(k_stage, dim3(grid_for(n)), dim3(kStageBlock), 0, st, S, pos, h, a0, a1,
+                       0LL, n, n, u, v, hf, a0f, a1f, n, (unsigned long long*)nullptr);
+    ASP_HIP(hipGetLastError());
     return ASP_OK;
 }
 

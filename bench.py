@@ -55,8 +55,6 @@ def parse():
                          "device fp32 SoA staging (SURVEY 8(f)); the last two are not the "
                          "driver's line")
     ap.add_argument("--cube", type=int, default=512, help="cube edge (voxels), --workload cube")
-    ap.add_argument("--chunks", type=int, default=None,
-                    help="particle chunks of the scatter/deposit pipeline (default: library's)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="N > 1: wait for each map's collective before the next map")
     ap.add_argument("--profile-steps", type=int, default=3,
@@ -412,8 +410,6 @@ def output_check(out0, out1, a0, a1, ratio, world=1):
 
 def main():
     args = parse()
-    if args.chunks is not None:
-        os.environ["ASP_CHUNKS"] = str(args.chunks)
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -545,9 +541,7 @@ def main():
     stages = {k: {"ms_per_launch": (ms / n if n else 0.0), "launches": n}
               for k, (ms, n) in prof_all.items() if n}
     # Dominant kernel = most device time per step (untimed breakdown), its duration measured
-    # by HIP events over the timed steps.  With a chunked pipeline a stage launches once
-    # per chunk (each over 1/chunks of the particles), so its per-step time is the sum of
-    # its launches and the algorithmic bytes are the step's.
+    # by HIP events over the timed steps (one launch per step).
     dom_ms = prof[dom][0] / args.steps
     achieved = bytes_alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic = None
@@ -555,7 +549,8 @@ def main():
     try:
         with open(args.pmc) as f:
             pm = json.load(f)
-        key = f"n{args.n}_g{G}_{args.kernel}_{args.h_law}_{args.map}"
+        # per-rank traffic: keyed on THIS rank's particle count (a profile of the shard)
+        key = f"n{n_local}_g{G}_{args.kernel}_{args.h_law}_{args.map}"
         if key in pm and dom in pm[key]:
             traffic = pm[key][dom]["hbm_bytes_per_launch"]
             traffic_src = pm[key].get("source")
@@ -592,7 +587,7 @@ def main():
                      "pipeline_frac": round(bytes_alg / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "stages": stages,
         "records_per_particle": round(st["records"] / max(1, n_local), 4),
-        "work_items": st["items"], "wide_particles": st["wide"], "chunks": st["chunks"],
+        "work_items": st["items"], "wide_particles": st["wide"], "large_records": st["large"],
         "output_ok": ok,
     }
     want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)

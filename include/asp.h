@@ -20,7 +20,8 @@
  *    with ASP_F_DEVICE_PTRS they are device pointers on `device` and the call is
  *    ordered on `stream` (a hipStream_t, NULL = the legacy default stream);
  *  - thread-safe: a per-device workspace cache guarded by a mutex; one call at a time
- *    per device.
+ *    per device enqueues work, and each call's stream first waits for the previous
+ *    call's work (an event), so calls on different streams never share buffers in flight.
  */
 #ifndef ASP_H
 #define ASP_H
@@ -48,6 +49,9 @@ extern "C" {
                                  * for pixels below ~2^-37 n_t max|A W| of their 64x64 tile
                                  * (DESIGN.md §4).  Default: fp64 accumulation.            */
 
+/* asp_project2d_f64 axis: cull on axis c's columns (the reference's mixed spellings) */
+#define ASP_AXIS_CULL(c) (((c) + 1) << 4)
+
 /* errors */
 #define ASP_OK 0
 #define ASP_ERR_INVALID -1     /* bad argument (ValueError on the Python side)             */
@@ -74,8 +78,9 @@ int asp_device_count(void);
  *   r_p^2 = (u_p - X_xi)^2 + (v_p - Y_yi)^2,  X_xi = u_min + xi * (u_max-u_min)/nx,
  *   Y_yi = v_min + yi * (v_max - v_min)/nx   (sic: nx -- reference quirk S2).
  *
- * Neighbour membership is decided with the reference's fp64 arithmetic (bit-exact
- * neighbour sets); values are accumulated in fp32.  a1/out1 (both non-NULL or both
+ * Neighbour membership is decided with the reference's fp64 arithmetic on the fp64
+ * values of the fp32 inputs (bit-exact neighbour sets for those inputs; for raw fp64
+ * reader arrays use asp_project2d_f64); values are accumulated in fp32 terms.  a1/out1 (both non-NULL or both
  * NULL) give a second map over the same neighbour sets (mass-weighted maps:
  * a0 = m*T, a1 = m, with ASP_F_RATIO).  n == 0 is valid (all-zero image).
  * chunk_size >= 1 is the reference's tile size; it only changes results for
@@ -85,6 +90,47 @@ int asp_project2d(const float *u, const float *v, const float *h, const float *a
                   const float *a1, int64_t n, double u_min, double u_max, double v_min,
                   double v_max, int32_t nx, int32_t ny, int32_t chunk_size, int32_t kernel_id,
                   int32_t flags, float *out0, float *out1, int32_t device, void *stream);
+
+/*
+ * create_image on the reader's own float64 arrays: the drop-in for create_image
+ * (_projector.py:75-120) as it is called, with positions (n, 3) float64 row-major (the
+ * reader's get_positions, _SnapshotBase.py:708-722), smoothing lengths and properties
+ * float64, and the projection axis (0 = X -> (y, z), 1 = Y -> (x, z), 2 = Z -> (x, y);
+ * _projector.py:38-46).  The reference decides the chunk cull (_projector.py:38-46, enum
+ * comparison) and the pixel test (_pixel_calculations.pyx:20-28, str().encode()) from
+ * the axis separately, so some spellings (a str "x") cull on other columns than they
+ * test: axis | ASP_AXIS_CULL(c) reproduces that, culling on axis c's columns.  The library stages float32 working copies in HBM and keeps the
+ * float64 arrays resident: every (particle, pixel) decision is the reference's fp64 test
+ * on the ORIGINAL fp64 values (bit-exact neighbour sets for any fp64 input, not only
+ * fp32-representable ones); values accumulate as in asp_project2d.  Host pointers unless
+ * ASP_F_DEVICE_PTRS (then device pointers, ordered on `stream`).  Other arguments and
+ * flags as asp_project2d.
+ */
+int asp_project2d_f64(const double *positions, const double *h, const double *a0,
+                      const double *a1, int64_t n, int32_t axis, double u_min, double u_max,
+                      double v_min, double v_max, int32_t nx, int32_t ny, int32_t chunk_size,
+                      int32_t kernel_id, int32_t flags, float *out0, float *out1, int32_t device,
+                      void *stream);
+
+/*
+ * The kernel_func plugin point (_projector.py:26, 86; _pixel_calculations.pyx:30-33):
+ * for an arbitrary user kernel W(r, h) -- Python code that cannot run on the device --
+ * the device produces the neighbour pairs and the host evaluates W on them.  For the
+ * GPU tiles tile_lo <= t < tile_hi (64 x 64 pixels, t = tx * ceil(ny/64) + ty), every
+ * (pixel, particle) pair create_image includes (the same exact decision as
+ * asp_project2d_f64) is written at the pixel's slot range: particle[k] (index into the
+ * inputs) and r2[k] = dx*dx + dy*dy in fp64 as the reference forms it (.pyx:13-14,
+ * :20-30), k in [offsets[q], offsets[q+1]) for the q-th pixel of the range, pixels
+ * tile by tile and (lx * 64 + ly) inside a tile (pixels outside the image: empty).
+ * offsets ((tile_hi - tile_lo) * 4096 + 1 entries, non-decreasing) come from the
+ * per-pixel neighbour counts (asp_project2d_f64 with ASP_KERNEL_INDICATOR and a = 1).
+ * Order inside a pixel is unspecified.  positions / h / axis / extent / chunk_size as
+ * asp_project2d_f64.  Host pointers unless ASP_F_DEVICE_PTRS.
+ */
+int asp_pairs_f64(const double *positions, const double *h, int64_t n, int32_t axis,
+                  double u_min, double u_max, double v_min, double v_max, int32_t nx, int32_t ny,
+                  int32_t chunk_size, int32_t tile_lo, int32_t tile_hi, const int64_t *offsets,
+                  int32_t *particle, double *r2, int32_t flags, int32_t device, void *stream);
 
 /*
  * 3-D voxel cube (build-defined; SURVEY.md §8(a) "512^3 cube" -- no reference
@@ -240,7 +286,7 @@ int asp_table_interp3(const double *table, int32_t n0, int32_t n1, int32_t n2,
  * stats[0] = records binned (particle x GPU-tile insertions), stats[1] = work items,
  * stats[2] = wide particles, stats[3] = GPU tile edge (pixels), stats[4] = GPU tiles,
  * stats[5] = records per work item, stats[6] = split tiles, stats[7] = partial slabs,
- * stats[8] = particle chunks of the scatter / deposit pipeline.
+ * stats[8] = records in the large (gathered) stream.
  */
 int asp_last_stats(int32_t device, int64_t *stats, int32_t nstats);
 
@@ -250,7 +296,7 @@ int asp_last_stats(int32_t device, int64_t *stats, int32_t nstats);
  * summed milliseconds and the number of launches since the last reset.  Stages:
  * 0 memset, 1 count, 2 colscan, 3 tilescan, 4 scatter, 5 scale, 6 deposit, 7 merge,
  * 8 wide, 9 ratio; cube (asp_project3d): 10 count, 11 colscan, 12 tilescan, 13 scatter,
- * 14 deposit, 15 merge; 16 band (2-D row-band deposit of non-small records).
+ * 14 deposit, 15 merge; 16 gather (2-D gathered deposit of the large-record stream).
  */
 int asp_profile(int32_t device, int32_t enable);
 /* As asp_profile(device, 1), but events only around the stages whose bit is set in

@@ -63,6 +63,32 @@ static double kernel_w(int kid, double r, double h)
     return 1.0; /* indicator: every included pair counts 1 */
 }
 
+/* The same kernels for the O(pairs) restatement below, with powers as products and the
+ * normalisation per particle (nrm = 1/(pi h^3), or 21/(16 pi h^3)): within an ulp or two
+ * of kernel_w, which the scatter restatement's own (sequential) summation order already
+ * exceeds; the bit-exact gather path keeps kernel_w. */
+static double kernel_w_fast(int kid, double q, double nrm)
+{
+    if (kid == ORC_CUBIC) {
+        if (q < 1.0)
+            return (1 - 1.5 * (q * q) + 0.75 * (q * q * q)) * nrm;
+        else if (q < 2.0) {
+            double t = 2 - q;
+            return (0.25 * (t * t * t)) * nrm;
+        }
+        return 0.0;
+    }
+    if (kid == ORC_WENDLAND_C2) {
+        if (q < 2.0) {
+            double t = 1.0 - 0.5 * q;
+            double t2 = t * t;
+            return nrm * (t2 * t2) * (1.0 + 2.0 * q);
+        }
+        return 0.0;
+    }
+    return 1.0;
+}
+
 void oracle_kernel_eval(int kid, const double *r, const double *h, double *w, int64_t n)
 {
     for (int64_t i = 0; i < n; ++i)
@@ -157,11 +183,17 @@ static int pixel_pass(const grid_t *g, double u, double v, double h, int xi, int
  * restricts the work to a subset -- used for the bounded CPU-baseline sample, where
  * the other pixels are left untouched.  img is (nx, ny) C-order, img[xi * ny + yi].
  */
-int oracle_create_image(const double *u, const double *v, const double *h, const double *A,
+int oracle_create_image(const double *u, const double *v, const double *cu, const double *cv,
+                        const double *h, const double *A,
                         int64_t n, int nx, int ny, int cs, double x_min, double x_max,
                         double y_min, double y_max, int kid, const int64_t *chunk_ids,
                         int64_t n_chunk_ids, int nthreads, double *img)
 {
+    /* cu, cv: the columns the cull reads (NULL: u, v).  The reference picks them with an
+     * enum comparison (_projector.py:38-46) and the pixel columns with str().encode()
+     * (.pyx:20-28), so some axis spellings cull on other columns than they test. */
+    if (!cu) cu = u;
+    if (!cv) cv = v;
     if (nx <= 0 || ny <= 0 || cs <= 0)
         return -1;
     grid_t g = make_grid(nx, ny, cs, x_min, x_max, y_min, y_max);
@@ -193,7 +225,7 @@ int oracle_create_image(const double *u, const double *v, const double *h, const
             /* cull (_projector.py:38-51): members in ascending particle order */
             int64_t m = 0;
             for (int64_t p = 0; p < n; ++p) {
-                if (cull_pass(&g, u[p], v[p], h[p], xi0, yi0)) {
+                if (cull_pass(&g, cu[p], cv[p], h[p], xi0, yi0)) {
                     if (m == cap) {
                         cap *= 2;
                         idx = (int64_t *)realloc(idx, sizeof(int64_t) * cap);
@@ -326,11 +358,14 @@ static void chunk_range(double w, double h, double w_min, double ps, int npx, in
  * Threads own disjoint bands of x rows, so the result is deterministic.
  * out0 gets sum(A0 W); out1 (nullable) gets sum(A1 W).
  */
-int oracle_project_scatter(const double *u, const double *v, const double *h, const double *A0,
+int oracle_project_scatter(const double *u, const double *v, const double *cu, const double *cv,
+                           const double *h, const double *A0,
                            const double *A1, int64_t n, int nx, int ny, int cs, double x_min,
                            double x_max, double y_min, double y_max, int kid, int nthreads,
                            double *out0, double *out1)
 {
+    if (!cu) cu = u; /* cull columns, as oracle_create_image */
+    if (!cv) cv = v;
     if (nx <= 0 || ny <= 0 || cs <= 0)
         return -1;
     grid_t g = make_grid(nx, ny, cs, x_min, x_max, y_min, y_max);
@@ -360,19 +395,22 @@ int oracle_project_scatter(const double *u, const double *v, const double *h, co
             int x0 = fx0 < bx0 ? bx0 : (int)fx0, x1 = fx1 > bx1 - 1 ? bx1 - 1 : (int)fx1;
             int y0 = fy0 < 0 ? 0 : (int)fy0, y1 = fy1 > ny - 1 ? ny - 1 : (int)fy1;
             int cx0, cx1, cy0, cy1;
-            chunk_range(up, hp, x_min, g.psx, nx, cs, &cx0, &cx1);
-            chunk_range(vp, hp, y_min, g.psy_cull, ny, cs, &cy0, &cy1);
+            chunk_range(cu[p], hp, x_min, g.psx, nx, cs, &cx0, &cx1);
+            chunk_range(cv[p], hp, y_min, g.psy_cull, ny, cs, &cy0, &cy1);
             if (cx0 > cx1 || cy0 > cy1)
                 continue;
             if (x0 < cx0 * cs) x0 = cx0 * cs;
             if (x1 > (cx1 + 1) * cs - 1) x1 = (cx1 + 1) * cs - 1;
             if (y0 < cy0 * cs) y0 = cy0 * cs;
             if (y1 > (cy1 + 1) * cs - 1) y1 = (cy1 + 1) * cs - 1;
+            const double nrm = kid == ORC_CUBIC ? 1.0 / (M_PI * (hp * hp * hp))
+                               : 21.0 / (16.0 * M_PI * (hp * hp * hp));
+            const double hinv = 1.0 / hp;
             for (int xi = x0; xi <= x1; ++xi)
                 for (int yi = y0; yi <= y1; ++yi) {
                     double r2;
                     if (pixel_pass(&g, up, vp, hp, xi, yi, &r2)) {
-                        double w = kernel_w(kid, sqrt(r2), hp);
+                        double w = kernel_w_fast(kid, sqrt(r2) * hinv, nrm);
                         int64_t o = (int64_t)xi * ny + yi;
                         out0[o] += A0[p] * w;
                         if (out1)

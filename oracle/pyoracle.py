@@ -39,7 +39,7 @@ def lib():
             build()
         L = C.CDLL(LIB_PATH)
         L.oracle_kernel_eval.argtypes = [C.c_int, _d, _d, _d, C.c_int64]
-        L.oracle_create_image.argtypes = [_d, _d, _d, _d, C.c_int64, C.c_int, C.c_int, C.c_int,
+        L.oracle_create_image.argtypes = [_d, _d, _d, _d, _d, _d, C.c_int64, C.c_int, C.c_int, C.c_int,
                                           C.c_double, C.c_double, C.c_double, C.c_double, C.c_int,
                                           _i64, C.c_int64, C.c_int, _d]
         L.oracle_chunk_members.argtypes = [_d, _d, _d, C.c_int64, C.c_int, C.c_int, C.c_int,
@@ -50,7 +50,7 @@ def lib():
                                               C.c_double, C.c_double, C.c_double, C.c_double,
                                               _i64, C.c_int64, _i64, _i32, C.c_int64]
         L.oracle_pixel_neighbours.restype = C.c_int64
-        L.oracle_project_scatter.argtypes = [_d, _d, _d, _d, _d, C.c_int64, C.c_int, C.c_int,
+        L.oracle_project_scatter.argtypes = [_d, _d, _d, _d, _d, _d, _d, C.c_int64, C.c_int, C.c_int,
                                              C.c_int, C.c_double, C.c_double, C.c_double,
                                              C.c_double, C.c_int, C.c_int, _d, _d]
         L.oracle_chunk_ranges.argtypes = [_d, _d, _d, C.c_int64, C.c_int, C.c_int, C.c_int,
@@ -81,6 +81,21 @@ def _uv(positions, axis):
     return _f64(positions[:, a]), _f64(positions[:, b])
 
 
+def _axes(positions, projection_axis):
+    """(u, v, cu, cv): pixel-test columns and cull columns.  ``projection_axis`` is an
+    axis (0/1/2 or enum: both the same) or a (pixel axis, cull axis) pair -- the
+    reference derives the two separately (_projector.py:38-46 vs .pyx:20-28)."""
+    if isinstance(projection_axis, tuple):
+        pa, ca = (int(a) for a in projection_axis)
+    else:
+        pa = ca = int(getattr(projection_axis, "value", projection_axis))
+    u, v = _uv(positions, pa)
+    if ca == pa:
+        return u, v, None, None
+    cu, cv = _uv(positions, ca)
+    return u, v, cu, cv
+
+
 def kernel_eval(kernel, r, h):
     r, h = _f64(r), _f64(h)
     w = np.empty_like(r)
@@ -92,12 +107,12 @@ def create_image(positions, smoothing_lengths, particle_properties, image_size, 
                  projection_axis, x_min, x_max, y_min, y_max, kernel="cubic", nthreads=0,
                  chunk_ids=None):
     """Reference-exact restatement of ``create_image`` (gather, fp64)."""
-    u, v = _uv(positions, projection_axis)
+    u, v, cu, cv = _axes(positions, projection_axis)
     h, A = _f64(smoothing_lengths), _f64(particle_properties)
     nx, ny = int(image_size[0]), int(image_size[1])
     img = np.zeros((nx, ny), dtype=np.float64)
     ids = None if chunk_ids is None else np.ascontiguousarray(chunk_ids, dtype=np.int64)
-    rc = lib().oracle_create_image(_p(u), _p(v), _p(h), _p(A), u.size, nx, ny, int(chunk_size),
+    rc = lib().oracle_create_image(_p(u), _p(v), _p(cu), _p(cv), _p(h), _p(A), u.size, nx, ny, int(chunk_size),
                                    float(x_min), float(x_max), float(y_min), float(y_max),
                                    KERNELS[kernel], _p(ids, _i64), 0 if ids is None else ids.size,
                                    int(nthreads), _p(img))
@@ -107,14 +122,17 @@ def create_image(positions, smoothing_lengths, particle_properties, image_size, 
 
 
 def project_scatter(u, v, h, a0, a1, image_size, chunk_size, x_min, x_max, y_min, y_max,
-                    kernel="cubic", nthreads=0):
-    """O(pairs) restatement; returns (out0, out1-or-None), float64 (nx, ny)."""
+                    kernel="cubic", nthreads=0, cu=None, cv=None):
+    """O(pairs) restatement; returns (out0, out1-or-None), float64 (nx, ny).  cu, cv:
+    the cull's columns when they differ from (u, v) (the reference's mixed axes)."""
     u, v, h, a0 = _f64(u), _f64(v), _f64(h), _f64(a0)
+    cu = None if cu is None else _f64(cu)
+    cv = None if cv is None else _f64(cv)
     a1 = None if a1 is None else _f64(a1)
     nx, ny = int(image_size[0]), int(image_size[1])
     o0 = np.empty((nx, ny), np.float64)
     o1 = None if a1 is None else np.empty((nx, ny), np.float64)
-    rc = lib().oracle_project_scatter(_p(u), _p(v), _p(h), _p(a0), _p(a1), u.size, nx, ny,
+    rc = lib().oracle_project_scatter(_p(u), _p(v), _p(cu), _p(cv), _p(h), _p(a0), _p(a1), u.size, nx, ny,
                                       int(chunk_size), float(x_min), float(x_max), float(y_min),
                                       float(y_max), KERNELS[kernel], int(nthreads), _p(o0), _p(o1))
     if rc != 0:
@@ -255,21 +273,23 @@ def stage_particles(positions, h, props, axis, L=None, centre=None, shift=None,
         return out
     lo = -(L / 2) if centred else 0.0
     R = 2.0 * np.abs(hh) * (1.0 + 2.0 ** -20) + 2.0 ** -20 * L
-    ok = (R > 0) & (R < L)
-
-    def direction(w):
-        inside = (w >= lo) & (w < lo + L) & ok
-        d = np.where(inside & (w - lo < R), 1, 0)
-        return np.where(inside & (d == 0) & ((lo + L) - w <= R), -1, d)
-
-    dx, dy = direction(x), direction(y)
+    inside = (x >= lo) & (x < lo + L) & (y >= lo) & (y < lo + L)
+    ok = inside & (R > 0) & (R <= 3 * L)
+    # copies at x + k L whose reach [x + kL - R, x + kL + R] meets [lo, lo + L)
+    with np.errstate(invalid="ignore"):
+        kx0 = np.where(ok, np.floor((lo - x - R) / L) + 1, 0).astype(np.int64)
+        kx1 = np.where(ok, np.ceil((lo + L - x + R) / L) - 1, 0).astype(np.int64)
+        ky0 = np.where(ok, np.floor((lo - y - R) / L) + 1, 0).astype(np.int64)
+        ky1 = np.where(ok, np.ceil((lo + L - y + R) / L) - 1, 0).astype(np.int64)
     extra = [[] for _ in cols]
-    for sx, sy, sel in ((dx, 0, dx != 0), (0, dy, dy != 0), (dx, dy, (dx != 0) & (dy != 0))):
-        sx = np.broadcast_to(sx, x.shape)[sel]
-        sy = np.broadcast_to(sy, y.shape)[sel]
-        shifted = [x[sel] + sx * L, y[sel] + sy * L] + [c[sel] for c in cols[2:]]
-        for k, c in enumerate(shifted):
-            extra[k].append(c)
+    for kx in range(-3, 4):
+        for ky in range(-3, 4):
+            if kx == 0 and ky == 0:
+                continue
+            sel = (kx0 <= kx) & (kx <= kx1) & (ky0 <= ky) & (ky <= ky1)
+            shifted = [x[sel] + kx * L, y[sel] + ky * L] + [c[sel] for c in cols[2:]]
+            for k, c in enumerate(shifted):
+                extra[k].append(c)
     return [np.concatenate([o] + [e.astype(np.float32) for e in ex]) for o, ex in zip(out, extra)]
 
 

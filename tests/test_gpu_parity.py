@@ -35,6 +35,22 @@ def assert_map_close(g, r, abs_tol=ABS_TOL, rel_tol=REL_TOL):
     assert rel.max() <= rel_tol, f"max rel err {rel.max():.3e}"
 
 
+def assert_ratio_close(r, o0, o1, abs_tol=ABS_TOL, rel_tol=REL_TOL):
+    """Weighted map r = s0 / s1 against the reference components o0, o1: zeros exact, and
+    the error within what the component bar allows to propagate into the quotient,
+    |dr| <= (abs_tol max|o0| + |r| abs_tol max|o1|) / o1 + 2 rel_tol |r| (a pixel whose
+    weight comes only from pairs at the kernel's edge has tiny o1)."""
+    r = np.asarray(r, np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        want = np.where(o1 != 0, o0 / o1, 0.0)
+    np.testing.assert_array_equal(r == 0, want == 0)
+    cov = o1 != 0
+    bound = ((abs_tol * np.abs(o0).max() + np.abs(want[cov]) * abs_tol * np.abs(o1).max())
+             / np.abs(o1[cov]) + 2 * rel_tol * np.abs(want[cov]))
+    err = np.abs(r[cov] - want[cov])
+    assert np.all(err <= bound), f"ratio error {np.max(err / bound):.3f} x its bound"
+
+
 def g3():
     g = golden("g3_plummer_1e4_256.npz")
     return (g["pos"].astype(np.float64), g["h"].astype(np.float64), g["A"].astype(np.float64),
@@ -57,8 +73,10 @@ def test_g2_hand_cases(gpu, case):
     from asp_amd.tools.projections import create_image
     g = golden("g2_hand_cases.npz")
     c = {k: g[f"c{case}_{k}"] for k in ("pos", "h", "A", "size", "cs", "axis", "ext", "img")}
+    from asp_amd import CoordinateAxes
+    # the fixture ran the reference with its enum member (an int would mean Z there)
     img = create_image(c["pos"].reshape(-1, 3), c["h"], c["A"], tuple(c["size"]), int(c["cs"]),
-                       int(c["axis"]), *c["ext"])
+                       CoordinateAxes(int(c["axis"])), *c["ext"])
     assert img.dtype == np.float64 and img.shape == c["img"].shape
     assert_map_close(img, c["img"])
     assert np.array_equal(img != 0, c["img"] != 0)
@@ -287,9 +305,8 @@ def test_edge_cases(gpu):
     assert create_image([[0, 0, 0]], [0.5], [1.0], (4, 4), -3, 2, -1, 1, -1, 1).sum() == 0
     with pytest.raises(ValueError):
         create_image([[0, 0, 0]], [0.5], [1.0], (4, 4), 0, 2, -1, 1, -1, 1)
-    with pytest.raises(TypeError):
-        create_image([[0, 0, 0]], [0.5], [1.0], (4, 4), 4, 2, -1, 1, -1, 1,
-                     kernel_func=lambda r, h: r)
+    with pytest.raises(TypeError):  # kernel_func must be callable
+        create_image([[0, 0, 0]], [0.5], [1.0], (4, 4), 4, 2, -1, 1, -1, 1, kernel_func=3.0)
     with pytest.raises(ValueError):
         create_image([[0, 0, 0]], [0.5], [1.0], (4, 4), 4, 2, 1, -1, -1, 1)
 
@@ -356,82 +373,37 @@ def test_default_vs_deterministic_modes(gpu):
     assert_map_close(b, a, abs_tol=1e-6, rel_tol=1e-5)
 
 
-@pytest.mark.parametrize("band_cols", ["1", "17", "65"])
-def test_row_band_path(gpu, oracle, band_cols, monkeypatch):
-    """Force records into the row-band deposit (K4b; ASP_BAND_COLS = minimum clipped box
-    columns) or keep them all on the sweep/lane paths: neighbour counts stay bit-exact and
-    values within tolerance either way."""
+@pytest.mark.parametrize("gmin", ["5", "12", "65"])
+def test_large_stream_threshold(gpu, oracle, gmin, monkeypatch):
+    """Records whose box clipped to a tile spans >= gather_min pixels on both axes go to
+    the large stream and are GATHERED (K4g: LDS list, register sums); the rest are
+    swept or deposited lane-per-record (K4).  Any threshold must give the same neighbour
+    counts (bit-exact) and values within tolerance: 5 sends almost every non-small box
+    to K4g, 65 none.  Tiles holding both streams are split items merged by K5."""
+    from asp_amd.device import stats
     from asp_amd.tools.projections import create_image, create_weighted_image, indicator_kernel
-    monkeypatch.setenv("ASP_BAND_COLS", band_cols)
+    monkeypatch.setenv("ASP_GATHER_MIN", gmin)
     rng = np.random.default_rng(11)
     n = 6000
-    pos = np.asarray(rng.normal(0, 0.4, (n, 3)), np.float32).astype(np.float64)
-    h = np.asarray(rng.uniform(0.002, 0.08, n), np.float32).astype(np.float64)
-    A = np.asarray(rng.uniform(0.5, 1.5, n), np.float32).astype(np.float64)
-    T = np.asarray(rng.uniform(1.0, 3.0, n), np.float32).astype(np.float64)
+    pos = rng.normal(0, 0.4, (n, 3))
+    h = rng.uniform(0.002, 0.08, n)
+    A = rng.uniform(0.5, 1.5, n)
+    T = rng.uniform(1.0, 3.0, n)
     G, ext = 512, (-1.0, 1.0, -1.0, 1.0)
     cnt = create_image(pos, h, np.ones(n), (G, G), 64, 2, *ext, kernel_func=indicator_kernel)
+    large = stats(0)["large"]
+    assert (large == 0) == (gmin == "65")
     want, _ = oracle.project_scatter(pos[:, 0], pos[:, 1], h, np.ones(n), None, (G, G), 64,
                                      *ext, kernel="indicator")
     assert np.array_equal(cnt, want)
     r, s0, s1 = create_weighted_image(pos, h, A, T, (G, G), 64, 2, *ext, return_components=True)
-    AT = np.asarray(A * T, np.float32).astype(np.float64)
-    w0, w1 = oracle.project_scatter(pos[:, 0], pos[:, 1], h, AT, A, (G, G), 64, *ext)
+    w0, w1 = oracle.project_scatter(pos[:, 0], pos[:, 1], h, A * T, A, (G, G), 64, *ext)
     assert_map_close(s0, w0)
     assert_map_close(s1, w1)
-
-
-@pytest.mark.parametrize("chunks", ["2", "3", "5"])
-def test_chunked_pipeline(gpu, oracle, chunks, monkeypatch):
-    """Particles cut into chunks whose deposits overlap the next chunk's scatter (side
-    stream, maps accumulated chunk by chunk, ratio taken by the last chunk): same bars as
-    the one-chunk path -- bit-exact neighbour counts, components and ratio within
-    tolerance; wide particles and split tiles included."""
-    from asp_amd.device import stats
-    from asp_amd.tools.projections import create_image, create_weighted_image, indicator_kernel
-    monkeypatch.setenv("ASP_CHUNKS", chunks)
-    monkeypatch.setenv("ASP_WIDE_TILES", "16")
-    p = plummer_f32(300_000, seed=21, h_law="pixel", grid=1024)
-    pos, h, m, T = p["pos"], p["h"], p["m"], p["T"]
-    h[:30] = np.float32(0.9)  # wide: ~50 > 16 tiles
-    G, ext = 1024, (-4.0, 4.0, -4.0, 4.0)
-    n = h.size
-    cnt = create_image(pos, h, np.ones(n), (G, G), 64, 2, *ext, kernel_func=indicator_kernel)
-    assert stats(0)["chunks"] == int(chunks) and stats(0)["wide"] > 20
-    want, _ = oracle.project_scatter(pos[:, 0], pos[:, 1], h, np.ones(n), None, (G, G), 64,
-                                     *ext, kernel="indicator")
-    assert np.array_equal(cnt, want)
-    r, s0, s1 = create_weighted_image(pos, h, m, T, (G, G), 64, 2, *ext, return_components=True)
-    a0 = (m * T).astype(np.float32).astype(np.float64)
-    o0, o1 = oracle.project_scatter(pos[:, 0], pos[:, 1], h, a0, m, (G, G), 64, *ext)
-    assert_map_close(s0, o0)
-    assert_map_close(s1, o1)
-    with np.errstate(divide="ignore", invalid="ignore"):
-        ratio_want = np.where(o1 != 0, o0 / o1, 0.0)
-    np.testing.assert_array_equal(r == 0, ratio_want == 0)
-    # the wide path's fixed point (DESIGN.md §4) holds its pixels to the component bar
-    # (2e-5 x max); a ratio of two tail-only sums ~1e-12 x max inherits their relative error
-    sig = o1 >= 1e-6 * o1.max()
-    np.testing.assert_allclose(r[sig], ratio_want[sig], rtol=2e-4, atol=0)
-    # fused ratio (no wide particles) with tiles that are empty in the last chunk
-    hs = h.copy()
-    hs[:30] = h[30:60]
-    r2 = create_weighted_image(pos, hs, m, T, (G, G), 64, 2, *ext)
-    o0, o1 = oracle.project_scatter(pos[:, 0], pos[:, 1], hs, a0, m, (G, G), 64, *ext)
-    with np.errstate(divide="ignore", invalid="ignore"):
-        ratio_want = np.where(o1 != 0, o0 / o1, 0.0)
-    np.testing.assert_array_equal(r2 == 0, ratio_want == 0)
-    np.testing.assert_allclose(r2, ratio_want, rtol=2e-4, atol=0)
-    # a clump: split tiles inside chunks
-    rng = np.random.default_rng(22)
-    cl = np.asarray(rng.normal(0, 0.01, (200_000, 3)), np.float32).astype(np.float64)
-    hc = np.full(200_000, 0.004)
-    Ac = np.asarray(rng.uniform(0.5, 1.5, 200_000), np.float32).astype(np.float64)
-    img = create_image(cl, hc, Ac, (512, 512), 64, 2, -1.0, 1.0, -1.0, 1.0)
-    assert stats(0)["merges"] > 0
-    ref, _ = oracle.project_scatter(cl[:, 0], cl[:, 1], hc, Ac, None, (512, 512), 64,
-                                    -1.0, 1.0, -1.0, 1.0)
-    assert_map_close(img, ref)
+    dr, d0, d1 = create_weighted_image(pos, h, A, T, (G, G), 64, 2, *ext, return_components=True,
+                                       deterministic=True)
+    assert_map_close(d0, w0)
+    assert_map_close(d1, w1)
 
 
 def test_speculative_scatter_grow_and_reuse(gpu, oracle, monkeypatch):
@@ -485,37 +457,53 @@ def test_unaligned_inputs_and_ragged_batches(gpu, oracle, n):
     assert_map_close(a1.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("n,G,h_law,kernel", [(200_000, 512, "physical", "cubic"),
-                                              (50_000, 300, "physical", "wendland_c2"),
-                                              (100_000, 512, "pixel", "cubic")])
-def test_gathered_large_records(gpu, oracle, monkeypatch, n, G, h_law, kernel):
-    """ASP_GATHER=1: large-box records are gathered per pixel from an LDS list (register
-    sums) instead of swept with LDS atomics.  Same decision logic, so neighbour counts
-    stay bit-exact; values within the stated tolerance; the weighted map as well.  The
-    G3 fixture (the reference's own output) is checked through the same path."""
-    from asp_amd.tools.projections import (create_image, create_weighted_image,
-                                           indicator_kernel, quartic_spline_kernel,
-                                           wendland_c2_kernel)
-    monkeypatch.setenv("ASP_GATHER", "1")
-    p = plummer_f32(n, seed=n + 7, h_law=h_law, grid=G)
-    ext = (-4.0, 4.0, -4.0, 4.0)
-    kf = {"cubic": quartic_spline_kernel, "wendland_c2": wendland_c2_kernel}[kernel]
-    img = create_image(p["pos"], p["h"], p["m"], (G, G), 64, 2, *ext, kernel_func=kf)
-    ref, _ = oracle.project_scatter(p["pos"][:, 0], p["pos"][:, 1], p["h"], p["m"], None, (G, G),
-                                    64, *ext, kernel=kernel)
-    assert_map_close(img, ref)
-    cnt = create_image(p["pos"], p["h"], np.ones(n), (G, G), 64, 2, *ext,
-                       kernel_func=indicator_kernel)
-    want, _ = oracle.project_scatter(p["pos"][:, 0], p["pos"][:, 1], p["h"], np.ones(n), None,
-                                     (G, G), 64, *ext, kernel="indicator")
-    assert np.array_equal(cnt, want)
-    w = create_weighted_image(p["pos"], p["h"], p["m"], p["T"], (G, G), 64, 2, *ext,
-                              kernel_func=kf)
-    r0, r1 = oracle.project_scatter(p["pos"][:, 0], p["pos"][:, 1], p["h"], p["m"] * p["T"],
-                                    p["m"], (G, G), 64, *ext, kernel=kernel)
-    with np.errstate(divide="ignore", invalid="ignore"):
-        wref = np.where(r1 != 0, r0 / r1, 0.0)
-    np.testing.assert_array_equal(w == 0, wref == 0)
-    np.testing.assert_allclose(w, wref, rtol=2e-4, atol=0)
-    pos, h, A, size, cs, ext3, g3ref = g3()
-    assert_map_close(create_image(pos, h, A, size, cs, 2, *ext3), g3ref)
+# ------------------------------------------------------------------ kernel_func plugin
+def wendland_c2_numpy(r, h):
+    """The same NumPy callable tests/golden/make_golden.py handed the reference for G6."""
+    r = np.asarray(r, dtype=np.float64)
+    h = np.asarray(h, dtype=np.float64)
+    q = r / h
+    t = np.clip(1.0 - 0.5 * q, 0.0, None)
+    return np.where(q < 2.0, 21.0 / (16.0 * np.pi * h ** 3) * t ** 4 * (1.0 + 2.0 * q), 0.0)
+
+
+def test_plugin_g6_generic_callable(gpu, monkeypatch):
+    """G6 (the reference run with a NumPy Wendland-C2 through its kernel_func plugin
+    point, _projector.py:86 / .pyx:33) reproduced by handing create_image the same
+    Python callable: the device produces the neighbour pairs and the reference's fp64
+    r, the callable runs on the host.  Small pair batches force several device calls."""
+    from asp_amd.tools.projections import _plugin, create_image
+    monkeypatch.setattr(_plugin, "MAX_PAIRS", 1 << 22)
+    pos, h, A, size, cs, ext, _ = g3()
+    ref = golden("g6_wendland_c2.npz")["img"]
+    calls = []
+
+    def kern(r, hh):
+        calls.append(r.size)
+        return wendland_c2_numpy(r, hh)
+
+    img = create_image(pos, h, A, size, cs, 2, *ext, kernel_func=kern)
+    assert len(calls) > 1
+    np.testing.assert_allclose(img, ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
+    assert np.array_equal(img != 0, ref != 0)
+
+
+def test_plugin_matches_native_kernels(gpu):
+    """A Python restatement of the cubic spline through the plugin path equals the
+    native kernel within the fp32 bar, on G3 (the reference's own output) and on a
+    weighted map."""
+    from asp_amd.tools.projections import create_image, create_weighted_image, quartic_spline_kernel
+
+    def cubic(r, hh):
+        q = r / hh
+        w = np.where(q < 1.0, 1 - 1.5 * q ** 2 + 0.75 * q ** 3,
+                     np.where(q < 2.0, 0.25 * (2 - q) ** 3, 0.0))
+        return w / (np.pi * hh ** 3)
+
+    pos, h, A, size, cs, ext, ref = g3()
+    img = create_image(pos, h, A, size, cs, 2, *ext, kernel_func=cubic)
+    np.testing.assert_allclose(img, ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
+    T = np.linspace(1.0, 2.0, h.size)
+    r1 = create_weighted_image(pos, h, A, T, size, cs, 2, *ext, kernel_func=cubic)
+    r2 = create_weighted_image(pos, h, A, T, size, cs, 2, *ext, kernel_func=quartic_spline_kernel)
+    np.testing.assert_allclose(r1, r2, rtol=2e-5)

@@ -164,3 +164,29 @@ def test_periodic_map_translation_invariance(gpu):
     m0 = create_periodic_image(pos, h, A, (G, G), 64, 2, L, c)
     m1 = create_periodic_image(pos, h, A, (G, G), 64, 2, L, c - np.array([k * L / G, 0.0, 0.0]))
     assert_map_close(np.roll(m0, k, axis=0), m1, abs_tol=1e-4, rel_tol=1e-3)
+
+
+def test_stage_periodic_images_large_h(gpu, oracle):
+    """Reach comparable to the box (2|h| up to 1.2 L): copies on both sides of an axis and
+    several box widths over, as the oracle's restatement enumerates them; the periodic
+    map then matches the oracle gather over that set.  Reach beyond 3 L is an error."""
+    from asp_amd.stage import stage_particles
+    from asp_amd.tools.projections import create_periodic_image
+    rng = np.random.default_rng(19)
+    L, n, G = 2.0, 3000, 48
+    pos = rng.uniform(0.0, L, (n, 3))
+    h = rng.uniform(0.01, 0.6 * L, n)
+    A = rng.uniform(0.5, 2.0, n)
+    want = oracle.stage_particles(pos, h, [A], 2, L=L, shift="wrap", images=True)
+    got = stage_particles(pos, h, A, projection_axis=2, box_width=L, shift="wrap", images=True)
+    got = [t.cpu().numpy() for t in (got[0], got[1], got[2], got[3][0])]
+    assert got[0].size == want[0].size > 3 * n
+    assert np.array_equal(_as_set([g[n:] for g in got]), _as_set([w[n:] for w in want]))
+    img = create_periodic_image(pos, h, A, (G, G), 16, 2, L)
+    st = np.stack([want[0], want[1], np.zeros_like(want[0])], axis=1).astype(np.float64)
+    ref = oracle.create_image(st, want[2].astype(np.float64), want[3].astype(np.float64),
+                              (G, G), 16, 2, 0.0, L, 0.0, L)
+    assert_map_close(img, ref)
+    h[0] = 2.0 * L  # 2|h| = 4 L
+    with pytest.raises(NotImplementedError):
+        stage_particles(pos, h, A, projection_axis=2, box_width=L, shift="wrap", images=True)

@@ -78,10 +78,17 @@ def test_kernel_plugin_resolution(asp):
 
     def quartic_spline_kernel_ref(r, h):
         return r
-    quartic_spline_kernel_ref.__name__ = "quartic_spline_kernel"  # the reference's object
-    assert kernel_id_of(quartic_spline_kernel_ref) == 0
+    # a callable that merely shares the reference kernel's name is NOT taken for the
+    # native kernel: every non-package callable goes to the plugin path (None)
+    quartic_spline_kernel_ref.__name__ = "quartic_spline_kernel"
+    assert kernel_id_of(quartic_spline_kernel_ref) is None
+    assert kernel_id_of(lambda r, h: r) is None
     with pytest.raises(TypeError):
-        kernel_id_of(lambda r, h: r)
+        kernel_id_of(3.0)
+    from asp_amd.tools.projections._kernels import native_kernel_id
+    with pytest.raises(TypeError):
+        native_kernel_id(lambda r, h: r)
+    assert native_kernel_id(wendland_c2_kernel) == 1
     with pytest.raises(ValueError, match="dtype"):
         quartic_spline_kernel(np.zeros(3, np.float32), np.ones(3))
     assert quartic_spline_kernel(np.zeros(0), np.zeros(0)).shape == (0,)
