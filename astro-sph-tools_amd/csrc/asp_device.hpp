@@ -46,7 +46,8 @@ struct Grid {
     double psy_cull;  // (y_max - y_min) / ny                        _projector.py:35
     float xminf, yminf;   // fp32 copies for the candidate-box estimate
     float ipsx, ipsy;     // fp32 reciprocal pitches (pixel pitches)
-    float mg;         // bound on |corner coordinate| in the frame of any decision (band)
+    float mg;         // bound on |corner coordinate|, absolute frame (error band)
+    float mgl;        // the same for the records' box-origin / tile frames (128 pitches)
     int nx, ny, cs;
     int ncx, ncy;     // reference chunks per axis
     int ntx, nty, ntiles;  // GPU tiles
@@ -54,6 +55,7 @@ struct Grid {
     int mixed;        // the cull reads other position columns than the pixel test (Src64)
     int wide_tiles;   // particles over more tiles than this take the wide path (K6)
     int gather_min;   // records with clipped boxes >= this on both axes are gathered (K4)
+    int gexp;         // experiment switch (temporary)
 };
 
 // The caller's particle arrays, resident in HBM, read by particle index where the exact
@@ -272,16 +274,16 @@ __device__ __forceinline__ float kernel_shape(float q) {
 }
 
 // Error band of a record: thr = (2h)^2 in fp32 and the band around it
-// inside which the fp32 decision is not trusted (+inf: every pair goes to fp64).  It
-// bounds the fp32 decision error in either frame: absolute corners (|X| <= M) or
-// tile-local ones (|X| <= 64 pitches), g.mg = the larger of the two bounds.
+// inside which the fp32 decision is not trusted (+inf: every pair goes to fp64).  mg
+// bounds the coordinates of the frame the decision is taken in: g.mg for absolute
+// corners (|X| <= M), g.mgl for the records' box-origin frame (offsets < 64 pitches).
 __device__ __forceinline__ float rec_thr(float h) {
     float D = 2.0f * h;
     return D * D;
 }
-__device__ __forceinline__ float rec_band(const Grid& g, float h) {
+__device__ __forceinline__ float rec_band(float mg, float h) {
     float Da = fabsf(2.0f * h);
-    float eps = 0x1p-21f * (g.mg + Da);
+    float eps = 0x1p-21f * (mg + Da);
     float band = 4.0f * Da * eps + 2.0f * eps * eps + 0x1p-20f * Da * Da;
     // Negative h narrows the chunk cull below the disc: decide every pair in fp64.
     if (h < 0.0f || !__builtin_isfinite(band)) band = __builtin_inff();
@@ -306,7 +308,7 @@ __device__ __forceinline__ bool prep_record(const Grid& g, const Src64& s, int p
     P.v = v;
     P.h = h;
     P.p = p;
-    set_band(P, rec_thr(h), rec_band(g, h));
+    set_band(P, rec_thr(h), rec_band(g.mg, h));
     P.hinv = __builtin_amdgcn_rcpf(h);  // value path only (fp32 tolerance)
     if constexpr (ACC == kAccFix) {
         P.s0 = (float)ldexp(term_coef<KID>(a0, h), k0);

@@ -119,10 +119,13 @@ __device__ __forceinline__ bool box_large(unsigned bp, int gmin) {
 }
 
 // Histogram column of a (particle, tile) insertion: t (small / mid-size stream) or
-// t + ntiles (large stream, gathered by K4g).
-__device__ __forceinline__ int column(const Grid& g, const Box& b, int tx, int ty) {
+// t + ntiles (large stream, gathered by K4g).  `maybe`: the unclipped box is large.
+__device__ __forceinline__ int column(const Grid& g, const Box& b, bool maybe, int tx, int ty) {
     const int t = tx * g.nty + ty;
-    return box_large(tile_box(b, tx, ty), g.gather_min) ? t + g.ntiles : t;
+    return maybe && box_large(tile_box(b, tx, ty), g.gather_min) ? t + g.ntiles : t;
+}
+__device__ __forceinline__ bool maybe_large(const Grid& g, const Box& b) {
+    return b.x1 - b.x0 + 1 >= g.gather_min && b.y1 - b.y0 + 1 >= g.gather_min;
 }
 
 // ----------------------------------------------------------------------------------
@@ -157,8 +160,9 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
                 ++nwide;
                 continue;
             }
+            const bool mb = maybe_large(g, b);
             for (int tx = tx0; tx <= tx1; ++tx)
-                for (int ty = ty0; ty <= ty1; ++ty) atomicAdd(&lh[column(g, b, tx, ty)], 1);
+                for (int ty = ty0; ty <= ty1; ++ty) atomicAdd(&lh[column(g, b, mb, tx, ty)], 1);
         }
 #pragma unroll
         for (int k = 0; k < kCountUnroll; ++k) {
@@ -276,7 +280,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                 }
                 continue;
             }
-            const float band = rec_band(g, ph[k]);
+            const float band = rec_band(g.mgl, ph[k]);  // decided in the box-origin frame
             // coordinates relative to the record's box origin, from the exact inputs: the
             // deposit's pair arithmetic then carries 2^-24 of the pair distance, not of |u|
             // 
@@ -286,11 +290,12 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             first_band[k] = band;
             first_lu[k] = (float)(U - corner_x(g, max(b.x0, tx0 * kTile)));
             first_lv[k] = (float)(V - corner_y(g, max(b.y0, ty0 * kTile)));
+            const bool mb = maybe_large(g, b);
             for (int tx = tx0; tx <= tx1; ++tx)
                 for (int ty = ty0; ty <= ty1; ++ty) {
                     const int t = tx * g.nty + ty;
                     const unsigned bp = tile_box(b, tx, ty);
-                    const int col = box_large(bp, g.gather_min) ? t + g.ntiles : t;
+                    const int col = mb && box_large(bp, g.gather_min) ? t + g.ntiles : t;
                     int slot = atomicAdd(&cur[col], 1);
                     if constexpr (ACC == kAccFix) {
                         atomicMax(&cm[t * NOUT], c0);
@@ -717,71 +722,92 @@ __device__ __forceinline__ void deferred(const Grid& g, const Src64& s,
 }
 
 // ----------------------------------------------------------------------------------
-// Gather form for large boxes (K4g, K6).  A sweep costs two LDS atomics per pair; here a
-// block's large records go to an LDS list and every thread OWNS 8 pixels of the tile --
-// wave w rows 8w .. 8w+7, lane l row 8w + l/8, columns 8 (l % 8) .. + 7 -- tests each
-// list entry against them (a wave skips entries whose box misses its 8 rows) and sums the
-// terms in registers: fp32 partials over <= kFoldEvery entries folded into fp64 totals
-// (or exact int64 fixed point).  No atomics, no LDS tile.
+// Gather form for mid and large boxes (K4g, K6).  A sweep costs an LDS atomic per pair
+// and a pass per 64 box pixels; here every thread OWNS 8 pixels of the tile and sums
+// their terms in registers.  Wave w owns the 16 x 32 region rows 16 (w / 2) .., columns
+// 32 (w % 2) .., as 2 x 4 blocks of 8 x 8 pixels; lane l owns pixel (l / 8, l % 8) of
+// each block (block j: block row j / 4, block column j % 4).  Each wave streams the
+// item's records itself, 64 at a time (lane i prepares record i into a GEntry held in
+// VGPRs), ballots which of them meet its region and walks those: v_readlane puts the
+// entry's fields in SGPRs, the blocks the box meets are found with scalar compares, and
+// only those blocks' pixels are evaluated -- one pixel per lane per block, so an entry
+// costs ~ its box area / 64 wave instructions-per-pixel, whatever its size.  No LDS list,
+// no block barrier, no atomics.  Sums: fp32 partials over <= 64 entries folded into fp64
+// totals the thread owns in LDS (kAccF64), or exact int64 fixed point in registers
+// (kAccFix).
 // ----------------------------------------------------------------------------------
-constexpr int kFoldEvery = 128;
-
-struct GEntry {  // 40 B; every lane reads the same entry (LDS broadcast)
-    float u, v, h, lo, hi, hinv, s0, s1;
+constexpr int kGatherThreads = 64;  // one wave per workgroup: one region of the tile
+constexpr int kGatherRegions = 8;   // 16 x 32-pixel regions per tile
+constexpr int kGatherPix = 8 * kGatherThreads;
+static_assert(kGatherRegions * kGatherPix == kTile * kTile, "8 regions x 512 pixels cover the tile");
+constexpr int kKernelIndicator = ASP_KERNEL_INDICATOR;
+struct GEntry {
+    float u, v, lo, hi, hinv, s0, s1;  // tile frame; s0, s1 with the shape's scale folded in
     int p;
-    unsigned box;  // tile-local x0 | x1 << 8 | y0 << 16 | y1 << 24
+    unsigned box;  // tile-local x0 | x1 << 8 | y0 << 16 | y1 << 24 (kNoBox: nothing)
 };
+constexpr unsigned kNoBox = 0x00ff00ffu;  // x0 = 255 > x1 = 0: meets no region
 
-__device__ __forceinline__ GEntry make_gentry(const Prep& P, int X0, int Y0) {
-    GEntry e;
-    e.u = P.u; e.v = P.v; e.h = P.h; e.lo = P.lo; e.hi = P.hi; e.hinv = P.hinv;
-    e.s0 = P.s0; e.s1 = P.s1; e.p = P.p;
-    e.box = (unsigned)(P.b.x0 - X0) | ((unsigned)(P.b.x1 - X0) << 8) |
-            ((unsigned)(P.b.y0 - Y0) << 16) | ((unsigned)(P.b.y1 - Y0) << 24);
-    return e;
+// Shape f(q) / kShapeScale for kernels that vanish continuously at q = 2 (cubic,
+// Wendland), written so that q >= 2 gives exactly 0 without a comparison:
+// t = max(1 - q/2, 0).  Cubic: (2 - q)^3 / 4 = 2 t^3, the inner branch halved to match.
+template <int KID>
+constexpr float kShapeScale = KID == 0 ? 2.0f : 1.0f;
+template <int KID>
+__device__ __forceinline__ float edge_shape(float q) {
+    const float t = fmaxf(fmaf(-0.5f, q, 1.0f), 0.0f);
+    if constexpr (KID == 0) {
+        const float a = fmaf(q * q, fmaf(0.375f, q, -0.75f), 0.5f);  // (1 - 1.5q^2 + .75q^3)/2
+        return q < 1.0f ? a : t * t * t;
+    } else {
+        const float t2 = t * t;
+        return (t2 * t2) * fmaf(2.0f, q, 1.0f);
+    }
 }
 
 // One thread's 8 pixels: fp32 partials in registers folded into fp64 totals that the
-// thread owns in LDS (kAccF64), or exact int64 fixed-point sums in registers (kAccFix).
+// thread owns in LDS (kAccF64; word j * 64 + lane: conflict-free), or exact int64
+// fixed-point sums in registers (kAccFix).
 template <int NOUT, int ACC>
 struct GAcc {
     using T = typename std::conditional<ACC == kAccFix, unsigned long long, float>::type;
     T a0[8], a1[8];
-    double* t0;  // this thread's 8 consecutive LDS totals per map (kAccF64)
+    double* t0;
     double* t1;
-    __device__ __forceinline__ void init(double* tot, int k) {
+    __device__ __forceinline__ void init(double* tot) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             a0[j] = 0;
             a1[j] = 0;
         }
-        t0 = tot + k;
-        t1 = tot + kTile * kTile + k;
+        t0 = tot + threadIdx.x;
+        t1 = tot + kGatherPix + threadIdx.x;
         if constexpr (ACC != kAccFix) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                t0[j] = 0.0;
-                if (NOUT == 2) t1[j] = 0.0;
+                t0[j * kGatherThreads] = 0.0;
+                if (NOUT == 2) t1[j * kGatherThreads] = 0.0;
             }
         }
     }
-    __device__ __forceinline__ void add(int j, float x0, float x1) {
+    // pixel j += w * (s0, s1)
+    __device__ __forceinline__ void add(int j, float w, float s0, float s1) {
         if constexpr (ACC == kAccFix) {
-            a0[j] += f2fix(x0);
-            if (NOUT == 2) a1[j] += f2fix(x1);
+            a0[j] += f2fix(s0 * w);
+            if (NOUT == 2) a1[j] += f2fix(s1 * w);
         } else {
-            a0[j] += x0;
-            if (NOUT == 2) a1[j] += x1;
+            a0[j] = fmaf(s0, w, a0[j]);
+            if (NOUT == 2) a1[j] = fmaf(s1, w, a1[j]);
         }
     }
     __device__ __forceinline__ void fold() {
         if constexpr (ACC != kAccFix) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                t0[j] += (double)a0[j];
+                t0[j * kGatherThreads] += (double)a0[j];
                 a0[j] = 0.0f;
                 if (NOUT == 2) {
-                    t1[j] += (double)a1[j];
+                    t1[j * kGatherThreads] += (double)a1[j];
                     a1[j] = 0.0f;
                 }
             }
@@ -790,76 +816,217 @@ struct GAcc {
     // the accumulator word of pixel j (as the LDS tile / slabs hold it)
     __device__ __forceinline__ unsigned long long word0(int j) const {
         if constexpr (ACC == kAccFix) return a0[j];
-        else return (unsigned long long)__double_as_longlong(t0[j]);
+        else return (unsigned long long)__double_as_longlong(t0[j * kGatherThreads]);
     }
     __device__ __forceinline__ unsigned long long word1(int j) const {
         if constexpr (ACC == kAccFix) return a1[j];
-        else return (unsigned long long)__double_as_longlong(t1[j]);
+        else return (unsigned long long)__double_as_longlong(t1[j * kGatherThreads]);
     }
 };
 
-// LDS of K4g / K6: the fp64 totals (one word per pixel and map), then the list.
-constexpr int kGatherBatch = 256;  // list entries (records per K4g batch)
+// LDS of K4g / K6: the fp64 totals, one word per pixel and map (none in fixed point).
 template <int NOUT, int ACC>
 constexpr size_t gather_lds() {
-    return (ACC == kAccFix ? 0 : (size_t)NOUT * kTile * kTile * 8) + (size_t)kGatherBatch * 40;
+    return ACC == kAccFix ? 8 : (size_t)NOUT * kGatherPix * 8;
 }
 
-// One list entry against this thread's 8 pixels (row lx, columns ly0 .. ly0 + 7).
-template <int KID, int NOUT, int ACC>
-__device__ __forceinline__ void gather_entry(const Grid& g, const Src64& s, const GEntry& E,
-                                             int X0, int Y0, int lx, int ly0, float X,
-                                             const float* Yc, GAcc<NOUT, ACC>& ga) {
-    const int x0 = E.box & 255u, x1 = (E.box >> 8) & 255u;
-    const int y0 = (E.box >> 16) & 255u, y1 = E.box >> 24;
-    if (lx < x0 || lx > x1 || ly0 + 7 < y0 || ly0 > y1) return;
-    const float dx = E.u - X;
-    const float dx2 = dx * dx;
-    if (dx2 > E.hi) return;  // r2 >= dx2 > hi for the whole row: outside
-    unsigned amb = 0u;
+// This thread's pixels: pixel j at row r0 + 8 (j / 4) + lr, column c0 + 8 (j % 4) + lc.
+struct GOwn {
+    int r0, c0;  // the wave's region (uniform)
+    int lr, lc;  // the lane's place in each 8 x 8 block
+    __device__ __forceinline__ int row(int j) const { return r0 + 8 * (j >> 2) + lr; }
+    __device__ __forceinline__ int col(int j) const { return c0 + 8 * (j & 3) + lc; }
+};
+__device__ __forceinline__ GOwn gather_owner(int w) {  // w: the region (uniform)
+    const int lane = threadIdx.x;
+    GOwn o;
+    o.r0 = (w >> 1) * 16;
+    o.c0 = (w & 1) * 32;
+    o.lr = lane >> 3;
+    o.lc = lane & 7;
+    return o;
+}
+
+// Tile-local corner offsets fl32(k * pitch): the values of the corner tables (K4), here
+// computed where they are needed (a gather workgroup has no tables).
+__device__ __forceinline__ float corner_off_x(const Grid& g, int k) { return (float)((double)k * g.psx); }
+__device__ __forceinline__ float corner_off_y(const Grid& g, int k) { return (float)((double)k * g.psy_pix); }
+
+// The corner coordinates of the thread's pixels: 2 rows, 4 columns.
+struct GCorner {
+    float X[2], Y[4];
+};
+__device__ __forceinline__ GCorner gather_corners(const Grid& g, const GOwn& o) {
+    GCorner c;
+    c.X[0] = corner_off_x(g, o.row(0));
+    c.X[1] = corner_off_x(g, o.row(4));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c.Y[k] = corner_off_y(g, o.col(k));
+    return c;
+}
+
+__device__ __forceinline__ GEntry make_gentry(const Prep& P, int X0, int Y0, float scale) {
+    GEntry e;
+    e.u = P.u; e.v = P.v; e.lo = P.lo; e.hi = P.hi; e.hinv = P.hinv;
+    e.s0 = P.s0 * scale; e.s1 = P.s1 * scale; e.p = P.p;
+    e.box = (unsigned)(P.b.x0 - X0) | ((unsigned)(P.b.x1 - X0) << 8) |
+            ((unsigned)(P.b.y0 - Y0) << 16) | ((unsigned)(P.b.y1 - Y0) << 24);
+    return e;
+}
+
+__device__ __forceinline__ bool meets_region(unsigned box, const GOwn& o) {
+    return (int)(box & 255u) <= o.r0 + 15 && (int)((box >> 8) & 255u) >= o.r0 &&
+           (int)((box >> 16) & 255u) <= o.c0 + 31 && (int)(box >> 24) >= o.c0;
+}
+
+// Lane l's entry, wave-uniform (SGPRs).
+__device__ __forceinline__ GEntry lane_entry(const GEntry& e, int l) {
+    GEntry E;
+    E.u = bcast(e.u, l); E.v = bcast(e.v, l); E.lo = bcast(e.lo, l); E.hi = bcast(e.hi, l);
+    E.hinv = bcast(e.hinv, l); E.s0 = bcast(e.s0, l); E.s1 = bcast(e.s1, l);
+    E.p = bcast(e.p, l); E.box = (unsigned)bcast((int)e.box, l);
+    return E;
+}
+
+// Which of the wave's 8 blocks the box meets (bit j; uniform).
+__device__ __forceinline__ unsigned block_hits(unsigned box, const GOwn& o) {
+    const int x0 = box & 255u, x1 = (box >> 8) & 255u;
+    const int y0 = (box >> 16) & 255u, y1 = box >> 24;
+    unsigned m = 0u;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const bool col = ly0 + j >= y0 && ly0 + j <= y1;
-        const float dy = E.v - Yc[j];
-        const float r2 = dx2 + dy * dy;
-        const bool in = col && r2 < E.lo;
-        amb |= (col && r2 >= E.lo && r2 <= E.hi) ? (1u << j) : 0u;
-        const float w = in ? kernel_shape<KID>(__builtin_amdgcn_sqrtf(r2) * E.hinv) : 0.0f;
-        ga.add(j, E.s0 * w, E.s1 * w);
+        const int br = o.r0 + 8 * (j >> 2), bc = o.c0 + 8 * (j & 3);
+        if (x0 <= br + 7 && x1 >= br && y0 <= bc + 7 && y1 >= bc) m |= 1u << j;
     }
-    if (amb) {  // band pairs (rare): the reference's fp64 decision, one call site
-        unsigned ok = 0u;
-        for (unsigned m = amb; m; m &= m - 1u) {
-            const int j = __builtin_ctz(m);
-            if (exact_pair(g, s, E.p, X0 + lx, Y0 + ly0 + j)) ok |= 1u << j;
-        }
-        if (ok) {
+    return m;
+}
+
+// One (uniform) entry, edge-continuous kernel (cubic / Wendland) on a square grid
+// without a mixed cull: W by edge_shape for every pixel of every block the box meets --
+// no decision at all.  A pixel the reference excludes has exact r >= 2h, so its fp32 q is
+// >= 2 (1 - 2^-21) and its term 0 or < 2^-60 W(0); one it includes the same way.  Pixels
+// of a met block outside the box have r >= 2h as well (the box is a superset of the disc).
+template <int KID, int NOUT, int ACC>
+__device__ __forceinline__ void gather_entry_edge(const GEntry& E, const GOwn& o,
+                                                  const GCorner& c, GAcc<NOUT, ACC>& ga, int gexp) {
+    const float vs = E.v * E.hinv;  // in units of h
+    if (gexp == 1) {  // both block rows, no branch
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {  // static indices: the sums stay in registers
-                if (!(ok & (1u << j))) continue;
-                const float dy = E.v - Yc[j];
-                const float w =
-                    kernel_shape<KID>(__builtin_amdgcn_sqrtf(dx2 + dy * dy) * E.hinv);
-                ga.add(j, E.s0 * w, E.s1 * w);
+        for (int r = 0; r < 2; ++r) {
+            const float dxs = (E.u - c.X[r]) * E.hinv;
+            const float dx2 = dxs * dxs;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float dys = fmaf(-E.hinv, c.Y[k], vs);
+                const float q = __builtin_amdgcn_sqrtf(fmaf(dys, dys, dx2));
+                ga.add(4 * r + k, edge_shape<KID>(q), E.s0, E.s1);
+            }
+        }
+        return;
+    }
+    // A met block row is evaluated whole (4 independent pixels in flight): a pixel
+    // outside the box contributes exactly 0 there, as above.  (The box meets the wave's
+    // region, so it meets a block row iff its rows do.)
+    const int x0 = E.box & 255u, x1 = (E.box >> 8) & 255u;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int br = o.r0 + 8 * r;
+        if (x0 <= br + 7 && x1 >= br) {
+            const float dxs = (E.u - c.X[r]) * E.hinv;
+            const float dx2 = dxs * dxs;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float dys = fmaf(-E.hinv, c.Y[k], vs);
+                const float q = __builtin_amdgcn_sqrtf(fmaf(dys, dys, dx2));
+                ga.add(4 * r + k, edge_shape<KID>(q), E.s0, E.s1);
             }
         }
     }
 }
 
-// The first nl entries of the LDS list against this thread's pixels.
+// One (uniform) entry, every other case: the box's own rows and columns (non-square grids
+// and mixed culls clip the box to the chunk ranges), the error band and the fp64
+// decision -- the indicator kernel's neighbour sets are the reference's exactly.
 template <int KID, int NOUT, int ACC>
-__device__ __forceinline__ void gather_list(const Grid& g, const Src64& s, const GEntry* list,
-                                            int nl, int X0, int Y0, int lx, int ly0, float X,
-                                            const float* Yc, GAcc<NOUT, ACC>& ga) {
-    const int w0 = (threadIdx.x >> 6) * 8;  // this wave's first row
-    for (int e0 = 0; e0 < nl; e0 += kFoldEvery) {
-        const int e1 = min(nl, e0 + kFoldEvery);
-        for (int e = e0; e < e1; ++e) {
-            const unsigned bx = list[e].box;  // wave-uniform reject on the wave's rows
-            if ((int)(bx & 255u) > w0 + 7 || (int)((bx >> 8) & 255u) < w0) continue;
-            gather_entry<KID, NOUT, ACC>(g, s, list[e], X0, Y0, lx, ly0, X, Yc, ga);
+__device__ __forceinline__ void gather_entry(const Grid& g, const Src64& s, const GEntry& E,
+                                             int X0, int Y0, const GOwn& o, const GCorner& c,
+                                             GAcc<NOUT, ACC>& ga) {
+    const unsigned m = block_hits(E.box, o);
+    const int x0 = E.box & 255u, x1 = (E.box >> 8) & 255u;
+    const int y0 = (E.box >> 16) & 255u, y1 = E.box >> 24;
+    unsigned in = 0u, amb = 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (m & (1u << j)) {
+            const float dx = E.u - c.X[j >> 2], dy = E.v - c.Y[j & 3];
+            const float r2 = dx * dx + dy * dy;
+            const bool inb = (unsigned)(o.row(j) - x0) <= (unsigned)(x1 - x0) &&
+                             (unsigned)(o.col(j) - y0) <= (unsigned)(y1 - y0);
+            in |= (inb && r2 < E.lo) ? (1u << j) : 0u;
+            amb |= (inb && r2 >= E.lo && r2 <= E.hi) ? (1u << j) : 0u;
         }
-        ga.fold();
+    }
+    for (unsigned a = amb; a; a &= a - 1u) {  // the reference's fp64 decision, one call site
+        const int j = __builtin_ctz(a);
+        if (exact_pair(g, s, E.p, X0 + o.row(j), Y0 + o.col(j))) in |= 1u << j;
+    }
+    const float sc = 1.0f / kShapeScale<KID>;  // s0, s1 carry the edge form's scale
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (in & (1u << j)) {  // (the same r2 as above: same operations)
+            const float dx = E.u - c.X[j >> 2], dy = E.v - c.Y[j & 3];
+            const float r2 = dx * dx + dy * dy;
+            const float wk = kernel_shape<KID>(__builtin_amdgcn_sqrtf(r2) * E.hinv) * sc;
+            ga.add(j, wk, E.s0, E.s1);
+        }
+    }
+}
+
+// The wave's walk over its lanes' entries: those whose box meets the wave's region.
+template <int KID, int NOUT, int ACC>
+__device__ __forceinline__ void gather_walk(const Grid& g, const Src64& s, const GEntry& mine,
+                                            int X0, int Y0, const GOwn& o, const GCorner& c,
+                                            GAcc<NOUT, ACC>& ga) {
+    unsigned long long m = __ballot(meets_region(mine.box, o));
+    if (KID != kKernelIndicator && !g.nonsquare && !g.mixed) {  // uniform
+        while (m) {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            gather_entry_edge<KID, NOUT, ACC>(lane_entry(mine, l), o, c, ga, g.gexp);
+        }
+    } else {
+        while (m) {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            gather_entry<KID, NOUT, ACC>(g, s, lane_entry(mine, l), X0, Y0, o, c, ga);
+        }
+    }
+    ga.fold();
+}
+
+// Write the thread's 8 pixels: partial slab (split tiles) or the map.
+template <int NOUT, int ACC>
+__device__ __forceinline__ void gather_emit(const Grid& g, const GAcc<NOUT, ACC>& ga,
+                                            const GOwn& o, int X0, int Y0, int slab,
+                                            unsigned long long* slabs, int k0, int k1,
+                                            float* out0, float* out1, int flags) {
+    if (slab >= 0) {  // unpadded slab layout
+        unsigned long long* dst = slabs + (long long)slab * NOUT * kTilePix;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = o.row(j) * kTile + o.col(j);
+            dst[k] = ga.word0(j);
+            if (NOUT == 2) dst[kTilePix + k] = ga.word1(j);
+        }
+        return;
+    }
+    const int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (o.row(j) >= TW || o.col(j) >= TH) continue;
+        const long long off = (long long)(X0 + o.row(j)) * g.ny + (Y0 + o.col(j));
+        emit_pixel<NOUT, ACC>(off, ga.word0(j), NOUT == 2 ? ga.word1(j) : 0ull, k0, k1, out0,
+                              out1, flags);
     }
 }
 
@@ -983,69 +1150,44 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
 
 // ----------------------------------------------------------------------------------
 // K4g: deposit one work item of the LARGE stream (records whose clipped box is at least
-// gather_min pixels on both axes): 256 records at a time into the LDS list (coalesced
-// 32-B loads, the next batch in flight), then every wave walks the list (gather_list).
-// The tile (or its partial slab) is written straight from the registers.
+// gather_min pixels on both axes) in the gather form: every wave streams the item's
+// records 64 at a time (coalesced 32-B loads, the next 64 in flight) and walks those that
+// meet its region (gather_walk).  The tile (or its partial slab) is written straight
+// from the registers.
 // ----------------------------------------------------------------------------------
 template <int KID, int NOUT, int ACC>
-__global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_gather(
+__global__ __launch_bounds__(kGatherThreads) void k_gather(
     Grid g, Src64 s, const float4* __restrict__ recs, const Item* __restrict__ items,
     const int2* __restrict__ tile_k, unsigned long long* __restrict__ slabs,
     float* __restrict__ out0, float* __restrict__ out1, int flags) {
-    __shared__ float xt[kTile], yt[kTile];
     extern __shared__ __attribute__((aligned(16))) double tot[];
-    GEntry* list = (GEntry*)(tot + (ACC == kAccFix ? 0 : NOUT * kTilePix));
-    const Item it = items[blockIdx.x];
+    const Item it = items[blockIdx.x / kGatherRegions];
     if (it.mode != 1) return;
     const int tx = it.tile / g.nty, ty = it.tile - (it.tile / g.nty) * g.nty;
     const int X0 = tx * kTile, Y0 = ty * kTile;
-    const int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
     const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
-    corner_tables(g, X0, Y0, xt, yt);
+    const int lane = threadIdx.x;
     float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
-    if ((int)threadIdx.x < min(it.count, kGatherBatch)) load_rec(recs, it.start + threadIdx.x, r0, r1);
-    const int lane = threadIdx.x & 63;
-    const int lx = (threadIdx.x >> 6) * 8 + (lane >> 3), ly0 = (lane & 7) * 8;
+    if (lane < it.count) load_rec(recs, it.start + lane, r0, r1);
+    const GOwn o = gather_owner(blockIdx.x % kGatherRegions);
     GAcc<NOUT, ACC> ga;
-    ga.init(tot, lx * kTile + ly0);
-    __syncthreads();
-    const float X = xt[lx];
-    float Yc[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) Yc[j] = yt[ly0 + j];
-    for (int base = 0; base < it.count; base += kGatherBatch) {
-        const int nl = min(kGatherBatch, it.count - base);
-        if ((int)threadIdx.x < nl) {
+    ga.init(tot);
+    const GCorner cc = gather_corners(g, o);
+    for (int base = 0; base < it.count; base += 64) {
+        GEntry mine;
+        mine.box = kNoBox;
+        if (base + lane < it.count) {
             Prep P;
             rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
-            P.u += xt[P.b.x0 - X0];  // box-origin frame -> tile frame
-            P.v += yt[P.b.y0 - Y0];
-            list[threadIdx.x] = make_gentry(P, X0, Y0);
+            P.u += corner_off_x(g, P.b.x0 - X0);  // box-origin frame -> tile frame
+            P.v += corner_off_y(g, P.b.y0 - Y0);
+            mine = make_gentry(P, X0, Y0, kShapeScale<KID>);
         }
-        r0 = r1 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if ((int)threadIdx.x < kGatherBatch && base + kGatherBatch + (int)threadIdx.x < it.count)
-            load_rec(recs, it.start + base + kGatherBatch + threadIdx.x, r0, r1);
-        __syncthreads();
-        gather_list<KID, NOUT, ACC>(g, s, list, nl, X0, Y0, lx, ly0, X, Yc, ga);
-        __syncthreads();  // the list is rewritten next batch
+        // the next 64 records load while this batch is walked
+        if (base + 64 + lane < it.count) load_rec(recs, it.start + base + 64 + lane, r0, r1);
+        gather_walk<KID, NOUT, ACC>(g, s, mine, X0, Y0, o, cc, ga);
     }
-    if (it.slab >= 0) {  // split tile: partial sums, merged by K5 (unpadded slab layout)
-        unsigned long long* dst = slabs + (long long)it.slab * NOUT * kTilePix + lx * kTile + ly0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            dst[j] = ga.word0(j);
-            if (NOUT == 2) dst[kTilePix + j] = ga.word1(j);
-        }
-        return;
-    }
-    if (lx >= TW) return;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        if (ly0 + j >= TH) continue;
-        const long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly0 + j);
-        emit_pixel<NOUT, ACC>(o, ga.word0(j), NOUT == 2 ? ga.word1(j) : 0ull, kk.x, kk.y, out0,
-                              out1, flags);
-    }
+    gather_emit<NOUT, ACC>(g, ga, o, X0, Y0, it.slab, slabs, kk.x, kk.y, out0, out1, flags);
 }
 
 // ----------------------------------------------------------------------------------
@@ -1096,43 +1238,35 @@ __global__ __launch_bounds__(kBlock) void k_merge(Grid g, const Merge* __restric
 
 // ----------------------------------------------------------------------------------
 // K6: wide particles (footprint over > wide_tiles tiles): they are never binned.  One
-// workgroup per tile walks the wide list kGatherBatch particles at a time, keeps those whose
-// clipped box meets the tile (compacted into the LDS list) and gathers them as K4g does;
+// workgroup per tile; every wave streams the wide list 64 particles at a time, prepares
+// them (prep_record + clip to the tile) and gathers those meeting its region as K4g does;
 // fixed point with the wide particles' own bound.  Adds onto the tile K4/K4g/K5 wrote.
 // ----------------------------------------------------------------------------------
 template <int KID, int NOUT, int ACC>
-__global__ __launch_bounds__(kDepBlock) void k_wide(
+__global__ __launch_bounds__(kGatherThreads) void k_wide(
     Grid g, Src64 s, const float* __restrict__ u, const float* __restrict__ v,
     const float* __restrict__ h, const float* __restrict__ a0, const float* __restrict__ a1,
     const int* __restrict__ wide_list, int n_wide, const int* __restrict__ ctr,
     float* __restrict__ out0, float* __restrict__ out1) {
-    __shared__ float xt[kTile], yt[kTile];
-    __shared__ int s_n;
     extern __shared__ __attribute__((aligned(16))) double tot[];
-    GEntry* list = (GEntry*)(tot + (ACC == kAccFix ? 0 : NOUT * kTilePix));
-    const int t = blockIdx.x;
+    const int t = blockIdx.x / kGatherRegions;
     const int tx = t / g.nty, ty = t - (t / g.nty) * g.nty;
     const int X0 = tx * kTile, Y0 = ty * kTile;
     const int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
-    corner_tables(g, X0, Y0, xt, yt);
     const int k0 = ACC == kAccFix ? scale_exp(n_wide, __uint_as_float((unsigned)ctr[cWideMax0])) : 0;
     const int k1 = (ACC == kAccFix && NOUT == 2)
                        ? scale_exp(n_wide, __uint_as_float((unsigned)ctr[cWideMax1])) : 0;
-    const int lane = threadIdx.x & 63;
-    const int lx = (threadIdx.x >> 6) * 8 + (lane >> 3), ly0 = (lane & 7) * 8;
+    const int lane = threadIdx.x;
+    const GOwn o = gather_owner(blockIdx.x % kGatherRegions);
     GAcc<NOUT, ACC> ga;
-    ga.init(tot, lx * kTile + ly0);
-    __syncthreads();
-    const float X = xt[lx];
-    float Yc[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) Yc[j] = yt[ly0 + j];
-    bool any = false;
-    for (int c = 0; c < n_wide; c += kGatherBatch) {
-        if (threadIdx.x == 0) s_n = 0;
-        __syncthreads();
-        const int k = c + (int)threadIdx.x;
-        if ((int)threadIdx.x < kGatherBatch && k < n_wide) {
+    ga.init(tot);
+    const GCorner cc = gather_corners(g, o);
+    bool any = false;  // wave-uniform
+    for (int c = 0; c < n_wide; c += 64) {
+        GEntry mine;
+        mine.box = kNoBox;
+        const int k = c + lane;
+        if (k < n_wide) {
             const int p = wide_list[k];
             Prep P;
             if (prep_record<KID, ACC>(g, s, p, u[p], v[p], h[p], a0[p], NOUT == 2 ? a1[p] : 0.0f,
@@ -1140,23 +1274,14 @@ __global__ __launch_bounds__(kDepBlock) void k_wide(
                 clip(P.b, X0, Y0, TW, TH)) {
                 P.u = (float)(src_u(s, p, P.u) - corner_x(g, X0));  // tile-local frame
                 P.v = (float)(src_v(s, p, P.v) - corner_y(g, Y0));
-                list[atomicAdd(&s_n, 1)] = make_gentry(P, X0, Y0);
+                mine = make_gentry(P, X0, Y0, kShapeScale<KID>);
             }
         }
-        __syncthreads();
-        const int nl = s_n;
-        any = any || nl > 0;
-        gather_list<KID, NOUT, ACC>(g, s, list, nl, X0, Y0, lx, ly0, X, Yc, ga);
-        __syncthreads();  // the list is rewritten next round
+        any = any || __ballot(mine.box != kNoBox) != 0ull;
+        gather_walk<KID, NOUT, ACC>(g, s, mine, X0, Y0, o, cc, ga);
     }
-    if (!any || lx >= TW) return;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        if (ly0 + j >= TH) continue;
-        const long long o = (long long)(X0 + lx) * g.ny + (Y0 + ly0 + j);
-        emit_pixel<NOUT, ACC>(o, ga.word0(j), NOUT == 2 ? ga.word1(j) : 0ull, k0, k1, out0, out1,
-                              kFlagAccumulate);
-    }
+    if (!any) return;
+    gather_emit<NOUT, ACC>(g, ga, o, X0, Y0, -1, nullptr, k0, k1, out0, out1, kFlagAccumulate);
 }
 
 // K7: out0 <- out0 / out1 (0 where out1 == 0).
@@ -1364,11 +1489,12 @@ bool make_grid(double x_min, double x_max, double y_min, double y_max, int nx, i
     g.ipsx = (float)(1.0 / g.psx);
     g.ipsy = (float)(1.0 / g.psy_pix);
     if (!std::isfinite(g.ipsx) || !std::isfinite(g.ipsy)) return false;
-    // |corner| over the grid (absolute frame), and 2x the tile span (tile-local frame)
+    // |corner| over the grid (absolute frame); 2x the tile span (the records' frames)
+    const double mgl = 2.0 * kTile * std::max(g.psx, g.psy_pix);
     double mg = std::max({std::fabs(x_min), std::fabs(x_min + nx * g.psx), std::fabs(y_min),
-                          std::fabs(y_min + ny * g.psy_pix), 2.0 * kTile * g.psx,
-                          2.0 * kTile * g.psy_pix});
+                          std::fabs(y_min + ny * g.psy_pix), mgl});
     g.mg = (float)(mg * (1.0 + 1e-6));
+    g.mgl = (float)(mgl * (1.0 + 1e-6));
     g.nx = nx;
     g.ny = ny;
     g.cs = cs;
@@ -1458,7 +1584,8 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
     if (pl.n_large > 0) {
         StageMark m(ws, kSGather, st);
         const size_t lds = gather_lds<NOUT, ACC>();
-        hipLaunchKernelGGL((k_gather<KID, NOUT, ACC>), dim3(pl.n_items), dim3(kDepBlock), lds, st, g,
+        hipLaunchKernelGGL((k_gather<KID, NOUT, ACC>), dim3(pl.n_items * kGatherRegions),
+                           dim3(kGatherThreads), lds, st, g,
                            s, (const float4*)ws.recs.p, (const Item*)ws.items.p,
                            (const int2*)ws.tile_k.p, (unsigned long long*)ws.slabs.p, o0, o1,
                            dflags);
@@ -1476,7 +1603,8 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
     if (pl.n_wide > 0) {
         StageMark m(ws, kSWide, st);
         const size_t lds = gather_lds<NOUT, ACC>();
-        hipLaunchKernelGGL((k_wide<KID, NOUT, ACC>), dim3(g.ntiles), dim3(kDepBlock), lds, st, g, s,
+        hipLaunchKernelGGL((k_wide<KID, NOUT, ACC>), dim3(g.ntiles * kGatherRegions),
+                           dim3(kGatherThreads), lds, st, g, s,
                            u, v, h, a0, a1, (const int*)ws.wide.p, pl.n_wide, (const int*)dc, o0,
                            o1);
         ASP_LAUNCHED();
@@ -1497,7 +1625,9 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
 // Tunables read once per call (experiments; the defaults are the measured choices).
 static void grid_tunables(Grid& g) {
     if (const char* e = getenv("ASP_WIDE_TILES")) g.wide_tiles = std::max(1, atoi(e));
-    if (const char* e = getenv("ASP_GATHER_MIN")) g.gather_min = std::max(5, atoi(e));
+    if (const char* e = getenv("ASP_GATHER_MIN")) g.gather_min = std::max(2, atoi(e));
+    g.gexp = 0;
+    if (const char* e = getenv("ASP_GEXP")) g.gexp = atoi(e);
 }
 
 // The projection on DEVICE arrays (fp32 working copies u, v, h, a0, a1; s: the caller's

@@ -23,7 +23,8 @@ import re
 
 STAGE_OF = {"k_count": "count", "k_colscan": "colscan", "k_tilescan": "tilescan",
             "k_scatter": "scatter", "k_deposit": "deposit", "k_wide": "wide",
-            "k_ratio": "ratio", "k_bin": "scatter", "k_deposit3d": "deposit"}
+            "k_ratio": "ratio", "k_bin": "scatter", "k_deposit3d": "deposit",
+            "k_gather": "gather", "k_merge": "merge"}
 
 
 def short(name):
