@@ -41,7 +41,7 @@ EXPORTS = ("asp_version", "asp_last_error", "asp_device_count", "asp_project2d",
            "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges", "asp_pixel_neighbours", "asp_ratio",
            "asp_profile", "asp_profile_stages", "asp_profile_read", "asp_last_stats",
            "asp_release", "asp_stage_particles", "asp_periodic", "asp_wrapped_distance",
-           "asp_knn_smoothing_lengths", "asp_table_interp3")
+           "asp_knn_smoothing_lengths", "asp_table_interp3", "asp_table_interp")
 
 STAGES = ("memset", "count", "colscan", "tilescan", "scatter", "scale", "deposit", "merge",
           "wide", "ratio", "cube_count", "cube_colscan", "cube_tilescan", "cube_scatter",
@@ -121,11 +121,14 @@ def lib():
     L.asp_table_interp3.argtypes = ([_d, C.c_int32, C.c_int32, C.c_int32, _d, _d, _d, _d,
                                      C.c_int32, C.c_int32, C.c_double, C.c_int64, C.c_double,
                                      C.c_int32, _d, _d, _d, C.c_int32, C.c_void_p])
+    L.asp_table_interp.argtypes = ([_d, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_void_p),
+                                    _d, C.c_int32, C.c_int32, C.c_double, C.c_int64, C.c_double,
+                                    C.c_int32, C.c_int32, _d, _d, _d, C.c_int32, C.c_void_p])
     for name in ("asp_project2d", "asp_project2d_f64", "asp_pairs_f64", "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges",
                  "asp_pixel_neighbours", "asp_ratio", "asp_profile", "asp_profile_stages",
                  "asp_profile_read", "asp_last_stats", "asp_release", "asp_stage_particles",
                  "asp_periodic", "asp_wrapped_distance", "asp_knn_smoothing_lengths",
-                 "asp_table_interp3"):
+                 "asp_table_interp3", "asp_table_interp"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

@@ -55,7 +55,6 @@ struct Grid {
     int mixed;        // the cull reads other position columns than the pixel test (Src64)
     int wide_tiles;   // particles over more tiles than this take the wide path (K6)
     int gather_min;   // records with clipped boxes >= this on both axes are gathered (K4)
-    int gexp;         // experiment switch (temporary)
 };
 
 // The caller's particle arrays, resident in HBM, read by particle index where the exact

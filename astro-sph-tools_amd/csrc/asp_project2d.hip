@@ -67,7 +67,7 @@ static_assert(kBatch == (long long)kScatterBlock * kUnroll, "count and scatter b
 // Records whose box clipped to a tile is at least this wide on both axes go to the large
 // stream (K4g); the threshold is a Grid field so it can be tuned per call
 // (ASP_GATHER_MIN).
-constexpr int kGatherMinDefault = 12;
+constexpr int kGatherMinDefault = 5;
 
 // Vector of U floats (one 4 U-byte load per lane).
 template <int U>
@@ -748,20 +748,40 @@ struct GEntry {
 };
 constexpr unsigned kNoBox = 0x00ff00ffu;  // x0 = 255 > x1 = 0: meets no region
 
+typedef float f2 __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_* ops)
+
 // Shape f(q) / kShapeScale for kernels that vanish continuously at q = 2 (cubic,
-// Wendland), written so that q >= 2 gives exactly 0 without a comparison:
-// t = max(1 - q/2, 0).  Cubic: (2 - q)^3 / 4 = 2 t^3, the inner branch halved to match.
+// Wendland), written so that q >= 2 gives exactly 0 without a comparison, two pixels per
+// packed instruction: t = clamp(1 - q/2) (the VOP3P clamp bit; 1 - q/2 <= 1 as q >= 0).
+// Cubic: f = (2 - q)^3 / 4 - max(1 - q, 0)^3 = 2 t^3 - s^3 with s = clamp(1 - q) -- one
+// expression on [0, 2] (for q < 1 it expands to 1 - 1.5 q^2 + 0.75 q^3), no branch;
+// computed as f / 2 = t^3 - s^3 / 2.  Wendland C2: t^4 (1 + 2q).
 template <int KID>
 constexpr float kShapeScale = KID == 0 ? 2.0f : 1.0f;
+
+// clamp(1 - q/2, 0, 1) and clamp(1 - q, 0, 1) on two lanes of fp32 at once (inline
+// constants, both halves).  The leading s_nop covers the transcendental-result hazard
+// (q comes straight from v_sqrt_f32).
+__device__ __forceinline__ f2 pk_one_minus_half_clamp(f2 q) {
+    f2 d;
+    asm("s_nop 0\n\tv_pk_fma_f32 %0, %1, -0.5, 1.0 op_sel_hi:[1,0,0] clamp" : "=v"(d) : "v"(q));
+    return d;
+}
+__device__ __forceinline__ f2 pk_one_minus_clamp(f2 q) {
+    f2 d;
+    asm("s_nop 0\n\tv_pk_fma_f32 %0, %1, -1.0, 1.0 op_sel_hi:[1,0,0] clamp" : "=v"(d) : "v"(q));
+    return d;
+}
+
 template <int KID>
-__device__ __forceinline__ float edge_shape(float q) {
-    const float t = fmaxf(fmaf(-0.5f, q, 1.0f), 0.0f);
+__device__ __forceinline__ f2 edge_shape2(f2 q) {
+    const f2 t = pk_one_minus_half_clamp(q);
     if constexpr (KID == 0) {
-        const float a = fmaf(q * q, fmaf(0.375f, q, -0.75f), 0.5f);  // (1 - 1.5q^2 + .75q^3)/2
-        return q < 1.0f ? a : t * t * t;
+        const f2 s = pk_one_minus_clamp(q);
+        return __builtin_elementwise_fma((f2){-0.5f, -0.5f}, s * s * s, t * t * t);
     } else {
-        const float t2 = t * t;
-        return (t2 * t2) * fmaf(2.0f, q, 1.0f);
+        const f2 t2 = t * t;
+        return (t2 * t2) * __builtin_elementwise_fma((f2){2.0f, 2.0f}, q, (f2){1.0f, 1.0f});
     }
 }
 
@@ -770,8 +790,8 @@ __device__ __forceinline__ float edge_shape(float q) {
 // fixed-point sums in registers (kAccFix).
 template <int NOUT, int ACC>
 struct GAcc {
-    using T = typename std::conditional<ACC == kAccFix, unsigned long long, float>::type;
-    T a0[8], a1[8];
+    unsigned long long a0[8], a1[8];  // kAccFix sums
+    f2 p0[4], p1[4];                  // kAccF64 fp32 partials, pixels (2k, 2k + 1)
     double* t0;
     double* t1;
     __device__ __forceinline__ void init(double* tot) {
@@ -779,6 +799,11 @@ struct GAcc {
         for (int j = 0; j < 8; ++j) {
             a0[j] = 0;
             a1[j] = 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            p0[k] = (f2){0.0f, 0.0f};
+            p1[k] = (f2){0.0f, 0.0f};
         }
         t0 = tot + threadIdx.x;
         t1 = tot + kGatherPix + threadIdx.x;
@@ -796,20 +821,31 @@ struct GAcc {
             a0[j] += f2fix(s0 * w);
             if (NOUT == 2) a1[j] += f2fix(s1 * w);
         } else {
-            a0[j] = fmaf(s0, w, a0[j]);
-            if (NOUT == 2) a1[j] = fmaf(s1, w, a1[j]);
+            p0[j >> 1][j & 1] = fmaf(s0, w, p0[j >> 1][j & 1]);
+            if (NOUT == 2) p1[j >> 1][j & 1] = fmaf(s1, w, p1[j >> 1][j & 1]);
+        }
+    }
+    // pixels 2k, 2k + 1 += w.xy * (s0, s1)  (one v_pk_fma_f32 per map)
+    __device__ __forceinline__ void add2(int k, f2 w, float s0, float s1) {
+        if constexpr (ACC == kAccFix) {
+            add(2 * k, w.x, s0, s1);
+            add(2 * k + 1, w.y, s0, s1);
+        } else {
+            p0[k] = __builtin_elementwise_fma(w, (f2){s0, s0}, p0[k]);
+            if (NOUT == 2) p1[k] = __builtin_elementwise_fma(w, (f2){s1, s1}, p1[k]);
         }
     }
     __device__ __forceinline__ void fold() {
         if constexpr (ACC != kAccFix) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                t0[j * kGatherThreads] += (double)a0[j];
-                a0[j] = 0.0f;
-                if (NOUT == 2) {
-                    t1[j * kGatherThreads] += (double)a1[j];
-                    a1[j] = 0.0f;
-                }
+                t0[j * kGatherThreads] += (double)p0[j >> 1][j & 1];
+                if (NOUT == 2) t1[j * kGatherThreads] += (double)p1[j >> 1][j & 1];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                p0[k] = (f2){0.0f, 0.0f};
+                p1[k] = (f2){0.0f, 0.0f};
             }
         }
     }
@@ -908,37 +944,30 @@ __device__ __forceinline__ unsigned block_hits(unsigned box, const GOwn& o) {
 // of a met block outside the box have r >= 2h as well (the box is a superset of the disc).
 template <int KID, int NOUT, int ACC>
 __device__ __forceinline__ void gather_entry_edge(const GEntry& E, const GOwn& o,
-                                                  const GCorner& c, GAcc<NOUT, ACC>& ga, int gexp) {
-    const float vs = E.v * E.hinv;  // in units of h
-    if (gexp == 1) {  // both block rows, no branch
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const float dxs = (E.u - c.X[r]) * E.hinv;
-            const float dx2 = dxs * dxs;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float dys = fmaf(-E.hinv, c.Y[k], vs);
-                const float q = __builtin_amdgcn_sqrtf(fmaf(dys, dys, dx2));
-                ga.add(4 * r + k, edge_shape<KID>(q), E.s0, E.s1);
-            }
-        }
-        return;
-    }
-    // A met block row is evaluated whole (4 independent pixels in flight): a pixel
-    // outside the box contributes exactly 0 there, as above.  (The box meets the wave's
-    // region, so it meets a block row iff its rows do.)
+                                                  const GCorner& c, GAcc<NOUT, ACC>& ga) {
+    // Met 8 x 16 half block rows are evaluated whole (2 pixels per lane, one packed op
+    // each): a pixel outside the box contributes exactly 0, as above.
     const int x0 = E.box & 255u, x1 = (E.box >> 8) & 255u;
+    const int y0 = (E.box >> 16) & 255u, y1 = E.box >> 24;
+    const f2 hv = {-E.hinv, -E.hinv};
+    const f2 vs = {E.v * E.hinv, E.v * E.hinv};  // in units of h
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
         const int br = o.r0 + 8 * r;
         if (x0 <= br + 7 && x1 >= br) {
             const float dxs = (E.u - c.X[r]) * E.hinv;
-            const float dx2 = dxs * dxs;
+            const f2 dx2 = {dxs * dxs, dxs * dxs};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float dys = fmaf(-E.hinv, c.Y[k], vs);
-                const float q = __builtin_amdgcn_sqrtf(fmaf(dys, dys, dx2));
-                ga.add(4 * r + k, edge_shape<KID>(q), E.s0, E.s1);
+            for (int k = 0; k < 2; ++k) {
+                const int bc = o.c0 + 16 * k;
+                if (y0 <= bc + 15 && y1 >= bc) {
+                    const f2 dys = __builtin_elementwise_fma(hv, (f2){c.Y[2 * k], c.Y[2 * k + 1]}, vs);
+                    const f2 r2 = __builtin_elementwise_fma(dys, dys, dx2);
+                    f2 q;
+                    q.x = __builtin_amdgcn_sqrtf(r2.x);
+                    q.y = __builtin_amdgcn_sqrtf(r2.y);
+                    ga.add2(2 * r + k, edge_shape2<KID>(q), E.s0, E.s1);
+                }
             }
         }
     }
@@ -992,7 +1021,7 @@ __device__ __forceinline__ void gather_walk(const Grid& g, const Src64& s, const
         while (m) {
             const int l = __builtin_ctzll(m);
             m &= m - 1;
-            gather_entry_edge<KID, NOUT, ACC>(lane_entry(mine, l), o, c, ga, g.gexp);
+            gather_entry_edge<KID, NOUT, ACC>(lane_entry(mine, l), o, c, ga);
         }
     } else {
         while (m) {
@@ -1626,8 +1655,6 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
 static void grid_tunables(Grid& g) {
     if (const char* e = getenv("ASP_WIDE_TILES")) g.wide_tiles = std::max(1, atoi(e));
     if (const char* e = getenv("ASP_GATHER_MIN")) g.gather_min = std::max(2, atoi(e));
-    g.gexp = 0;
-    if (const char* e = getenv("ASP_GEXP")) g.gexp = atoi(e);
 }
 
 // The projection on DEVICE arrays (fp32 working copies u, v, h, a0, a1; s: the caller's

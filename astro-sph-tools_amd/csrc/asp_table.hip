@@ -240,6 +240,80 @@ __global__ __launch_bounds__(kSlabBlock) void k_table_slab(const double* __restr
     }
 }
 
+// ----------------------------------------------------------------------------------
+// Any number of table axes (IonisationTableBase accepts N input dimensions,
+// _IonisationTable.py:31-49).  scipy 1.15 evaluates N != 2 with _evaluate_linear:
+//   weight = 1; weight = weight * w_d over the axes in order; value = value + t * weight,
+// and a writeable native-fp64 2-D table with the Cython evaluate_linear_2d:
+//   value = value + t[corner] * w_0 * w_1   (left to right: the table value first).
+// Both over the corners in itertools.product order (last axis fastest).  `vfirst` selects
+// the 2-D form.  One lane per point; the axes are read from global memory (L1/L2).
+// ----------------------------------------------------------------------------------
+constexpr int kTabMaxDims = 6;
+struct TabND {
+    const double* g[kTabMaxDims];
+    int n[kTabMaxDims];
+    long long stride[kTabMaxDims];
+};
+
+template <int D>
+__global__ __launch_bounds__(kTabBlock) void k_table_nd(const double* __restrict__ t, TabND A,
+                                                        const double* __restrict__ pts, int ncol,
+                                                        int zaxis, double zc, long long n,
+                                                        double fill, int mode, int vfirst,
+                                                        const double* __restrict__ a0,
+                                                        const double* __restrict__ a1,
+                                                        double* __restrict__ out) {
+    const long long p = (long long)blockIdx.x * kTabBlock + threadIdx.x;
+    if (p >= n) return;
+    int i[D];
+    double y[D];
+    bool nan = false, oob = false;
+#pragma unroll
+    for (int d = 0, c = 0; d < D; ++d) {
+        double x;
+        if (ncol == D) {
+            x = pts[(long long)D * p + d];
+        } else if (d == zaxis) {
+            x = zc;
+        } else {
+            x = pts[(long long)ncol * p + c];
+            ++c;
+        }
+        const double inv = (double)(A.n[d] - 1) / (A.g[d][A.n[d] - 1] - A.g[d][0]);
+        locate(A.g[d], A.n[d], inv, x, i[d], y[d], nan, oob);
+    }
+    double v;
+    if (nan) {
+        v = NAN;
+    } else if (oob) {
+        v = fill;
+    } else {
+        v = 0.0;
+#pragma unroll
+        for (int c = 0; c < (1 << D); ++c) {
+            long long o = 0;
+#pragma unroll
+            for (int d = 0; d < D; ++d) o += (long long)(i[d] + ((c >> (D - 1 - d)) & 1)) * A.stride[d];
+            double term;
+            if (vfirst) {
+                term = t[o];
+#pragma unroll
+                for (int d = 0; d < D; ++d) term = term * (((c >> (D - 1 - d)) & 1) ? y[d] : 1 - y[d]);
+            } else {
+                double w = 1.0;
+#pragma unroll
+                for (int d = 0; d < D; ++d) w = w * (((c >> (D - 1 - d)) & 1) ? y[d] : 1 - y[d]);
+                term = t[o] * w;
+            }
+            v = v + term;
+        }
+    }
+    if (mode == 1) v = (a0[p] * a1[p]) * v;
+    else if (mode == 2) v = (a0[p] * a1[p]) * exp10(v);
+    out[p] = v;
+}
+
 }  // namespace asp
 
 using namespace asp;
@@ -279,6 +353,56 @@ extern "C" int asp_table_interp3(const double* table, int32_t n0, int32_t n1, in
         if (lds) hipLaunchKernelGGL((k_table<2, true>), grid, dim3(kTabBlock), 0, st, table, A, points, (int)zaxis, zvalue, (long long)n, fill, (int)mode, a0, a1, out);
         else hipLaunchKernelGGL((k_table<2, false>), grid, dim3(kTabBlock), 0, st, table, A, points, (int)zaxis, zvalue, (long long)n, fill, (int)mode, a0, a1, out);
     }
+    ASP_HIP(hipGetLastError());
+    return ASP_OK;
+}
+
+extern "C" int asp_table_interp(const double* table, int32_t ndim, const int32_t* shape,
+                                const double* const* axes, const double* points, int32_t ncol,
+                                int32_t zaxis, double zvalue, int64_t n, double fill,
+                                int32_t mode, int32_t order, const double* a0, const double* a1,
+                                double* out, int32_t device, void* stream) {
+    t_err.clear();
+    if (ndim < 1 || ndim > kTabMaxDims) return fail(ASP_ERR_UNSUPPORTED, "1 .. 6 table axes");
+    if (!shape || !axes) return fail(ASP_ERR_INVALID, "NULL shape / axes");
+    for (int d = 0; d < ndim; ++d)
+        if (shape[d] < 2 || !axes[d]) return fail(ASP_ERR_INVALID, "every table axis needs >= 2 points");
+    if (ncol != ndim && !(ncol == ndim - 1 && zaxis >= 0 && zaxis < ndim))
+        return fail(ASP_ERR_INVALID, "points must have ndim (or ndim - 1 + zvalue) columns");
+    if (mode < 0 || mode > 2 || order < 0 || order > 1) return fail(ASP_ERR_INVALID, "bad mode / order");
+    if (n < 0) return fail(ASP_ERR_INVALID, "n < 0");
+    if (n == 0) return ASP_OK;
+    if (!table || !points || !out || (mode && (!a0 || !a1))) return fail(ASP_ERR_INVALID, "NULL array");
+    int ndev = 0;
+    ASP_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(ASP_ERR_INVALID, "bad device");
+    ASP_HIP(hipSetDevice(device));
+    TabND A{};
+    long long st = 1;
+    for (int d = ndim - 1; d >= 0; --d) {
+        A.g[d] = axes[d];
+        A.n[d] = shape[d];
+        A.stride[d] = st;
+        st *= shape[d];
+    }
+    const dim3 grid((unsigned)((n + kTabBlock - 1) / kTabBlock));
+    hipStream_t s = (hipStream_t)stream;
+    const int vfirst = order == 1 && ndim == 2;
+#define ASP_TAB_ND(D)                                                                          \
+    case D:                                                                                    \
+        hipLaunchKernelGGL((k_table_nd<D>), grid, dim3(kTabBlock), 0, s, table, A, points,     \
+                           (int)ncol, (int)zaxis, zvalue, (long long)n, fill, (int)mode,       \
+                           vfirst, a0, a1, out);                                               \
+        break;
+    switch (ndim) {
+        ASP_TAB_ND(1)
+        ASP_TAB_ND(2)
+        ASP_TAB_ND(3)
+        ASP_TAB_ND(4)
+        ASP_TAB_ND(5)
+        ASP_TAB_ND(6)
+    }
+#undef ASP_TAB_ND
     ASP_HIP(hipGetLastError());
     return ASP_OK;
 }

@@ -282,6 +282,22 @@ int asp_table_interp3(const double *table, int32_t n0, int32_t n1, int32_t n2,
                       double *out, int32_t device, void *stream);
 
 /*
+ * The same for any number of table axes (IonisationTableBase takes N input dimensions,
+ * _IonisationTable.py:31-49): table (shape[0], ..., shape[ndim-1]) float64 C-order, axes[d]
+ * a device pointer to axis d (a HOST array of ndim pointers; shape is a host array too),
+ * 1 <= ndim <= 6.  points: (n, ndim) rows, or (n, ndim - 1) rows with `zvalue` inserted at
+ * axis `zaxis`.  order 0: scipy's _evaluate_linear (weights multiplied first, every ndim);
+ * order 1: its Cython 2-D fast path (value times w0 times w1), which scipy takes for a
+ * writeable native-float64 2-D table.  Bit-identical to scipy 1.15; fill / NaN / mode as
+ * asp_table_interp3.
+ */
+int asp_table_interp(const double *table, int32_t ndim, const int32_t *shape,
+                     const double *const *axes, const double *points, int32_t ncol,
+                     int32_t zaxis, double zvalue, int64_t n, double fill, int32_t mode,
+                     int32_t order, const double *a0, const double *a1, double *out,
+                     int32_t device, void *stream);
+
+/*
  * Statistics of the last asp_project2d call on `device` (inspection / roofline):
  * stats[0] = records binned (particle x GPU-tile insertions), stats[1] = work items,
  * stats[2] = wide particles, stats[3] = GPU tile edge (pixels), stats[4] = GPU tiles,

@@ -113,3 +113,34 @@ def test_at_redshift_any_axis_matches_restatement(gpu, oracle, zaxis):
         got = tab.evaluate_at_redshift(P, float(z))
         want = oracle.table_at_redshift(t, grids, P, float(z), zaxis=zaxis)
         assert np.array_equal(bits(got), bits(want)), (zaxis, z)
+
+
+@pytest.mark.parametrize("ndim", [1, 2, 4, 5])
+def test_nd_tables_bit_exact_vs_scipy(gpu, ndim):
+    """IonisationTableBase takes any number of axes (_IonisationTable.py:31-49): 1, 2, 4 and
+    5-D tables against scipy's RegularGridInterpolator (the reference's interpolator,
+    linear, fill -inf), __call__ and evaluate_at_redshift, including points outside the
+    table and NaN rows.  2-D also read-only (scipy's _evaluate_linear instead of its Cython
+    fast path: a different arithmetic order, both reproduced)."""
+    from scipy.interpolate import RegularGridInterpolator
+    from asp_amd.ionisation import IonisationTable
+    rng = np.random.default_rng(100 + ndim)
+    shape = tuple(int(x) for x in rng.integers(3, 12 if ndim <= 2 else 7, ndim))
+    grids = [np.cumsum(rng.uniform(0.05, 0.3, n)) - 1.0 for n in shape]
+    t = rng.normal(size=shape)
+    variants = [t]
+    if ndim == 2:
+        ro = t.copy()
+        ro.flags.writeable = False
+        variants.append(ro)
+    P = np.stack([rng.uniform(g[0] - 0.1, g[-1] + 0.1, 50_000) for g in grids], axis=1)
+    P[::331, 0] = np.nan
+    for tab_arr in variants:
+        ref = RegularGridInterpolator(grids, tab_arr, bounds_error=False, fill_value=-np.inf)
+        tab = IonisationTable(tab_arr, *grids, redshift_input_index=ndim - 1)
+        assert tab.number_of_input_dimensions == ndim
+        assert np.array_equal(bits(tab(P)), bits(ref(P)))
+        if ndim >= 2:
+            z = float(grids[-1][1] + 0.37 * (grids[-1][2] - grids[-1][1]))
+            full = np.concatenate([P[:, :-1], np.full((P.shape[0], 1), z)], axis=1)
+            assert np.array_equal(bits(tab.evaluate_at_redshift(P[:, :-1], z)), bits(ref(full)))
