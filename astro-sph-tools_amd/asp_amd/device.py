@@ -97,12 +97,13 @@ def _f64_arg(a, name, n, shape_tail=()):
 def project2d_f64(positions, h, a0, a1=None, *, projection_axis=2, image_size, extent,
                   chunk_size: int = 64, kernel="cubic", ratio: bool = False,
                   accumulate: bool = False, out0=None, out1=None, device: int = 0,
-                  stream=None, deterministic: bool = False):
+                  stream=None, deterministic: bool = False, device_out: bool = False):
     """asp_project2d_f64: the reader's float64 arrays (positions (N, 3), h, a0[, a1]) --
     host NumPy arrays or float64 device tensors -- projected with the reference's fp64
     decisions on those values.  ``projection_axis``: an axis (int 0/1/2, enum, "x") or a
-    (pixel axis, cull axis) pair (asp_amd._axes.reference_axes).  Returns float32 maps: device tensors for device inputs
-    (or the given ``out0``/``out1``), NumPy arrays for host inputs."""
+    (pixel axis, cull axis) pair (asp_amd._axes.reference_axes).  Returns float32 maps:
+    device tensors for device inputs or ``device_out`` (host inputs staged through pinned
+    buffers, maps left on ``device`` -- e.g. for an RCCL sum), else NumPy arrays."""
     import numpy as np
     import torch
     from ._axes import axis_index
@@ -138,6 +139,16 @@ def project2d_f64(positions, h, a0, a1=None, *, projection_axis=2, image_size, e
             out0 = torch.empty((nx, ny), dtype=torch.float32, device=dev)
         if nout == 2 and out1 is None:
             out1 = torch.empty((nx, ny), dtype=torch.float32, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+    elif device_out:
+        _lib.require_gpu(device)
+        flags |= _lib.ASP_F_DEVICE_OUTPUTS
+        dev = torch.device("cuda", device)
+        if out0 is None:
+            out0 = (torch.zeros if accumulate else torch.empty)((nx, ny), dtype=torch.float32, device=dev)
+        if nout == 2 and out1 is None:
+            out1 = (torch.zeros if accumulate else torch.empty)((nx, ny), dtype=torch.float32, device=dev)
         if stream is None:
             stream = torch.cuda.current_stream(dev).cuda_stream
     else:

@@ -19,8 +19,31 @@ from . import _lib
 from .device import project2d
 
 
-def zslab_bounds(z, world_size: int, sample: int = 1 << 20, seed: int = 0):
-    """Equal-count Z-slab edges from a random subsample of z (device tensor).
+def slab_cost(u, v, h, extent, pitch: float, binning_pairs: float = 1000.0):
+    """Per-particle work model for slab balancing, in units of one (pixel, particle) pair:
+    ``binning_pairs`` plus the footprint's pixels inside the image, ``(2h / pitch)^2``
+    clipped to the image's extent on each axis (0 for a particle whose footprint misses
+    it).  The constant is a fit to the per-slab times of tools/slab_balance.py at 10^8
+    particles -> 4096^2, physical h: a particle costs ~1000 pairs' worth
+    beyond its footprint area (binning, the gather's 8 x 16-pixel granularity, the K6
+    wide list); at pixel-scale h every particle weighs the same and the edges are the
+    equal-count ones."""
+    import torch
+    x_min, x_max, y_min, y_max = (float(e) for e in extent)
+    r = 2.0 * h.double().abs()
+    ud, vd = u.double(), v.double()
+    wx = (torch.minimum(ud + r, torch.full_like(ud, x_max)) -
+          torch.maximum(ud - r, torch.full_like(ud, x_min))).clamp(min=0.0)
+    wy = (torch.minimum(vd + r, torch.full_like(vd, y_max)) -
+          torch.maximum(vd - r, torch.full_like(vd, y_min))).clamp(min=0.0)
+    return binning_pairs + (wx / float(pitch)) * (wy / float(pitch))
+
+
+def zslab_bounds(z, world_size: int, sample: int = 1 << 20, seed: int = 0, weights=None):
+    """Z-slab edges from a random subsample of z (device tensor): equal particle counts,
+    or with ``weights`` (one per particle, e.g. :func:`slab_cost`) equal summed weight --
+    at physical h the pair work per particle grows as h^2, so equal counts leave the core
+    slabs with far more work than the outer ones.
 
     Returns a list of world_size + 1 floats (first -inf, last +inf).
     """
@@ -32,10 +55,18 @@ def zslab_bounds(z, world_size: int, sample: int = 1 << 20, seed: int = 0):
     g.manual_seed(seed)
     k = min(n, sample)
     idx = torch.randint(0, n, (k,), generator=g, device=z.device)
-    s = torch.sort(z[idx]).values
+    s, order = torch.sort(z[idx])
     edges = [float("-inf")]
-    for r in range(1, world_size):
-        edges.append(float(s[(k * r) // world_size]))
+    if weights is None:
+        for r in range(1, world_size):
+            edges.append(float(s[(k * r) // world_size]))
+    else:
+        c = torch.cumsum(weights[idx][order].double(), 0)
+        tot = float(c[-1])
+        targets = torch.tensor([tot * r / world_size for r in range(1, world_size)],
+                               dtype=torch.float64, device=z.device)
+        pos = torch.searchsorted(c, targets).clamp(max=k - 1)
+        edges += [float(s[int(i)]) for i in pos.tolist()]
     edges.append(float("inf"))
     return edges
 
@@ -65,10 +96,11 @@ class PendingMap:
     sum of map i overlaps the binning and deposit of map i + 1).
     """
 
-    def __init__(self, outs, works, ratio_here):
+    def __init__(self, outs, works, ratio_here, gather=None):
         self._outs = outs
         self._works = works
         self._ratio = ratio_here
+        self._gather = gather  # (full-size destination, group): all-gather map 0's slabs
         self._done = False
 
     def wait(self):
@@ -82,6 +114,11 @@ class PendingMap:
                 _lib.check(_lib.lib().asp_ratio(_lib.ptr(o0), _lib.ptr(o1), o0.numel(),
                                                 dev.index or 0,
                                                 torch.cuda.current_stream(dev).cuda_stream))
+            if self._gather is not None:
+                import torch.distributed as dist
+                full, group = self._gather
+                dist.all_gather_into_tensor(full, self._outs[0].contiguous(), group=group)
+                self._outs = [full]
             self._done = True
         return self._outs[0], (self._outs[1] if len(self._outs) > 1 else None)
 
@@ -94,7 +131,10 @@ def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
 
     Returns ``(out0, out1)``: the full map(s) on ``dst`` (``op="reduce"``), on every rank
     (``"allreduce"``), or this rank's row slab (``"reduce_scatter"``; requires
-    nx % world_size == 0).  With ``ratio`` the weighted map is formed after the sum.
+    nx % world_size == 0).  ``"reduce_scatter_gather"``: reduce-scatter, the ratio (or the
+    single map) formed per row slab, then ONE all-gather of that map into ``out0`` on
+    every rank -- returns ``(out0, None)``.  With ``ratio`` the weighted map is formed
+    after the sum.
     ``async_op=True`` returns a :class:`PendingMap` instead, whose ``wait()`` completes the
     collective (stream-ordered) and the ratio.
     ``projector`` replaces the local projection (tests drive the collective logic on CPU
@@ -104,12 +144,12 @@ def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
     import torch.distributed as dist
     if ratio and a1 is None:
         raise ValueError("ratio needs a1")
-    if op not in ("reduce", "allreduce", "reduce_scatter"):
+    if op not in ("reduce", "allreduce", "reduce_scatter", "reduce_scatter_gather"):
         raise ValueError(f"unknown op {op!r}")
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     nx = int(image_size[0])
-    if op == "reduce_scatter" and world > 1 and nx % world:
+    if op.startswith("reduce_scatter") and world > 1 and nx % world:
         raise ValueError("reduce_scatter needs nx divisible by the world size")
     proj = project2d if projector is None else projector
     kw = {"deterministic": True} if deterministic else {}
@@ -119,7 +159,7 @@ def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
     works = []
     fused = _adjacent(o0, o1)  # both maps in one buffer: one collective of 2 maps
     if world > 1:
-        if op == "reduce_scatter":
+        if op.startswith("reduce_scatter"):
             res = []
             for t in outs:
                 part = torch.empty((nx // world, t.shape[1]), dtype=t.dtype, device=t.device)
@@ -136,8 +176,54 @@ def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
                     works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group,
                                                  async_op=True))
     ratio_here = ratio and (op != "reduce" or rank == dst or world == 1)
-    pending = PendingMap(outs, works, ratio_here)
+    gather = None
+    if op == "reduce_scatter_gather" and world > 1:
+        # each rank forms the ratio (or the single map) of ITS row slab, then one
+        # all-gather of that one map: 2 maps reduce-scattered + 1 map gathered on the wire
+        # instead of 2 maps reduced to one rank and the ratio there
+        gather = (o0, group)
+    pending = PendingMap(outs, works, ratio_here, gather)
     return pending if async_op else pending.wait()
+
+
+def project2d_sharded_host(positions, h, a0, a1=None, *, projection_axis=2, image_size,
+                           extent, chunk_size: int = 64, kernel="cubic", ratio: bool = False,
+                           op: str = "reduce", dst: int = 0, group=None, device=None,
+                           out0=None, out1=None, projector=None, deterministic: bool = False,
+                           async_op: bool = False):
+    """The reader -> stage -> project -> collective chain from each rank's OWN float64
+    host arrays, as the reference's readers hand them out under their MPI split
+    (io/EAGLE/_SnapshotEAGLE.py:120-130: any particle split is fine; a Z-slab split
+    balances the work).  The arrays go through pinned bounce buffers to the rank's GPU
+    (asp_project2d_f64 with ASP_F_DEVICE_OUTPUTS: the fp64 values stay resident for the
+    exact decisions), the map stays on the device and :func:`project2d_sharded`'s
+    collective sums it over ``group``.  ``projector`` replaces the local projection (the
+    CPU tests inject the oracle; its signature is :func:`project2d_f64_local`'s)."""
+    import torch
+    if device is None:
+        device = torch.cuda.current_device() if projector is None else 0
+
+    def local(_u, _v, _h, _a0, _a1, *, image_size, extent, chunk_size, kernel, ratio, out0,
+              out1, **kw):
+        f = project2d_f64_local if projector is None else projector
+        return f(positions, h, a0, a1, projection_axis=projection_axis, image_size=image_size,
+                 extent=extent, chunk_size=chunk_size, kernel=kernel, out0=out0, out1=out1,
+                 device=device, **kw)
+
+    return project2d_sharded(None, None, None, a0, a1, image_size=image_size, extent=extent,
+                             chunk_size=chunk_size, kernel=kernel, ratio=ratio, op=op, dst=dst,
+                             group=group, out0=out0, out1=out1, projector=local,
+                             deterministic=deterministic, async_op=async_op)
+
+
+def project2d_f64_local(positions, h, a0, a1=None, *, projection_axis, image_size, extent,
+                        chunk_size, kernel, out0, out1, device, deterministic=False):
+    """One rank's fp64 host arrays -> its device map(s) (no ratio: formed after the sum)."""
+    from .device import project2d_f64
+    return project2d_f64(positions, h, a0, a1, projection_axis=projection_axis,
+                         image_size=image_size, extent=extent, chunk_size=chunk_size,
+                         kernel=kernel, out0=out0, out1=out1, device=device,
+                         deterministic=deterministic, device_out=True)
 
 
 # ---------------------------------------------------------------------------------------

@@ -63,13 +63,12 @@ struct Workspace {
     Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
         wide, slabs, morton, aux[6];
     Buf in64[4];     // asp_project2d_f64: the caller's fp64 arrays, resident for exact decisions
-    Buf tile_large;  // per 2-D tile: holds records gathered by the deposit's large path
     Buf pairs[4];    // asp_pair_list
     int* h_counters = nullptr;  // pinned
     int morton_ntx = -1, morton_nty = -1;
     int morton3_key[3] = {-1, -1, -1};
     long long stats[9] = {0};
-    // Chunked 2-D pipeline: deposits run on a side stream, each behind its chunk's scatter.
+    // Side stream of the chunked host staging (asp_stage_particles).
     hipStream_t side = nullptr;
     hipEvent_t chunk_ev[kMarks] = {};
     hipEvent_t done_ev = nullptr;
@@ -79,9 +78,15 @@ struct Workspace {
     // it, so calls on different streams never overwrite buffers still being read.
     hipEvent_t last_ev = nullptr;
     Buf morton3;  // brick order of the 3-D cube
+    // Host -> device copies of pageable caller arrays go through two pinned bounce
+    // buffers (h2d_staged): the CPU copy of one piece overlaps the DMA of the previous.
+    void* pin[2] = {nullptr, nullptr};
+    hipEvent_t pin_ev[2] = {};
+    bool pin_busy[2] = {false, false};
+    int pin_next = 0;
     std::vector<Buf*> all_bufs() {
         std::vector<Buf*> v = {&hist, &cmx, &tile_total, &tile_start, &tile_k, &items, &merges,
-                               &counters, &recs, &wide, &slabs, &morton, &morton3, &tile_large};
+                               &counters, &recs, &wide, &slabs, &morton, &morton3};
         for (auto& b : in) v.push_back(&b);
         for (auto& b : out) v.push_back(&b);
         for (auto& b : aux) v.push_back(&b);
@@ -127,6 +132,11 @@ inline int ws_end(Workspace& ws, hipStream_t st) {
 
 // asp_stage.hip: reader arrays on the device -> the projector's fp32 working copies
 // (axis selection of _projector.py:38-46, round to nearest), enqueued on st.
+// Pageable host -> device copy through the workspace's pinned bounce buffers, ordered on
+// st (asp_stage.hip).  Returns once every piece's DMA is enqueued; the host source may be
+// reused then (its bytes are in the bounce buffers or already on the device).
+int h2d_staged(Workspace& ws, void* dst, const void* src, size_t bytes, hipStream_t st);
+void release_pinned(Workspace& ws);
 int stage_device(const double* pos, const double* h, const double* a0, const double* a1,
                  long long n, int axis, float* u, float* v, float* hf, float* a0f, float* a1f,
                  hipStream_t st);

@@ -1875,9 +1875,7 @@ static int project2d(const float* u, const float* v, const float* h, const float
         const float* src[5] = {u, v, h, a0, a1};
         for (int k = 0; k < 4 + (nout == 2); ++k) {
             ASP_TRY(ensure(ws.in[k], (size_t)n * sizeof(float)));
-            if (n > 0)
-                ASP_HIP(hipMemcpyAsync(ws.in[k].p, src[k], (size_t)n * sizeof(float),
-                                       hipMemcpyHostToDevice, st));
+            ASP_TRY(h2d_staged(ws, ws.in[k].p, src[k], (size_t)n * sizeof(float), st));
         }
         du = (const float*)ws.in[0].p;
         dv = (const float*)ws.in[1].p;
@@ -1915,6 +1913,7 @@ static int project2d_f64(const double* pos, const double* h, const double* a0,
     ASP_TRY(ws_begin(ws, st));
     const int nout = out1 ? 2 : 1;
     const bool dev = flags & ASP_F_DEVICE_PTRS;
+    const bool dev_out = dev || (flags & ASP_F_DEVICE_OUTPUTS);  // maps stay on the device
     const long long npix = (long long)nx * ny;
     const double *dpos = pos, *dh64 = h, *da0 = a0, *da1 = a1;
     float *d0 = out0, *d1 = out1;
@@ -1924,15 +1923,13 @@ static int project2d_f64(const double* pos, const double* h, const double* a0,
         const size_t words[4] = {3, 1, 1, 1};
         for (int k = 0; k < 3 + (nout == 2); ++k) {
             ASP_TRY(ensure(ws.in64[k], (size_t)n * words[k] * sizeof(double)));
-            if (n > 0)
-                ASP_HIP(hipMemcpyAsync(ws.in64[k].p, src[k], (size_t)n * words[k] * sizeof(double),
-                                       hipMemcpyHostToDevice, st));
+            ASP_TRY(h2d_staged(ws, ws.in64[k].p, src[k], (size_t)n * words[k] * sizeof(double), st));
         }
         dpos = (const double*)ws.in64[0].p;
         dh64 = (const double*)ws.in64[1].p;
         da0 = (const double*)ws.in64[2].p;
         da1 = nout == 2 ? (const double*)ws.in64[3].p : nullptr;
-        ASP_TRY(host_outputs(ws, out0, out1, npix, flags, st, d0, d1));
+        if (!dev_out) ASP_TRY(host_outputs(ws, out0, out1, npix, flags, st, d0, d1));
     }
     for (int k = 0; k < 4 + (nout == 2); ++k) ASP_TRY(ensure(ws.in[k], (size_t)n * sizeof(float)));
     float* f[5] = {(float*)ws.in[0].p, (float*)ws.in[1].p, (float*)ws.in[2].p, (float*)ws.in[3].p,
@@ -1942,8 +1939,8 @@ static int project2d_f64(const double* pos, const double* h, const double* a0,
     const Src64 s{dpos + cols[axis][0], dpos + cols[axis][1], dpos + cols[cull_axis][0],
                   dpos + cols[cull_axis][1], dh64, 3, f[0], f[1], f[2]};
     ASP_TRY(project2d_device(ws, g, s, f[0], f[1], f[2], f[3], f[4], n, kid,
-                             flags | ASP_F_DEVICE_PTRS, d0, d1, st));
-    if (!dev) ASP_TRY(host_results(out0, out1, d0, d1, npix, st));
+                             (flags & ~ASP_F_DEVICE_OUTPUTS) | ASP_F_DEVICE_PTRS, d0, d1, st));
+    if (!dev_out) ASP_TRY(host_results(out0, out1, d0, d1, npix, st));
     return ws_end(ws, st);
 }
 
@@ -1986,9 +1983,8 @@ static int pairs_f64(const double* pos, const double* h, long long n, int axis, 
         ASP_TRY(ensure(ws.in64[0], (size_t)n * 3 * sizeof(double)));
         ASP_TRY(ensure(ws.in64[1], (size_t)n * sizeof(double)));
         if (n > 0) {
-            ASP_HIP(hipMemcpyAsync(ws.in64[0].p, pos, (size_t)n * 3 * sizeof(double),
-                                   hipMemcpyHostToDevice, st));
-            ASP_HIP(hipMemcpyAsync(ws.in64[1].p, h, (size_t)n * sizeof(double), hipMemcpyHostToDevice, st));
+            ASP_TRY(h2d_staged(ws, ws.in64[0].p, pos, (size_t)n * 3 * sizeof(double), st));
+            ASP_TRY(h2d_staged(ws, ws.in64[1].p, h, (size_t)n * sizeof(double), st));
         }
         dpos = (const double*)ws.in64[0].p;
         dh64 = (const double*)ws.in64[1].p;
@@ -2287,6 +2283,7 @@ int asp_release(int32_t device) {
         }
         if (ws.h_counters) (void)hipHostFree(ws.h_counters);
         ws.h_counters = nullptr;
+        release_pinned(ws);
         ws.morton_ntx = ws.morton_nty = -1;
         ws.morton3_key[0] = ws.morton3_key[1] = ws.morton3_key[2] = -1;
     }

@@ -16,6 +16,9 @@
 // bit-identical to it (tests/test_gpu_stage.py against tests/golden/g8_periodic.npz).
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+#include <thread>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -247,8 +250,9 @@ static int stage_particles(const double* pos, const double* h, const double* a0,
             ASP_HIP(hipGetLastError());
         }
     } else {
-        // Host arrays: chunks copied into two device staging sets alternately (stream st,
-        // side stream), so the copy of chunk c + 1 overlaps the conversion of chunk c.
+        // Host arrays: chunks copied (pinned bounce buffers) into two device staging sets
+        // alternately (stream st, side stream): the copy of chunk c + 1 overlaps the
+        // conversion of chunk c.
         ASP_TRY(ensure_side(ws));
         const long long C = std::min<long long>(kStageChunk, n);
         for (int s = 0; s < 2; ++s) ASP_TRY(ensure(ws.aux[s], (size_t)C * 6 * sizeof(double)));
@@ -261,11 +265,10 @@ static int stage_particles(const double* pos, const double* h, const double* a0,
             hipStream_t s = ss[c & 1];
             double* d = (double*)ws.aux[c & 1].p;
             double *dp = d, *dh = d + 3 * C, *d0 = d + 4 * C, *d1 = d + 5 * C;
-            ASP_HIP(hipMemcpyAsync(dp, pos + 3 * i0, (size_t)m * 3 * sizeof(double),
-                                   hipMemcpyHostToDevice, s));
-            if (h) ASP_HIP(hipMemcpyAsync(dh, h + i0, (size_t)m * sizeof(double), hipMemcpyHostToDevice, s));
-            if (a0) ASP_HIP(hipMemcpyAsync(d0, a0 + i0, (size_t)m * sizeof(double), hipMemcpyHostToDevice, s));
-            if (a1) ASP_HIP(hipMemcpyAsync(d1, a1 + i0, (size_t)m * sizeof(double), hipMemcpyHostToDevice, s));
+            ASP_TRY(h2d_staged(ws, dp, pos + 3 * i0, (size_t)m * 3 * sizeof(double), s));
+            if (h) ASP_TRY(h2d_staged(ws, dh, h + i0, (size_t)m * sizeof(double), s));
+            if (a0) ASP_TRY(h2d_staged(ws, d0, a0 + i0, (size_t)m * sizeof(double), s));
+            if (a1) ASP_TRY(h2d_staged(ws, d1, a1 + i0, (size_t)m * sizeof(double), s));
             hipLaunchKernelGGL(k_stage, dim3(grid_for(m)), dim3(kStageBlock), 0, s, S, dp,
                                h ? dh : nullptr, a0 ? d0 : nullptr, a1 ? d1 : nullptr, i0, i0 + m,
                                n, u, v, hf, a0f, a1f, cap, dimg);
@@ -288,6 +291,66 @@ static int stage_particles(const double* pos, const double* h, const double* a0,
                                          std::to_string(*n_out) + " > " + std::to_string(cap) +
                                          "); n_out holds the size needed");
     return ASP_OK;
+}
+
+// ----------------------------------------------------------------------------------
+// Pinned staging (reader arrays -> HBM).  A DMA from pageable
+// memory is staged by the runtime piece by piece with the CPU waiting on each; here two
+// 32 MiB pinned buffers alternate: piece k is copied into buffer k % 2 by 4 host threads
+// while the DMA of piece k - 1 runs, then its DMA is enqueued on the caller's stream.  A
+// buffer is refilled only after its previous DMA completed (event).
+// ----------------------------------------------------------------------------------
+constexpr size_t kPinBytes = (size_t)32 << 20;
+constexpr int kPinThreads = 4;
+
+static void par_copy(char* d, const char* s, size_t n) {
+    if (n < ((size_t)4 << 20)) {
+        memcpy(d, s, n);
+        return;
+    }
+    const size_t part = ((n + kPinThreads - 1) / kPinThreads + 4095) & ~(size_t)4095;
+    std::thread th[kPinThreads - 1];
+    int nt = 0;
+    for (int t = 1; t < kPinThreads; ++t) {
+        const size_t o = part * t;
+        if (o >= n) break;
+        th[nt++] = std::thread([=] { memcpy(d + o, s + o, std::min(part, n - o)); });
+    }
+    memcpy(d, s, std::min(part, n));
+    for (int t = 0; t < nt; ++t) th[t].join();
+}
+
+int h2d_staged(Workspace& ws, void* dst, const void* src, size_t bytes, hipStream_t st) {
+    if (bytes == 0) return ASP_OK;
+    for (int b = 0; b < 2; ++b) {
+        if (!ws.pin[b]) {
+            ASP_HIP(hipHostMalloc(&ws.pin[b], kPinBytes, hipHostMallocDefault));
+            ASP_HIP(hipEventCreateWithFlags(&ws.pin_ev[b], hipEventDisableTiming));
+            ws.pin_busy[b] = false;
+        }
+    }
+    for (size_t off = 0; off < bytes; off += kPinBytes) {
+        const int b = ws.pin_next & 1;
+        ws.pin_next ^= 1;
+        const size_t len = std::min(kPinBytes, bytes - off);
+        if (ws.pin_busy[b]) ASP_HIP(hipEventSynchronize(ws.pin_ev[b]));
+        par_copy((char*)ws.pin[b], (const char*)src + off, len);
+        ASP_HIP(hipMemcpyAsync((char*)dst + off, ws.pin[b], len, hipMemcpyHostToDevice, st));
+        ASP_HIP(hipEventRecord(ws.pin_ev[b], st));
+        ws.pin_busy[b] = true;
+    }
+    return ASP_OK;
+}
+
+void release_pinned(Workspace& ws) {
+    for (int b = 0; b < 2; ++b) {
+        if (ws.pin_busy[b]) (void)hipEventSynchronize(ws.pin_ev[b]);
+        if (ws.pin[b]) (void)hipHostFree(ws.pin[b]);
+        if (ws.pin_ev[b]) (void)hipEventDestroy(ws.pin_ev[b]);
+        ws.pin[b] = nullptr;
+        ws.pin_ev[b] = nullptr;
+        ws.pin_busy[b] = false;
+    }
 }
 
 // Reader arrays already on the device -> fp32 working copies (no periodic options).

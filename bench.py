@@ -41,7 +41,11 @@ def parse():
     ap.add_argument("--h-law", default="pixel", choices=["pixel", "physical"])
     ap.add_argument("--kernel", default="wendland_c2", choices=["wendland_c2", "cubic"])
     ap.add_argument("--map", default="weighted", choices=["weighted", "surface"])
-    ap.add_argument("--op", default="reduce", choices=["reduce", "allreduce", "reduce_scatter"])
+    ap.add_argument("--op", default="reduce",
+                    choices=["reduce", "allreduce", "reduce_scatter", "reduce_scatter_gather"])
+    ap.add_argument("--slab-weight", default="cost", choices=["cost", "count"],
+                    help="N > 1 Z-slab edges: equal modelled work (distributed.slab_cost) or "
+                         "equal particle counts")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget for the bounded CPU-baseline sample")
@@ -444,7 +448,10 @@ def main():
     t0 = time.time()
     d = plummer_torch(args.n, seed=0, h_law=args.h_law, extent=extent, grid=G, device=dev)
     if world > 1:
-        e = zslab_bounds(d["z"], world)
+        from asp_amd.distributed import slab_cost
+        w = None if args.slab_weight == "count" else slab_cost(d["x"], d["y"], d["h"], ext, 2 * extent / G)
+        e = zslab_bounds(d["z"], world, weights=w)
+        del w
         keep = (d["z"] >= e[rank]) & (d["z"] < e[rank + 1])
         d = {k: v[keep].contiguous() for k, v in d.items()}
     u, v, h = d["x"], d["y"], d["h"]
@@ -576,7 +583,8 @@ def main():
                    "particles": args.n, "grid": G, "kernel": args.kernel, "h_law": args.h_law,
                    "map": args.map, "parallelism": f"zslab{world}" if world > 1 else "single",
                    "accumulation": "int64 fixed point" if args.deterministic else "fp64",
-                   "collective_overlap": nbuf > 1},
+                   "collective_overlap": nbuf > 1,
+                   **({"slab_weight": args.slab_weight, "collective": args.op} if world > 1 else {})},
         "particles_per_s": pps,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -48,6 +48,10 @@ extern "C" {
                                  * input-order independent maps; relative precision degrades
                                  * for pixels below ~2^-37 n_t max|A W| of their 64x64 tile
                                  * (DESIGN.md §4).  Default: fp64 accumulation.            */
+#define ASP_F_DEVICE_OUTPUTS 0x10 /* host (pageable) inputs, device outputs: the reader's
+                                   * arrays in, a device map out for the RCCL sum; the
+                                   * inputs go through pinned bounce buffers (two 32 MiB
+                                   * pieces, CPU copy overlapping the DMA)                 */
 
 /* asp_project2d_f64 axis: cull on axis c's columns (the reference's mixed spellings) */
 #define ASP_AXIS_CULL(c) (((c) + 1) << 4)

@@ -72,6 +72,11 @@ def _worker(rank, world, port, q):
                                        image_size=(G, G), extent=EXT, chunk_size=16,
                                        kernel="cubic", op=op, projector=_oracle_projector)
             res[op] = (o0.numpy().copy(), o1.numpy().copy())
+        o0, _ = project2d_sharded(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3],
+                                  image_size=(G, G), extent=EXT, chunk_size=16, kernel="cubic",
+                                  op="reduce_scatter_gather", projector=_oracle_projector,
+                                  out0=torch.empty((G, G)), out1=torch.empty((G, G)))
+        res["rsg"] = o0.numpy().copy()
         maps = torch.empty((2, G, G))  # adjacent maps: one fused collective
         for op in ("reduce", "allreduce"):
             o0, o1 = project2d_sharded(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3],
@@ -136,8 +141,111 @@ def test_zslab_sharded_sum_world2():
         np.testing.assert_allclose(out[r]["pipelined"][2], full0, atol=tol, rtol=0)
         rows = slice(r * G // world, (r + 1) * G // world)
         np.testing.assert_allclose(out[r]["reduce_scatter"][0], full0[rows], atol=tol, rtol=0)
+        # reduce-scatter, then the one map all-gathered: the full map on every rank
+        np.testing.assert_allclose(out[r]["rsg"], full0, atol=tol, rtol=0)
     # the slabs really are partial maps: neither rank alone holds the full map
     assert not np.allclose(out[1]["reduce"][0], full0, atol=tol)
+
+
+# ------------------------------------------- reader fp64 host arrays -> stage -> reduce
+def _oracle_f64(positions, h, a0, a1, *, projection_axis, image_size, extent, chunk_size,
+                kernel, out0, out1, device, deterministic=False):
+    """The local projection of project2d_sharded_host on CPU: the oracle on the rank's own
+    float64 host arrays (the GPU path is asp_project2d_f64 with ASP_F_DEVICE_OUTPUTS)."""
+    import pyoracle
+    from asp_amd._axes import reference_axes
+    u, v, cu, cv = pyoracle._axes(positions, reference_axes(projection_axis))
+    o0, o1 = pyoracle.project_scatter(u, v, h, a0, a1, image_size, chunk_size, *extent,
+                                      kernel=kernel, cu=cu, cv=cv)
+    t0 = torch.from_numpy(o0.astype(np.float32))
+    t1 = None if o1 is None else torch.from_numpy(o1.astype(np.float32))
+    return t0, t1
+
+
+def _f64_data():
+    import sys
+    sys.path.insert(0, PKG_ROOT)
+    from asp_amd.plummer import plummer
+    rng = np.random.default_rng(9)
+    p = plummer(3000, seed=4, h_law="physical")
+    pos = p["pos"] * (1.0 + rng.uniform(-3e-9, 3e-9, p["pos"].shape))  # off the fp32 grid
+    return pos, p["h"], p["m"], p["m"] * p["T"]
+
+
+def _host_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, PKG_ROOT)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from asp_amd.distributed import project2d_sharded_host
+        pos, h, m, mT = _f64_data()
+        # the reader's own split: every other particle (any split works for the sum)
+        sel = slice(rank, None, world)
+        res = {}
+        for op in ("reduce", "allreduce"):
+            o0, o1 = project2d_sharded_host(np.ascontiguousarray(pos[sel]), h[sel], mT[sel],
+                                            m[sel], projection_axis=2, image_size=(G, G),
+                                            extent=EXT, chunk_size=16, kernel="cubic", op=op,
+                                            projector=_oracle_f64)
+            res[op] = (o0.numpy().copy(), o1.numpy().copy())
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_from_fp64_host_arrays_world2():
+    """Each rank hands its own raw-fp64 host arrays to project2d_sharded_host; the summed
+    map equals the oracle over all particles (fp64 decisions on the same values)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    pos, h, m, mT = _f64_data()
+    full0, full1 = pyoracle.project_scatter(pos[:, 0], pos[:, 1], h, mT, m, (G, G), 16, *EXT,
+                                            kernel="cubic")
+    t0, t1 = 1e-5 * np.abs(full0).max(), 1e-5 * np.abs(full1).max()
+    np.testing.assert_allclose(out[0]["reduce"][0], full0, atol=t0, rtol=0)
+    np.testing.assert_allclose(out[0]["reduce"][1], full1, atol=t1, rtol=0)
+    for r in range(world):
+        np.testing.assert_allclose(out[r]["allreduce"][0], full0, atol=t0, rtol=0)
+        np.testing.assert_allclose(out[r]["allreduce"][1], full1, atol=t1, rtol=0)
+
+
+def test_pair_weighted_zslabs():
+    """zslab_bounds with slab_cost weights: equal modelled work, not equal counts -- at
+    physical h the core slabs hold fewer particles than the outer ones."""
+    import sys
+    sys.path.insert(0, PKG_ROOT)
+    from asp_amd.distributed import slab_cost, zslab_bounds
+    from asp_amd.plummer import plummer
+    p = plummer(200_000, seed=3, h_law="physical")
+    x, y, z = (torch.tensor(p["pos"][:, k]) for k in range(3))
+    h = torch.tensor(p["h"])
+    w = slab_cost(x, y, h, (-4.0, 4.0, -4.0, 4.0), 8.0 / 2048)
+    for W in (2, 4, 8):
+        e = zslab_bounds(z, W, weights=w)
+        assert len(e) == W + 1 and e[0] == float("-inf") and e[-1] == float("inf")
+        sums = [float(w[(z >= e[r]) & (z < e[r + 1])].sum()) for r in range(W)]
+        counts = [int(((z >= e[r]) & (z < e[r + 1])).sum()) for r in range(W)]
+        assert max(sums) / min(sums) < 1.10, sums
+        if W == 8:
+            assert max(counts) / min(counts) > 1.5, counts  # work balance != count balance
+    e = zslab_bounds(z, 4)
+    counts = [int(((z >= e[r]) & (z < e[r + 1])).sum()) for r in range(4)]
+    assert max(counts) / min(counts) < 1.05
 
 
 # --------------------------------------------------------------------------- 3-D cube
