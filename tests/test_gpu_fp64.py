@@ -147,3 +147,27 @@ def test_raw_fp64_nonsquare_mixed_axis_vs_oracle(gpu, oracle):
     c_ref, _ = oracle.project_scatter(u, v, h, np.ones(n), None, size, cs, *ext,
                                       kernel="indicator", cu=cu, cv=cv)
     assert np.array_equal(cnt, c_ref)
+
+
+def test_host_inputs_device_outputs_pinned_staging(gpu):
+    """Reader fp64 host arrays -> pinned bounce buffers (several 32 MiB pieces: 3e6
+    particles = 72 MB of positions) -> device map (ASP_F_DEVICE_OUTPUTS, the RCCL-sum
+    input of project2d_sharded_host): bit-identical to the host-output call, and to the
+    same arrays handed over as device tensors."""
+    import torch
+    from asp_amd.device import project2d_f64
+    rng = np.random.default_rng(5)
+    n = 3_000_000
+    pos = rng.normal(0, 0.6, (n, 3))
+    h = rng.uniform(0.002, 0.01, n)
+    a0, a1 = rng.uniform(0.5, 2.0, n), rng.uniform(0.5, 2.0, n)
+    # fixed-point accumulation: bitwise reproducible, so the three calls must agree exactly
+    kw = dict(image_size=(512, 384), extent=(-2.0, 2.0, -1.5, 1.5), kernel="wendland_c2",
+              deterministic=True)
+    r0, r1 = project2d_f64(pos, h, a0, a1, **kw)
+    d0, d1 = project2d_f64(pos, h, a0, a1, device_out=True, **kw)
+    assert d0.is_cuda and d1.is_cuda
+    assert np.array_equal(d0.cpu().numpy(), r0) and np.array_equal(d1.cpu().numpy(), r1)
+    t = [torch.from_numpy(x).cuda() for x in (pos, h, a0, a1)]
+    e0, e1 = project2d_f64(*t, **kw)
+    assert np.array_equal(e0.cpu().numpy(), r0) and np.array_equal(e1.cpu().numpy(), r1)
