@@ -5,14 +5,36 @@ Same names, arguments and results; the arithmetic is the reference's fp64 NumPy
 operation sequence, done by ``asp_periodic`` / ``asp_wrapped_distance`` (asp_stage.hip),
 bit-identical to it (tests/test_gpu_stage.py against the golden vectors G8, produced by
 running the reference's own function bodies).  NumPy inputs give NumPy results; float64
-torch tensors on the GPU stay there.  unyt units are dropped (as the projector drops
-them, reference semantics S10).  There is no CPU fallback: without a GPU these raise.
+torch tensors on the GPU stay there.  There is no CPU fallback: without a GPU these raise.
+
+unyt arrays: the reference registers unyt overloads of ``calculate_periodic``,
+``shift_origin`` and ``shift_centre`` (:49-51, :58-60, :70-72) that convert every operand
+to one unit, run the NumPy body on the values and rewrap the result in that unit; the
+wrapped displacement / distance work on unyt arrays through NumPy's unit propagation
+(result in the units of ``to_positions``, squared for a squared distance).  The same is
+done here for any unit-carrying array (``.value``, ``.units``, ``.to(units)`` -- unyt's
+interface; unyt itself is not installed in this image, so the tests drive it with a
+stand-in class: parity with unyt is unpinned beyond that interface).
 """
 from __future__ import annotations
 
 import numpy as np
 
 from .. import _lib
+
+
+def _has_units(x) -> bool:
+    return hasattr(x, "units") and hasattr(x, "value") and hasattr(x, "to")
+
+
+def _in(x, units):
+    """The numerical values of ``x`` in ``units`` (plain arrays pass through)."""
+    return x.to(units).value if _has_units(x) else x
+
+
+def _wrap(like, values, units):
+    """``values`` as an array of ``like``'s unit-carrying type, in ``units``."""
+    return type(like)(values, units=units)
 
 
 def _prep(x):
@@ -57,6 +79,10 @@ def _run(op, a, b, box_width, origin_is_centre=False):
 def calculate_wrapped_displacement(from_positions, to_positions, box_width):
     """``to - from`` with every component farther than half a box brought back by one box
     width (reference :10-20)."""
+    if _has_units(to_positions):
+        u = to_positions.units
+        return _wrap(to_positions, _run(_lib.ASP_PB_DISPLACEMENT, _in(from_positions, u),
+                                        to_positions.value, _in(box_width, u)), u)
     return _run(_lib.ASP_PB_DISPLACEMENT, from_positions, to_positions, box_width)
 
 
@@ -65,6 +91,11 @@ def calculate_wrapped_distance(from_position, to_positions, box_width,
     """Length of the wrapped displacement (reference :22-34): rows of 3 for (N, 3)
     inputs, a scalar for two (3,) vectors."""
     import torch
+    if _has_units(to_positions):
+        u = to_positions.units
+        d = calculate_wrapped_distance(_in(from_position, u), to_positions.value,
+                                       _in(box_width, u), do_squared_distance)
+        return _wrap(to_positions, d, u ** 2 if do_squared_distance else u)
     tf, nf = _prep(from_position)
     tt, nt = _prep(to_positions)
     shape = torch.broadcast_shapes(tf.shape, tt.shape)
@@ -86,6 +117,10 @@ def calculate_wrapped_distance(from_position, to_positions, box_width,
 def make_periodic(positions, box_width, origin_is_centre: bool = False):
     """Wrap every coordinate outside the box back by one box width, IN PLACE
     (reference :36-43)."""
+    if _has_units(positions):  # the reference's body on a unyt array: values, same unit
+        vals = positions.value
+        make_periodic(vals, _in(box_width, positions.units), origin_is_centre)
+        return
     res = _run(_lib.ASP_PB_WRAP, positions, None, box_width, origin_is_centre)
     if isinstance(res, np.ndarray):
         positions[...] = res
@@ -94,18 +129,31 @@ def make_periodic(positions, box_width, origin_is_centre: bool = False):
 
 
 def calculate_periodic(start_positions, box_width, origin_is_centre: bool = False):
-    """A wrapped copy (reference :45-48)."""
+    """A wrapped copy (reference :45-48; unyt overload :49-51: in the positions' unit)."""
+    if _has_units(start_positions):
+        u = start_positions.units
+        return _wrap(start_positions, calculate_periodic(start_positions.value,
+                                                         _in(box_width, u), origin_is_centre), u)
     return _run(_lib.ASP_PB_WRAP, start_positions, None, box_width, origin_is_centre)
 
 
 def shift_origin(start_positions, new_origin, box_width, origin_is_centre: bool = False):
-    """Positions relative to ``new_origin``, wrapped (reference :54-57)."""
+    """Positions relative to ``new_origin``, wrapped (reference :54-57; unyt overload
+    :58-60: everything in the new origin's unit)."""
+    if _has_units(start_positions):
+        u = new_origin.units
+        return _wrap(start_positions, shift_origin(start_positions.to(u).value, new_origin.value,
+                                                   _in(box_width, u), origin_is_centre), u)
     return _run(_lib.ASP_PB_SHIFT_ORIGIN, start_positions, new_origin, box_width,
                 origin_is_centre)
 
 
 def shift_centre(start_positions, new_centre, box_width, origin_is_centre: bool = False):
     """Positions moved so that ``new_centre`` is the box centre, wrapped (reference
-    :63-69)."""
+    :63-69; unyt overload :70-72: everything in the new centre's unit)."""
+    if _has_units(start_positions):
+        u = new_centre.units
+        return _wrap(start_positions, shift_centre(start_positions.to(u).value, new_centre.value,
+                                                   _in(box_width, u), origin_is_centre), u)
     return _run(_lib.ASP_PB_SHIFT_CENTRE, start_positions, new_centre, box_width,
                 origin_is_centre)

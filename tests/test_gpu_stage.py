@@ -190,3 +190,49 @@ def test_stage_periodic_images_large_h(gpu, oracle):
     h[0] = 2.0 * L  # 2|h| = 4 L
     with pytest.raises(NotImplementedError):
         stage_particles(pos, h, A, projection_axis=2, box_width=L, shift="wrap", images=True)
+
+
+class _Unit:
+    """Stand-in for a unyt Unit (unyt is not installed here): a name and a scale."""
+    def __init__(self, name, scale):
+        self.name, self.scale = name, scale
+
+    def __pow__(self, k):
+        return _Unit(f"{self.name}**{k}", self.scale ** k)
+
+    def __eq__(self, other):
+        return self.name == other.name
+
+
+class _Q:
+    """Stand-in for unyt_array: .value, .units, .to(units), ctor (values, units=...)."""
+    def __init__(self, value, units):
+        self.value, self.units = np.asarray(value, dtype=np.float64), units
+
+    def to(self, units):
+        return _Q(self.value * (self.units.scale / units.scale), units)
+
+
+def test_periodic_helpers_unit_overloads(gpu, g8):
+    """The reference's unyt overloads (_periodic_box_manipulations.py:49-51, :58-60,
+    :70-72): operands converted to one unit (the positions' for calculate_periodic, the
+    new origin's / centre's for the shifts), the NumPy body on the values, the result
+    rewrapped in that unit.  Values must equal the plain call on the converted values."""
+    from asp_amd.tools import (calculate_periodic, calculate_wrapped_distance, shift_centre,
+                               shift_origin)
+    kpc, Mpc = _Unit("kpc", 1.0), _Unit("Mpc", 1000.0)
+    L, pos, c = float(g8["L"]), g8["pos"], g8["centre"]
+    P = _Q(pos * 1000.0, kpc)           # positions in kpc
+    C = _Q(c, Mpc)
+    B = _Q(L, Mpc)
+    r = calculate_periodic(P, B, False)
+    assert isinstance(r, _Q) and r.units == kpc
+    assert np.array_equal(bits(r.value), bits(calculate_periodic(P.value, L * 1000.0, False)))
+    for f in (shift_origin, shift_centre):
+        r = f(P, C, B, True)
+        assert isinstance(r, _Q) and r.units == Mpc
+        assert np.array_equal(bits(r.value), bits(f(P.to(Mpc).value, c, L, True)))
+    d = calculate_wrapped_distance(_Q(c, Mpc), P, B, True)
+    assert isinstance(d, _Q) and d.units == kpc ** 2
+    assert np.array_equal(bits(d.value), bits(calculate_wrapped_distance(c * 1000.0, P.value,
+                                                                         L * 1000.0, True)))

@@ -28,7 +28,7 @@ STAGE_OF = {"k_count": "count", "k_colscan": "colscan", "k_tilescan": "tilescan"
 
 
 def short(name):
-    m = re.search(r"asp::(k_\w+)(<[^>]*>)?", name)
+    m = re.search(r"asp::(k[0-9]?_\w+)(<[^>]*>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else None
 
 
