@@ -1694,6 +1694,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     if (const char* e = getenv("ASP_BIN_BLOCKS")) max_blk = std::max(1, atoi(e));
     pl.nblk = std::min<long long>(max_blk, std::max<long long>(1, (n + 8191) / 8192));
     pl.grp = kScatterGroup;
+    if (const char* e = getenv("ASP_SCATTER_GROUP")) pl.grp = std::max(1, atoi(e));
     pl.nblk_s = (pl.nblk + pl.grp - 1) / pl.grp;
     const bool det = (flags & ASP_F_DETERMINISTIC) != 0;
     ASP_TRY(ensure(ws.hist, (size_t)pl.nblk * 2 * g.ntiles * sizeof(int)));
