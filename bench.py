@@ -388,7 +388,7 @@ def run_ion(args, dev):
     print(json.dumps(res), flush=True)
 
 
-def output_check(out0, out1, a0, a1, ratio, world=1):
+def output_check(out0, out1, a0, a1, ratio, world=1, gathered_ratio=False):
     """Size-independent sanity of the timed map (the parity proper is tests/): finite,
     non-negative component sums (W >= 0, m > 0), and for the mass-weighted map every pixel a
     weighted MEAN of particle temperatures -- inside [min T, max T] wherever sum m W > 0,
@@ -398,6 +398,8 @@ def output_check(out0, out1, a0, a1, ratio, world=1):
         return False
     if not ratio:
         return bool((out0 >= 0).all().item()) and float(out0.sum().item()) > 0
+    if gathered_ratio:  # reduce_scatter_gather: out0 is the all-gathered ratio map, out1
+        out1 = out0     # this rank's own (unreduced) component: coverage from out0 itself
     if not bool(torch.isfinite(out1).all().item()) or not bool((out1 >= 0).all().item()):
         return False
     t = a0 / a1
@@ -533,7 +535,11 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    ok = output_check(out0, out1, a0, a1, ratio, world)
+    if world > 1 and args.op == "reduce_scatter":
+        ok = None  # the reduced map lives as row slabs returned to step(); not checked here
+    else:
+        ok = output_check(out0, out1, a0, a1, ratio, world,
+                          gathered_ratio=world > 1 and args.op == "reduce_scatter_gather")
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -607,7 +613,7 @@ def main():
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    if not ok:
+    if ok is False:
         log("bench: the timed map FAILED its output check")
         sys.exit(3)
 
