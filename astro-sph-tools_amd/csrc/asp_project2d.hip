@@ -20,12 +20,15 @@
 //                accumulators; boxes of <= 4 x 4 pixels lane-per-record, mid-size boxes
 //                swept by a whole wave (LDS atomics); the tile is written once, or (split
 //                tiles) stored as a partial slab
-//   K4g gather   one workgroup per work item of the large stream: the records go to an
-//                LDS list every wave walks, each thread summing its own 8 pixels in
-//                registers (no per-pair atomics); tile or slab written from registers
+//   K4g gather   the large stream: one single-wave workgroup per (work item, 16 x 32
+//                region of the tile); the wave streams the item's records into per-lane
+//                entries, walks those meeting its region with v_readlane (fields in
+//                SGPRs), each lane summing one pixel of each 8 x 8 block in registers
+//                (packed fp32, no per-pair atomics); tile or slab written from registers
 //   K5 merge     split tiles: sum of their slabs in slab order, write
-//   K6 wide      particles overlapping > wide_tiles tiles, per tile, gathered
+//   K6 wide      particles overlapping > wide_tiles tiles, per tile region, gathered
 //   K7 ratio     out0 / out1 (mass-weighted maps) when not fused into K4/K5
+//   K8 pairs     the kernel_func plug-in: every included (pixel, particle, r^2) pair
 //
 // No MFMA: this is gather/scatter work; the bounds are HBM bytes and VALU/LDS-atomic
 // issue.

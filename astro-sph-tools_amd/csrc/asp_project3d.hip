@@ -198,6 +198,22 @@ struct Rec3 {
     Box3 b;               // clipped to the brick, brick-local indices
 };
 
+// Edge-continuous kernels (cubic, Wendland) take no per-voxel decision (as the 2-D gather,
+// DESIGN.md §3): f(q) written to give exactly 0 for q >= 2, evaluated in fp32 from fp32
+// corner offsets, so a voxel whose exact test differs contributes < 2^-60 W(0).  The
+// indicator kernel keeps the fp64 test (bit-exact voxel counts).
+template <int KID>
+__device__ __forceinline__ float edge_shape3(float q) {
+    const float t = fminf(fmaxf(fmaf(-0.5f, q, 1.0f), 0.0f), 1.0f);
+    if constexpr (KID == 0) {
+        const float s = fminf(fmaxf(1.0f - q, 0.0f), 1.0f);
+        return fmaf(-(s * s), s, 2.0f * (t * t) * t);  // (2-q)^3/4 - max(1-q, 0)^3
+    } else {
+        const float t2 = t * t;
+        return (t2 * t2) * fmaf(2.0f, q, 1.0f);
+    }
+}
+
 // One (i, j) column of a record's box.  The oracle's test is
 //   r2 = dx * dx + dy * dy + dz * dz  <  (2h)^2      (voxel_pass, left to right in fp64)
 // so s = dx * dx + dy * dy is the same intermediate for every k of the column, and only
@@ -246,7 +262,20 @@ __device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, i
     double s;
     int a, b;
     if (!column_range(g, R, li, lj, xt, yt, s, a, b)) return;
-    for (int lk = a; lk <= b; ++lk) voxel3<KID>(R, s, li, lj, lk, zt, acc);
+    if constexpr (KID == 2) {
+        for (int lk = a; lk <= b; ++lk) voxel3<KID>(R, s, li, lj, lk, zt, acc);
+    } else {  // fp32 from here: dz against the plane offsets, no decision
+        const float sf = (float)s;
+        const float zr = (float)(R.z - zt[0]);  // z relative to the brick's first plane
+        const float pz = (float)g.pz;
+        double* col = acc + (li * kBY + lj) * kBZP;
+        for (int lk = a; lk <= b; ++lk) {
+            const float dz = fmaf(-(float)lk, pz, zr);
+            const float q = __builtin_amdgcn_sqrtf(fmaf(dz, dz, sf)) * R.hinv;
+            const float w = edge_shape3<KID>(q);
+            if (w != 0.0f) atomicAdd(&col[lk], (double)(R.s * w));
+        }
+    }
 }
 
 template <int KID>
