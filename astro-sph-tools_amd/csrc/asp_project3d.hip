@@ -259,13 +259,23 @@ template <int KID>
 __device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, int lj, int K0,
                                         const double* xt, const double* yt, const double* zt,
                                         double* acc) {
-    double s;
-    int a, b;
-    if (!column_range(g, R, li, lj, xt, yt, s, a, b)) return;
     if constexpr (KID == 2) {
+        double s;
+        int a, b;
+        if (!column_range(g, R, li, lj, xt, yt, s, a, b)) return;
         for (int lk = a; lk <= b; ++lk) voxel3<KID>(R, s, li, lj, lk, zt, acc);
-    } else {  // fp32 from here: dz against the plane offsets, no decision
-        const float sf = (float)s;
+    } else {  // fp32 throughout: the column's plane range and dz, no decision
+        const float dx = (float)(R.x - xt[li]), dy = (float)(R.y - yt[lj]);
+        const float sf = fmaf(dx, dx, dy * dy);
+        const float thr = (float)R.thr;
+        if (!(sf < thr * (1.0f + 0x1p-20f))) return;  // the column misses the sphere
+        // the planes of q < 2 (W > 0): |dz| < sqrt(thr - s), widened well past the roundings
+        float rz = __builtin_amdgcn_sqrtf(fmaxf(thr - sf, 0.0f) + thr * 0x1p-20f) * (float)g.ipz;
+        rz = rz * (1.0f + 0x1p-18f) + 0x1p-10f;
+        const float fa = fmaxf(ceilf(R.kc - rz), (float)R.b.k0);
+        const float fb = fminf(floorf(R.kc + rz), (float)R.b.k1);
+        if (!(fa <= fb)) return;
+        const int a = (int)fa, b = (int)fb;
         const float zr = (float)(R.z - zt[0]);  // z relative to the brick's first plane
         const float pz = (float)g.pz;
         double* col = acc + (li * kBY + lj) * kBZP;
@@ -478,6 +488,7 @@ static bool make_grid3(const double* ext, int nx, int ny, int nz, int k_lo, int 
     g.nb = nb > kMaxBricks ? -1 : (int)nb;
     g.lane_cols = kLaneCols;
     if (const char* e = getenv("ASP_CUBE_LANE_COLS")) g.lane_cols = std::max(0, atoi(e));
+
     return true;
 }
 
