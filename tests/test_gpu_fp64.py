@@ -171,3 +171,37 @@ def test_host_inputs_device_outputs_pinned_staging(gpu):
     t = [torch.from_numpy(x).cuda() for x in (pos, h, a0, a1)]
     e0, e1 = project2d_f64(*t, **kw)
     assert np.array_equal(e0.cpu().numpy(), r0) and np.array_equal(e1.cpu().numpy(), r1)
+
+
+def test_sharded_host_arrays_single_rank_hip_path(gpu):
+    """project2d_sharded_host through the real HIP path (a world-1 gloo group on the GPU
+    box): the rank's fp64 host arrays -> pinned staging -> device maps -> collective ->
+    ratio on the device; equal to project2d_f64 on the same arrays (fixed point: bitwise)."""
+    import os
+    import socket
+    import torch
+    import torch.distributed as dist
+    from asp_amd.device import project2d_f64
+    from asp_amd.distributed import project2d_sharded_host
+    rng = np.random.default_rng(8)
+    n = 400_000
+    pos = rng.normal(0, 0.5, (n, 3))
+    h = rng.uniform(0.003, 0.02, n)
+    m, T = rng.uniform(0.5, 2.0, n), rng.uniform(1e3, 1e5, n)
+    kw = dict(image_size=(256, 256), extent=(-2.0, 2.0, -2.0, 2.0), chunk_size=64,
+              kernel="wendland_c2", deterministic=True)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        r, _ = project2d_sharded_host(pos, h, m * T, m, ratio=True, op="reduce", **kw)
+    finally:
+        dist.destroy_process_group()
+    c0, c1 = project2d_f64(pos, h, m * T, m, **{k: v for k, v in kw.items()})
+    want = np.where(c1 != 0, c0 / np.where(c1 != 0, c1, 1), 0).astype(np.float32)
+    got = r.cpu().numpy()
+    assert r.is_cuda
+    np.testing.assert_allclose(got, want, rtol=2e-7, atol=0)
