@@ -206,6 +206,7 @@ inline int ensure(Buf& b, size_t bytes) {
                                        hipGetErrorString(e));
     }
     b.cap = want;
+    if (getenv("ASP_PRINT_ALLOC")) fprintf(stderr, "asp alloc %zu B at %p\n", want, b.p);
     return ASP_OK;
 }
 

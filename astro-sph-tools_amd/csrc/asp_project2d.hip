@@ -180,6 +180,16 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
     for (int t = threadIdx.x; t < 2 * g.ntiles; t += kCountBlock) row[t] = lh[t];
 }
 
+// Record stores of the scatter (ASP_NT_STORE: non-temporal, experiment).
+__device__ __forceinline__ void rec_store(float4* dst, float4 v) {
+#ifdef ASP_NT_STORE
+    typedef float nt4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store((nt4){v.x, v.y, v.z, v.w}, (nt4*)dst);
+#else
+    *dst = v;
+#endif
+}
+
 template <int NOUT>
 __device__ __forceinline__ void load_props(const float* __restrict__ a0,
                                            const float* __restrict__ a1, long long base,
@@ -308,12 +318,12 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                         first_slot[k] = slot;  // written by the paired store below
                         first_box[k] = bp;
                     } else {
-                        recs[2 * (long long)slot] =
-                            make_float4((float)(U - corner_x(g, max(b.x0, tx * kTile))),
-                                        (float)(V - corner_y(g, max(b.y0, ty * kTile))), ph[k],
-                                        cf0);
-                        recs[2 * (long long)slot + 1] =
-                            make_float4(cf1, __int_as_float(p), band, __uint_as_float(bp));
+                        rec_store(&recs[2 * (long long)slot],
+                                  make_float4((float)(U - corner_x(g, max(b.x0, tx * kTile))),
+                                              (float)(V - corner_y(g, max(b.y0, ty * kTile))),
+                                              ph[k], cf0));
+                        rec_store(&recs[2 * (long long)slot + 1],
+                                  make_float4(cf1, __int_as_float(p), band, __uint_as_float(bp)));
                     }
                 }
         }
@@ -335,7 +345,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                 int src = half * 32 + (lane >> 1);
                 int slot = __shfl(first_slot[k], src);
                 float4 val = st[2 * src + (lane & 1)];
-                if (slot >= 0) recs[2 * (long long)slot + (lane & 1)] = val;
+                if (slot >= 0) rec_store(&recs[2 * (long long)slot + (lane & 1)], val);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -503,8 +513,16 @@ __device__ __forceinline__ void rec_prep(const float4& r0, const float4& r1, int
 }
 
 __device__ __forceinline__ void load_rec(const float4* recs, long long i, float4& r0, float4& r1) {
+#ifdef ASP_NT_LOAD
+    typedef float nt4 __attribute__((ext_vector_type(4)));
+    const nt4 a = __builtin_nontemporal_load((const nt4*)&recs[2 * i]);
+    const nt4 b = __builtin_nontemporal_load((const nt4*)&recs[2 * i + 1]);
+    r0 = make_float4(a.x, a.y, a.z, a.w);
+    r1 = make_float4(b.x, b.y, b.z, b.w);
+#else
     r0 = recs[2 * i];
     r1 = recs[2 * i + 1];
+#endif
 }
 
 constexpr int kTilePix = kTile * kTile;
