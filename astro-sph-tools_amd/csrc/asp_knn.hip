@@ -203,6 +203,35 @@ __device__ __forceinline__ long long lower_bound(const unsigned long long* __res
     return lo;
 }
 
+// Cell table of one Morton level L (the finest level with about one particle per cell):
+// tab[c] = the first sorted index whose key lies in cell c or later (c < 8^L), tab[8^L] = n.
+// A cell of any level <= L is then a range [tab[.], tab[.]) by two loads instead of two
+// binary searches over the whole array; finer cells search inside their level-L cell only.
+struct CellTab {
+    const int* tab;
+    int sh;  // 63 - 3 L: key >> sh = the level-L cell
+};
+
+__global__ __launch_bounds__(kKnnBlock) void k_cell_table(const unsigned long long* __restrict__ keys,
+                                                           long long n, int sh, int* __restrict__ tab) {
+    long long i = (long long)blockIdx.x * kKnnBlock + threadIdx.x;
+    if (i >= n) return;
+    const long long c = (long long)(keys[i] >> sh);
+    const long long cp = i == 0 ? -1 : (long long)(keys[i - 1] >> sh);
+    for (long long q = cp + 1; q <= c; ++q) tab[q] = (int)i;  // the cells starting here
+}
+
+// First index with key >= k0 (k0 < 2^63), through the table.
+__device__ __forceinline__ long long cell_lower(const unsigned long long* __restrict__ keys,
+                                                long long n, const CellTab& T,
+                                                unsigned long long k0) {
+    const long long c = (long long)(k0 >> T.sh);
+    const long long a = T.tab[c];
+    if ((unsigned long long)c << T.sh == k0) return a;  // k0 starts a level-L cell
+    const long long b = T.tab[c + 1];
+    return a + lower_bound(keys + a, b - a, k0);
+}
+
 // The whole search for particle i by one lane: returns its k-th smallest d2.
 template <int K>
 __device__ __forceinline__ double knn_thread(long long i, const double* __restrict__ xs,
@@ -377,7 +406,7 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict
                                                         const int* __restrict__ idx, long long n,
                                                         int k, const KGrid* __restrict__ g,
                                                         double* __restrict__ h, int diag,
-                                                        int whalf, int fine) {
+                                                        int whalf, int fine, CellTab CT) {
     __shared__ double sx[kKnnBlock / 64][64], sy[kKnnBlock / 64][64], sz[kKnnBlock / 64][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long long base = ((long long)blockIdx.x * (kKnnBlock / 64) + wv) * 64;
@@ -425,8 +454,8 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict
                         md += d * d;
                     }
                     if (md * (1.0 - 0x1p-40) > C.T.mx) continue;
-                    long long j0 = lower_bound(keys, n, k0);
-                    long long j1 = sh3 >= 63 ? n : lower_bound(keys + j0, n - j0, k1) + j0;
+                    long long j0 = cell_lower(keys, n, CT, k0);
+                    long long j1 = sh3 >= 63 || (k1 >> 63) ? n : cell_lower(keys, n, CT, k1);
                     for (long long j = j0; j < min(j1, win0); ++j)
                         C.T.insert(dist2(x, y, z, xs[j], ys[j], zs[j]));
                     for (long long j = max(j0, win1); j < j1; ++j)
@@ -491,6 +520,17 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     hipLaunchKernelGGL(k_gather, dim3(grid), dim3(kKnnBlock), 0, st, dpos, (long long)n,
                        (const int*)iout, xs, ys, zs);
     ASP_LAUNCHED();
+    // level-L cell table: about one particle per cell, at most 8^9 cells (512 MiB)
+    int L = 1;
+    while (L < 9 && (1LL << (3 * L)) < n) ++L;
+    const long long ncell = 1LL << (3 * L);
+    ASP_TRY(ensure(ws.knn[7], (size_t)(ncell + 1) * sizeof(int)));
+    int* tab = (int*)ws.knn[7].p;
+    ASP_HIP(hipMemsetD32Async((hipDeviceptr_t)tab, (int)n, (size_t)(ncell + 1), st));
+    const CellTab CT{tab, 63 - 3 * L};
+    hipLaunchKernelGGL(k_cell_table, dim3(grid), dim3(kKnnBlock), 0, st,
+                       (const unsigned long long*)kout, (long long)n, CT.sh, tab);
+    ASP_LAUNCHED();
     // diagnostics only: ASP_KNN_THREAD = one lane per particle throughout;
     // ASP_KNN_DIAG = 1: the window pass alone (wrong results, timing)
     const bool per_thread = getenv("ASP_KNN_THREAD") != nullptr;
@@ -509,7 +549,7 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
                                dim3(kKnnBlock), 0, st, (const double*)xs, (const double*)ys,      \
                                (const double*)zs, (const unsigned long long*)kout,                \
                                (const int*)iout, (long long)n, k, (const KGrid*)dg, dh, diag, whalf,  \
-                               fine);    \
+                               fine, CT);    \
     } while (0)
     if (k <= 32)
         ASP_KNN(32);
