@@ -390,4 +390,41 @@ __device__ __forceinline__ int bcast(int x, int lane) {
     return __builtin_amdgcn_readlane(x, lane);
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_* ops)
+
+// Shape f(q) / kShapeScale for kernels that vanish continuously at q = 2 (cubic,
+// Wendland), written so that q >= 2 gives exactly 0 without a comparison, two pixels per
+// packed instruction: t = clamp(1 - q/2) (the VOP3P clamp bit; 1 - q/2 <= 1 as q >= 0).
+// Cubic: f = (2 - q)^3 / 4 - max(1 - q, 0)^3 = 2 t^3 - s^3 with s = clamp(1 - q) -- one
+// expression on [0, 2] (for q < 1 it expands to 1 - 1.5 q^2 + 0.75 q^3), no branch;
+// computed as f / 2 = t^3 - s^3 / 2.  Wendland C2: t^4 (1 + 2q).
+template <int KID>
+constexpr float kShapeScale = KID == 0 ? 2.0f : 1.0f;
+
+// clamp(1 - q/2, 0, 1) and clamp(1 - q, 0, 1) on two lanes of fp32 at once (inline
+// constants, both halves).  The leading s_nop covers the transcendental-result hazard
+// (q comes straight from v_sqrt_f32).
+__device__ __forceinline__ f2 pk_one_minus_half_clamp(f2 q) {
+    f2 d;
+    asm("s_nop 0\n\tv_pk_fma_f32 %0, %1, -0.5, 1.0 op_sel_hi:[1,0,0] clamp" : "=v"(d) : "v"(q));
+    return d;
+}
+__device__ __forceinline__ f2 pk_one_minus_clamp(f2 q) {
+    f2 d;
+    asm("s_nop 0\n\tv_pk_fma_f32 %0, %1, -1.0, 1.0 op_sel_hi:[1,0,0] clamp" : "=v"(d) : "v"(q));
+    return d;
+}
+
+template <int KID>
+__device__ __forceinline__ f2 edge_shape2(f2 q) {
+    const f2 t = pk_one_minus_half_clamp(q);
+    if constexpr (KID == 0) {
+        const f2 s = pk_one_minus_clamp(q);
+        return __builtin_elementwise_fma((f2){-0.5f, -0.5f}, s * s * s, t * t * t);
+    } else {
+        const f2 t2 = t * t;
+        return (t2 * t2) * __builtin_elementwise_fma((f2){2.0f, 2.0f}, q, (f2){1.0f, 1.0f});
+    }
+}
+
 }  // namespace asp

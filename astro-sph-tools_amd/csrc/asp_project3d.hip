@@ -45,8 +45,11 @@ constexpr int kBrickVox = kBX * kBY * kBZ;   // 8192 -> 64 KiB of fp64 accumulat
 // k of adjacent columns in the same LDS bank, and lanes walk adjacent columns
 constexpr int kBZP = kBZ + ASP_CUBE_PAD;
 constexpr int kBrickLds = kBX * kBY * kBZP;
+__device__ __forceinline__ int lds_at(int li, int lj, int lk) {
+    return (li * kBY + lj) * kBZP + lk;
+}
 __device__ __forceinline__ int lds_vox(int v) {  // dense brick index -> padded LDS index
-    return (v >> kBZs) * kBZP + (v & (kBZ - 1));
+    return lds_at(v >> (kBYs + kBZs), (v >> kBZs) & (kBY - 1), v & (kBZ - 1));
 }
 constexpr int kMaxBricks = 16384;            // C1/C3 LDS: one int per brick (64 KiB)
 static_assert(kMaxBricks <= kScanThreads * kScanPer, "k_tilescan holds <= kScanPer bricks per thread");
@@ -199,20 +202,10 @@ struct Rec3 {
 };
 
 // Edge-continuous kernels (cubic, Wendland) take no per-voxel decision (as the 2-D gather,
-// DESIGN.md §3): f(q) written to give exactly 0 for q >= 2, evaluated in fp32 from fp32
-// corner offsets, so a voxel whose exact test differs contributes < 2^-60 W(0).  The
-// indicator kernel keeps the fp64 test (bit-exact voxel counts).
-template <int KID>
-__device__ __forceinline__ float edge_shape3(float q) {
-    const float t = fminf(fmaxf(fmaf(-0.5f, q, 1.0f), 0.0f), 1.0f);
-    if constexpr (KID == 0) {
-        const float s = fminf(fmaxf(1.0f - q, 0.0f), 1.0f);
-        return fmaf(-(s * s), s, 2.0f * (t * t) * t);  // (2-q)^3/4 - max(1-q, 0)^3
-    } else {
-        const float t2 = t * t;
-        return (t2 * t2) * fmaf(2.0f, q, 1.0f);
-    }
-}
+// DESIGN.md §3): edge_shape2 (asp_device.hpp) gives exactly 0 for q >= 2, evaluated in fp32
+// from fp32 plane offsets, two planes per packed instruction, so a voxel whose exact test
+// differs contributes < 2^-60 W(0).  The indicator kernel keeps the fp64 test (bit-exact
+// voxel counts).
 
 // One (i, j) column of a record's box.  The oracle's test is
 //   r2 = dx * dx + dy * dy + dz * dz  <  (2h)^2      (voxel_pass, left to right in fp64)
@@ -251,7 +244,7 @@ __device__ __forceinline__ void voxel3(const Rec3& R, double s, int li, int lj, 
     if (r2 < R.thr) {
         float q = __builtin_amdgcn_sqrtf((float)r2) * R.hinv;
         float w = kernel_shape<KID>(q);
-        atomicAdd(&acc[(li * kBY + lj) * kBZP + lk], (double)(R.s * w));
+        atomicAdd(&acc[lds_at(li, lj, lk)], (double)(R.s * w));
     }
 }
 
@@ -277,13 +270,20 @@ __device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, i
         if (!(fa <= fb)) return;
         const int a = (int)fa, b = (int)fb;
         const float zr = (float)(R.z - zt[0]);  // z relative to the brick's first plane
-        const float pz = (float)g.pz;
-        double* col = acc + (li * kBY + lj) * kBZP;
-        for (int lk = a; lk <= b; ++lk) {
-            const float dz = fmaf(-(float)lk, pz, zr);
-            const float q = __builtin_amdgcn_sqrtf(fmaf(dz, dz, sf)) * R.hinv;
-            const float w = edge_shape3<KID>(q);
-            if (w != 0.0f) atomicAdd(&col[lk], (double)(R.s * w));
+        const f2 zr2 = {zr, zr}, npz = {-(float)g.pz, -(float)g.pz}, sf2 = {sf, sf};
+        const f2 hi2 = {R.hinv, R.hinv};
+        const float sc = R.s * kShapeScale<KID>;  // edge_shape2 returns f / kShapeScale
+        const f2 sc2 = {sc, sc};
+        double* col = acc + lds_at(li, lj, 0);
+        f2 lk2 = {(float)a, (float)(a + 1)};
+        for (int lk = a; lk <= b; lk += 2) {  // planes lk, lk + 1 (the second may pass b)
+            const f2 dz = __builtin_elementwise_fma(lk2, npz, zr2);
+            const f2 r2 = __builtin_elementwise_fma(dz, dz, sf2);
+            const f2 q = f2{__builtin_amdgcn_sqrtf(r2.x), __builtin_amdgcn_sqrtf(r2.y)} * hi2;
+            const f2 w = edge_shape2<KID>(q) * sc2;
+            atomicAdd(&col[lk], (double)w.x);
+            if (lk < b) atomicAdd(&col[lk + 1], (double)w.y);
+            lk2 += (f2){2.0f, 2.0f};
         }
     }
 }
