@@ -193,6 +193,9 @@ __device__ __forceinline__ double src_v(const Src64& s, int p, float v) {
 // reads other columns (Grid::mixed) -- the range is clipped to the chunks whose cull
 // accepts the particle, computed exactly from the inputs (fp64 ones when given), so
 // every pixel of the box passes the cull.  False when nothing can pass.
+// CULL = false: the caller has checked that the grid needs no chunk clipping (square
+// image, cull reads the pixel columns), so that code is not compiled in.
+template <bool CULL = true>
 __device__ __forceinline__ bool footprint(const Grid& g, const Src64& s, int p, float u, float v,
                                           float h, Box& b) {
     float hd = fabsf(2.0f * h);
@@ -214,7 +217,7 @@ __device__ __forceinline__ bool footprint(const Grid& g, const Src64& s, int p, 
     b.x1 = (int)fx1;
     b.y0 = (int)fy0;
     b.y1 = (int)fy1;
-    if (g.nonsquare || g.mixed) {
+    if (CULL && (g.nonsquare || g.mixed)) {
         const Vals x = src_values(g, s, p);
         int c0, c1;
         chunk_range(x.CV, x.H, g.y_min, g.psy_cull, g.ny, g.cs, c0, c1);

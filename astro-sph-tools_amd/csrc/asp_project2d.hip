@@ -134,6 +134,7 @@ __device__ __forceinline__ bool maybe_large(const Grid& g, const Box& b) {
 // ----------------------------------------------------------------------------------
 // K1: count insertions per (block, tile)
 // ----------------------------------------------------------------------------------
+template <bool CULL>
 __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__ u,
                                                        const float* __restrict__ v,
                                                        const float* __restrict__ h,
@@ -156,7 +157,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
         for (int k = 0; k < kCountUnroll; ++k) {
             Box b;
             const int p = (int)(base + (long long)threadIdx.x * kCountUnroll + k);
-            if (!footprint(g, s, p, pu[k], pv[k], ph[k], b)) continue;
+            if (!footprint<CULL>(g, s, p, pu[k], pv[k], ph[k], b)) continue;
             int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
             int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
             if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > g.wide_tiles) {
@@ -164,8 +165,19 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
                 continue;
             }
             const bool mb = maybe_large(g, b);
-            for (int tx = tx0; tx <= tx1; ++tx)
-                for (int ty = ty0; ty <= ty1; ++ty) atomicAdd(&lh[column(g, b, mb, tx, ty)], 1);
+            if (tx1 - tx0 <= 1 && ty1 - ty0 <= 1) {
+                // at most 2 x 2 tiles (every pixel-scale particle): straight-line, so a wave
+                // pays for the second column / row only when one of its lanes needs it
+                atomicAdd(&lh[column(g, b, mb, tx0, ty0)], 1);
+                if (tx1 > tx0) atomicAdd(&lh[column(g, b, mb, tx1, ty0)], 1);
+                if (ty1 > ty0) {
+                    atomicAdd(&lh[column(g, b, mb, tx0, ty1)], 1);
+                    if (tx1 > tx0) atomicAdd(&lh[column(g, b, mb, tx1, ty1)], 1);
+                }
+            } else {
+                for (int tx = tx0; tx <= tx1; ++tx)
+                    for (int ty = ty0; ty <= ty1; ++ty) atomicAdd(&lh[column(g, b, mb, tx, ty)], 1);
+            }
         }
 #pragma unroll
         for (int k = 0; k < kCountUnroll; ++k) {
@@ -207,7 +219,7 @@ __device__ __forceinline__ void load_props(const float* __restrict__ a0,
 // here, where the store-bound scatter has VALU to spare.  Also the per-(block, tile) max
 // |c| (fp32 bits) of the records it inserted, the fixed-point bound of K3b.
 // ----------------------------------------------------------------------------------
-template <int KID, int NOUT, int ACC>
+template <int KID, int NOUT, int ACC, bool CULL>
 __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
     const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long nblk,
@@ -267,7 +279,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
         for (int k = 0; k < kUnroll; ++k) {
             const int p = (int)(base + (long long)threadIdx.x * kUnroll + k);
             Box b;
-            if (!footprint(g, s, p, pu[k], pv[k], ph[k], b)) continue;
+            if (!footprint<CULL>(g, s, p, pu[k], pv[k], ph[k], b)) continue;
             // the fixed-point bound is taken over the same fp32 coefficients the deposit
             // scales
             const float cf0 = (float)term_coef<KID>(pa0[k], ph[k]);
@@ -298,28 +310,38 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             first_lu[k] = (float)(U - corner_x(g, max(b.x0, tx0 * kTile)));
             first_lv[k] = (float)(V - corner_y(g, max(b.y0, ty0 * kTile)));
             const bool mb = maybe_large(g, b);
-            for (int tx = tx0; tx <= tx1; ++tx)
-                for (int ty = ty0; ty <= ty1; ++ty) {
-                    const int t = tx * g.nty + ty;
-                    const unsigned bp = tile_box(b, tx, ty);
-                    const int col = mb && box_large(bp, g.gather_min) ? t + g.ntiles : t;
-                    int slot = atomicAdd(&cur[col], 1);
-                    if constexpr (ACC == kAccFix) {
-                        atomicMax(&cm[t * NOUT], c0);
-                        if (NOUT == 2) atomicMax(&cm[t * NOUT + 1], c1);
-                    }
-                    if (tx == tx0 && ty == ty0) {
-                        first_slot[k] = slot;  // written by the paired store below
-                        first_box[k] = bp;
-                    } else {
-                        rec_store(&recs[2 * (long long)slot],
-                                  make_float4((float)(U - corner_x(g, max(b.x0, tx * kTile))),
-                                              (float)(V - corner_y(g, max(b.y0, ty * kTile))),
-                                              ph[k], cf0));
-                        rec_store(&recs[2 * (long long)slot + 1],
-                                  make_float4(cf1, __int_as_float(p), band, __uint_as_float(bp)));
-                    }
+            auto insert = [&](int tx, int ty, bool first) {
+                const int t = tx * g.nty + ty;
+                const unsigned bp = tile_box(b, tx, ty);
+                const int col = mb && box_large(bp, g.gather_min) ? t + g.ntiles : t;
+                int slot = atomicAdd(&cur[col], 1);
+                if constexpr (ACC == kAccFix) {
+                    atomicMax(&cm[t * NOUT], c0);
+                    if (NOUT == 2) atomicMax(&cm[t * NOUT + 1], c1);
                 }
+                if (first) {
+                    first_slot[k] = slot;  // written by the paired store below
+                    first_box[k] = bp;
+                } else {
+                    rec_store(&recs[2 * (long long)slot],
+                              make_float4((float)(U - corner_x(g, max(b.x0, tx * kTile))),
+                                          (float)(V - corner_y(g, max(b.y0, ty * kTile))),
+                                          ph[k], cf0));
+                    rec_store(&recs[2 * (long long)slot + 1],
+                              make_float4(cf1, __int_as_float(p), band, __uint_as_float(bp)));
+                }
+            };
+            if (tx1 - tx0 <= 1 && ty1 - ty0 <= 1) {  // at most 2 x 2 tiles: straight-line
+                insert(tx0, ty0, true);
+                if (tx1 > tx0) insert(tx1, ty0, false);
+                if (ty1 > ty0) {
+                    insert(tx0, ty1, false);
+                    if (tx1 > tx0) insert(tx1, ty1, false);
+                }
+            } else {
+                for (int tx = tx0; tx <= tx1; ++tx)
+                    for (int ty = ty0; ty <= ty1; ++ty) insert(tx, ty, tx == tx0 && ty == ty0);
+            }
         }
         // Paired store of every particle's first record: lanes 2j and 2j+1 write the two
         // 16-B halves of record j, so one store instruction covers 32 whole 32-B records
@@ -1538,7 +1560,9 @@ static int launch_scatter(const Grid& g, const Src64& s, Workspace& ws, const Pl
                           const float* a1, long long rec_cap, int wide_cap, hipStream_t st) {
     int* dc = (int*)ws.counters.p;
     StageMark m(ws, kSScatter, st);
-    hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC>), dim3((unsigned)pl.nblk_s), dim3(kScatterBlock),
+    hipLaunchKernelGGL((g.nonsquare || g.mixed ? k_scatter<KID, NOUT, ACC, true>
+                                               : k_scatter<KID, NOUT, ACC, false>),
+                       dim3((unsigned)pl.nblk_s), dim3(kScatterBlock),
                        scatter_lds(g, NOUT, ACC == kAccFix), st, u, v, h, a0, a1, pl.n, pl.nblk,
                        g, s, (const int*)ws.hist.p, (const long long*)ws.tile_start.p,
                        (float4*)ws.recs.p, (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc, pl.grp,
@@ -1680,7 +1704,8 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     ASP_HIP(hipMemsetAsync(dc, 0, (size_t)cNum * sizeof(int), st));
     {
         StageMark m(ws, kSCount, st);
-        hipLaunchKernelGGL(k_count, dim3((unsigned)pl.nblk), dim3(kCountBlock),
+        hipLaunchKernelGGL(g.nonsquare || g.mixed ? k_count<true> : k_count<false>,
+                           dim3((unsigned)pl.nblk), dim3(kCountBlock),
                            (size_t)2 * g.ntiles * sizeof(int), st, du, dv, dh, n, pl.nblk, g, s,
                            (int*)ws.hist.p, dc);
         ASP_LAUNCHED();
