@@ -154,31 +154,26 @@ __global__ __launch_bounds__(kKnnBlock) void k_gather(const double* __restrict__
     zs[i] = pos[3 * p + 2];
 }
 
-// The k smallest d2 seen, in registers (static indexing only): replace the maximum.
+// The k smallest d2 seen, in registers (static indexing only), kept sorted ascending in
+// the LAST k of K slots (the first K - k hold -inf and never move), so the k-th smallest is
+// v[K - 1].  Inserting d (< v[K - 1]) is a branch-free merge step:
+//   v'[q] = min(v[q], max(v[q - 1], d)),  v[-1] = -inf
+// = the q-th smallest of v and d (v[q] if d > v[q], else max(v[q - 1], d)): 2K min / max.
 template <int K>
 struct TopK {
     double v[K];
     double mx;  // the k-th smallest so far (+inf until k values are in)
-    int mi;
     __device__ __forceinline__ void init(int k) {
 #pragma unroll
-        for (int q = 0; q < K; ++q) v[q] = q < k ? INFINITY : -INFINITY;  // -inf: unused slot
+        for (int q = 0; q < K; ++q) v[q] = q < K - k ? -INFINITY : INFINITY;
         mx = INFINITY;
-        mi = 0;
     }
     __device__ __forceinline__ void insert(double d) {
         if (!(d < mx)) return;
 #pragma unroll
-        for (int q = 0; q < K; ++q)
-            if (q == mi) v[q] = d;
-        mx = v[0];
-        mi = 0;
-#pragma unroll
-        for (int q = 1; q < K; ++q)
-            if (v[q] > mx) {
-                mx = v[q];
-                mi = q;
-            }
+        for (int q = K - 1; q > 0; --q) v[q] = fmin(v[q], fmax(v[q - 1], d));
+        v[0] = fmin(v[0], d);
+        mx = v[K - 1];
     }
 };
 
