@@ -393,6 +393,30 @@ __device__ __forceinline__ void wave_scan(long long a, long long b, const double
     }
 }
 
+// One lane's scan of sorted particles [a, b): four particles' coordinates are loaded
+// before any of them is inserted, so the lane has 12 loads in flight instead of 3
+// (57 -> 54 ms at 10^7; 8 or 16 at a time: 69-70 ms, register pressure).
+constexpr int kScanUnroll = 4;
+template <int K>
+__device__ __forceinline__ void scan_range(long long a, long long b, const double* __restrict__ xs,
+                                           const double* __restrict__ ys,
+                                           const double* __restrict__ zs, double x, double y,
+                                           double z, TopK<K>& T) {
+    long long j = a;
+    for (; j + kScanUnroll <= b; j += kScanUnroll) {
+        double px[kScanUnroll], py[kScanUnroll], pz[kScanUnroll];
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u) {
+            px[u] = xs[j + u];
+            py[u] = ys[j + u];
+            pz[u] = zs[j + u];
+        }
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u) T.insert(dist2(x, y, z, px[u], py[u], pz[u]));
+    }
+    for (; j < b; ++j) T.insert(dist2(x, y, z, xs[j], ys[j], zs[j]));
+}
+
 template <int K>
 __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict__ xs,
                                                         const double* __restrict__ ys,
@@ -435,10 +459,6 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict
         for (long long cx = ca[0]; cx <= cb[0]; ++cx)
             for (long long cy = ca[1]; cy <= cb[1]; ++cy)
                 for (long long cz = ca[2]; cz <= cb[2]; ++cz) {
-                    unsigned long long p = morton3(cx, cy, cz);
-                    unsigned long long k0 = sh3 >= 63 ? 0ULL : p << sh3;
-                    unsigned long long k1 = sh3 >= 63 ? ~0ULL : (p + 1) << sh3;  // exclusive
-                    if (k0 >= klo && k1 <= khi) continue;  // inside the window already
                     const long long cc[3] = {cx, cy, cz};
                     double md = 0.0;
 #pragma unroll
@@ -448,13 +468,15 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict
                         double d = c3[a] < clo ? clo - c3[a] : (c3[a] > chi ? c3[a] - chi : 0.0);
                         md += d * d;
                     }
-                    if (md * (1.0 - 0x1p-40) > C.T.mx) continue;
+                    if (md * (1.0 - 0x1p-40) > C.T.mx) continue;  // beyond the k-th distance
+                    unsigned long long p = morton3(cx, cy, cz);
+                    unsigned long long k0 = sh3 >= 63 ? 0ULL : p << sh3;
+                    unsigned long long k1 = sh3 >= 63 ? ~0ULL : (p + 1) << sh3;  // exclusive
+                    if (k0 >= klo && k1 <= khi) continue;  // inside the window already
                     long long j0 = cell_lower(keys, n, CT, k0);
                     long long j1 = sh3 >= 63 || (k1 >> 63) ? n : cell_lower(keys, n, CT, k1);
-                    for (long long j = j0; j < min(j1, win0); ++j)
-                        C.T.insert(dist2(x, y, z, xs[j], ys[j], zs[j]));
-                    for (long long j = max(j0, win1); j < j1; ++j)
-                        C.T.insert(dist2(x, y, z, xs[j], ys[j], zs[j]));
+                    scan_range<K>(j0, min(j1, win0), xs, ys, zs, x, y, z, C.T);
+                    scan_range<K>(max(j0, win1), j1, xs, ys, zs, x, y, z, C.T);
                 }
     }
     if (act) h[idx[i]] = sqrt(C.T.mx);
