@@ -219,7 +219,11 @@ __device__ __forceinline__ void load_props(const float* __restrict__ a0,
 // here, where the store-bound scatter has VALU to spare.  Also the per-(block, tile) max
 // |c| (fp32 bits) of the records it inserted, the fixed-point bound of K3b.
 // ----------------------------------------------------------------------------------
-template <int KID, int NOUT, int ACC, bool CULL>
+// SRC: where the record frame's exact coordinates come from -- 0: the fp32 arrays (fp32
+// callers), 1: the resident fp64 arrays, loaded with the batch (s.u64 != null), 2: decided
+// per particle (src_u: the chunk-cull kernels).  0 and 1 keep loads out of the per-particle
+// branches (the fp32 kernels carry no fp64 load path at all).
+template <int KID, int NOUT, int ACC, bool CULL, int SRC>
 __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
     const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long nblk,
@@ -256,6 +260,22 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     // so waiting for them (vmcnt counts loads and stores in issue order) never waits on
     // the scattered stores.
     float pu[kUnroll], pv[kUnroll], ph[kUnroll], pa0[kUnroll], pa1[kUnroll];
+    double pU[kUnroll], pV[kUnroll];  // SRC 1: the exact coordinates
+    // SRC 1: the fp64 coordinates of U consecutive particles (index clamped to the array:
+    // unconditional loads; lanes past the end are never binned)
+    auto load_src = [&](long long b, double* dU, double* dV) {
+        if constexpr (SRC == 1) {
+#pragma unroll
+            for (int k = 0; k < kUnroll; ++k) {
+                const long long q = min(b + (long long)threadIdx.x * kUnroll + k, n - 1) * s.stride;
+                dU[k] = s.u64[q];
+                dV[k] = s.v64[q];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kUnroll; ++k) dU[k] = dV[k] = 0.0;
+        }
+    };
     int first_slot[kUnroll];
     // the prepared fields of every particle's first record (the paired store's payload)
     float first_c0[kUnroll], first_c1[kUnroll], first_band[kUnroll], first_lu[kUnroll],
@@ -270,11 +290,14 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     const bool al = aligned_vec<kUnroll>(u, v, h) && aligned_vec<kUnroll>(a0, NOUT == 2 ? a1 : a0, a0);
     load_batch<kUnroll>(u, v, h, p0, n, al, pu, pv, ph);
     load_props<NOUT>(a0, a1, p0, n, al, pa0, pa1);
+    load_src(p0, pU, pV);
     for (long long base = p0, next; base < n; base = next) {
         next = batch_base(++c);
         float nu[kUnroll], nv[kUnroll], nh[kUnroll], na0[kUnroll], na1[kUnroll];
         load_batch<kUnroll>(u, v, h, next, n, al, nu, nv, nh);
         load_props<NOUT>(a0, a1, next, n, al, na0, na1);
+        double nU[kUnroll], nV[kUnroll];
+        load_src(next, nU, nV);
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
             const int p = (int)(base + (long long)threadIdx.x * kUnroll + k);
@@ -303,7 +326,8 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             // coordinates relative to the record's box origin, from the exact inputs: the
             // deposit's pair arithmetic then carries 2^-24 of the pair distance, not of |u|
             // 
-            const double U = src_u(s, p, pu[k]), V = src_v(s, p, pv[k]);
+            const double U = SRC == 0 ? (double)pu[k] : SRC == 1 ? pU[k] : src_u(s, p, pu[k]);
+            const double V = SRC == 0 ? (double)pv[k] : SRC == 1 ? pV[k] : src_v(s, p, pv[k]);
             first_c0[k] = cf0;
             first_c1[k] = cf1;
             first_band[k] = band;
@@ -374,6 +398,8 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             ph[k] = nh[k];
             pa0[k] = na0[k];
             pa1[k] = na1[k];
+            pU[k] = nU[k];
+            pV[k] = nV[k];
         }
     }
     if constexpr (ACC == kAccFix) {
@@ -1096,15 +1122,20 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
     {
         int* dlist = defer_lds[threadIdx.x >> 6];
         int ndef = 0;  // wave-uniform
-        // Software pipeline, two batches deep: batches i+1 and i+2 load while batch i deposits.
-        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, q0 = r0, q1 = r0;
-        if ((int)threadIdx.x < it.count) load_rec(recs, it.start + threadIdx.x, r0, r1);
-        if ((int)threadIdx.x + kDepBlock < it.count)
-            load_rec(recs, it.start + threadIdx.x + kDepBlock, q0, q1);
+        // Software pipeline: batch i + 2 is issued before batch i deposits.  The loads are
+        // unconditional (index clamped to the item's last record; lanes past the end ignore
+        // theirs), so every iteration issues the same two loads and the compiler's wait
+        // before batch i leaves the batch just issued in flight (vmcnt(2); the register
+        // rotation makes it wait for batch i + 1 too).  Loads under a branch made it
+        // vmcnt(0), i.e. one full memory latency per batch: deposit 1.26 -> 1.22 ms (cfg 3).
+        const int last = it.count - 1;
+        float4 r0, r1, q0, q1;
+        load_rec(recs, it.start + min((int)threadIdx.x, last), r0, r1);
+        load_rec(recs, it.start + min((int)threadIdx.x + kDepBlock, last), q0, q1);
         for (int base = 0; base < it.count; base += kDepBlock) {
             int i = base + threadIdx.x;
-            float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0;
-            if (i + 2 * kDepBlock < it.count) load_rec(recs, it.start + i + 2 * kDepBlock, n0, n1);
+            float4 n0, n1;
+            load_rec(recs, it.start + min(i + 2 * kDepBlock, last), n0, n1);
             Prep P;
             P.b = Box{0, -1, 0, -1};
             const bool live = i < it.count;
@@ -1188,8 +1219,11 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(
     const int X0 = tx * kTile, Y0 = ty * kTile;
     const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
     const int lane = threadIdx.x;
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
-    if (lane < it.count) load_rec(recs, it.start + lane, r0, r1);
+    // unconditional loads (index clamped to the item's last record), so no wait or copy
+    // of the next batch is forced inside the walk
+    const int last = it.count - 1;
+    float4 r0, r1;
+    load_rec(recs, it.start + min(lane, last), r0, r1);
     const GOwn o = gather_owner(blockIdx.x % kGatherRegions);
     GAcc<NOUT, ACC> ga;
     ga.init(tot);
@@ -1205,7 +1239,7 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(
             mine = make_gentry(P, X0, Y0, kShapeScale<KID>);
         }
         // the next 64 records load while this batch is walked
-        if (base + 64 + lane < it.count) load_rec(recs, it.start + base + 64 + lane, r0, r1);
+        load_rec(recs, it.start + min(base + 64 + lane, last), r0, r1);
         gather_walk<KID, NOUT, ACC>(g, s, mine, X0, Y0, o, cc, ga);
     }
     gather_emit<NOUT, ACC>(g, ga, o, X0, Y0, it.slab, slabs, kk.x, kk.y, out0, out1, flags);
@@ -1560,8 +1594,9 @@ static int launch_scatter(const Grid& g, const Src64& s, Workspace& ws, const Pl
                           const float* a1, long long rec_cap, int wide_cap, hipStream_t st) {
     int* dc = (int*)ws.counters.p;
     StageMark m(ws, kSScatter, st);
-    hipLaunchKernelGGL((g.nonsquare || g.mixed ? k_scatter<KID, NOUT, ACC, true>
-                                               : k_scatter<KID, NOUT, ACC, false>),
+    hipLaunchKernelGGL((g.nonsquare || g.mixed ? k_scatter<KID, NOUT, ACC, true, 2>
+                        : s.u64               ? k_scatter<KID, NOUT, ACC, false, 1>
+                                              : k_scatter<KID, NOUT, ACC, false, 0>),
                        dim3((unsigned)pl.nblk_s), dim3(kScatterBlock),
                        scatter_lds(g, NOUT, ACC == kAccFix), st, u, v, h, a0, a1, pl.n, pl.nblk,
                        g, s, (const int*)ws.hist.p, (const long long*)ws.tile_start.p,
