@@ -95,17 +95,27 @@ def cpu_baseline(args, extent):
     nch = (args.grid // cs) ** 2
     order = np.random.default_rng(0).permutation(nch)
     done, spent, batch = 0, 0.0, max(cores, 8)
+    per_chunk = []  # seconds per chunk of each batch (the batches are random samples)
     while done < nch and spent < args.cpu_seconds:
         ids = order[done:done + batch]
         t = time.perf_counter()
         for A in maps:
             pyoracle.create_image(pos, h, A, (args.grid, args.grid), cs, 2, *([-extent, extent] * 2),
                                   kernel=args.kernel, nthreads=cores, chunk_ids=ids)
-        spent += time.perf_counter() - t
+        dt = time.perf_counter() - t
+        spent += dt
         done += ids.size
+        per_chunk.append(dt / ids.size)
     full_s = spent * nch / done
     mpix = args.grid * args.grid / full_s / 1e6
+    # standard error of the extrapolation: spread of the per-batch chunk times (random
+    # chunks: the Plummer core's chunks cost far more than the outskirts'), with the
+    # finite-population correction for sampling `done` of `nch` chunks
+    b = np.asarray(per_chunk)
+    rse = (float(b.std(ddof=1) / b.mean() / np.sqrt(b.size) * np.sqrt(1.0 - done / nch))
+           if b.size > 1 else None)
     return {"value": mpix, "unit": "Mpixels/s", "cores": cores, "kind": "port",
+            "rel_stderr": None if rse is None else round(rse, 4),
             "particles_per_s": args.n / full_s,
             "sample": f"{done} of {nch} random 64x64 chunks of the {args.n:.0e}-particle "
                       f"{args.grid}^2 map ({len(maps)} reference-style create_image call(s)), "
