@@ -258,6 +258,9 @@ __device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, i
         if (!column_range(g, R, li, lj, xt, yt, s, a, b)) return;
         for (int lk = a; lk <= b; ++lk) voxel3<KID>(R, s, li, lj, lk, zt, acc);
     } else {  // fp32 throughout: the column's plane range and dz, no decision
+        // the record's fp32 fields as scalars (reading them through the struct inside the
+        // loop nest made the compiler keep it in scratch memory)
+        const float hinv = R.hinv, rs = R.s, kc = R.kc;
         const float dx = (float)(R.x - xt[li]), dy = (float)(R.y - yt[lj]);
         const float sf = fmaf(dx, dx, dy * dy);
         const float thr = (float)R.thr;
@@ -265,14 +268,14 @@ __device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, i
         // the planes of q < 2 (W > 0): |dz| < sqrt(thr - s), widened well past the roundings
         float rz = __builtin_amdgcn_sqrtf(fmaxf(thr - sf, 0.0f) + thr * 0x1p-20f) * (float)g.ipz;
         rz = rz * (1.0f + 0x1p-18f) + 0x1p-10f;
-        const float fa = fmaxf(ceilf(R.kc - rz), (float)R.b.k0);
-        const float fb = fminf(floorf(R.kc + rz), (float)R.b.k1);
+        const float fa = fmaxf(ceilf(kc - rz), (float)R.b.k0);
+        const float fb = fminf(floorf(kc + rz), (float)R.b.k1);
         if (!(fa <= fb)) return;
         const int a = (int)fa, b = (int)fb;
         const float zr = (float)(R.z - zt[0]);  // z relative to the brick's first plane
         const f2 zr2 = {zr, zr}, npz = {-(float)g.pz, -(float)g.pz}, sf2 = {sf, sf};
-        const f2 hi2 = {R.hinv, R.hinv};
-        const float sc = R.s * kShapeScale<KID>;  // edge_shape2 returns f / kShapeScale
+        const f2 hi2 = {hinv, hinv};
+        const float sc = rs * kShapeScale<KID>;  // edge_shape2 returns f / kShapeScale
         const f2 sc2 = {sc, sc};
         double* col = acc + lds_at(li, lj, 0);
         f2 lk2 = {(float)a, (float)(a + 1)};
@@ -324,19 +327,16 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         zt[threadIdx.x - kBX - kBY] = g.z_min + (double)(K0 + (int)threadIdx.x - kBX - kBY) * g.pz;
     __syncthreads();
     int lane = threadIdx.x & 63;
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
-    if ((int)threadIdx.x < it.count) {
-        r0 = recs[2 * (it.start + threadIdx.x)];
-        r1 = recs[2 * (it.start + threadIdx.x) + 1];
-    }
+    // unconditional prefetch (index clamped to the item's last record): a load under a
+    // branch makes the compiler wait for the batch just issued (vmcnt(0))
+    const int last = it.count - 1;
+    float4 r0 = recs[2 * (it.start + min((int)threadIdx.x, last))];
+    float4 r1 = recs[2 * (it.start + min((int)threadIdx.x, last)) + 1];
     for (int base = 0; base < it.count; base += k3Block) {
         int i = base + threadIdx.x;
-        float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0;
-        if (i + k3Block < it.count) {
-            n0 = recs[2 * (it.start + i + k3Block)];
-            n1 = recs[2 * (it.start + i + k3Block) + 1];
-        }
-        Rec3 R;
+        const long long nx = it.start + min(i + k3Block, last);
+        float4 n0 = recs[2 * nx], n1 = recs[2 * nx + 1];
+        Rec3 R = {};  // fully initialised: a partly set struct went to scratch memory
         bool live = false;
         if (i < it.count && footprint3(g, r0.x, r0.y, r0.z, r0.w, R.b)) {
             R.b.i0 = max(R.b.i0, I0) - I0;
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         while (big) {
             int l = __builtin_ctzll(big);
             big &= big - 1;
-            Rec3 Q;
+            Rec3 Q = {};
             Q.x = __shfl(R.x, l);
             Q.y = __shfl(R.y, l);
             Q.z = __shfl(R.z, l);
