@@ -60,6 +60,12 @@ constexpr int k3Block = 512;                 // count / scatter / deposit workgr
 constexpr int kLaneCols = ASP_CUBE_LANE_COLS;  // boxes up to this many (i, j) columns:
                                                // lane-per-record, wider: a wave per record
 
+// Deposit rounds: records classified per round (LDS list of 2-byte indices) and the
+// classes (0: boxes of more than lane_cols columns, 1-4: lane-per-record boxes by volume)
+constexpr int kRound = 4096;
+constexpr int kQCls = 5;
+static_assert(kRound % k3Block == 0 && kRound <= 65536, "round of whole blocks, 16-bit index");
+
 struct Grid3 {
     double x_min, y_min, z_min;
     double px, py, pz;       // (max - min) / n per axis
@@ -300,6 +306,8 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
     double* xt = acc + kBrickLds;
     double* yt = xt + kBX;
     double* zt = yt + kBY;
+    __shared__ unsigned short qlist[kRound];  // the round's record indices, by class
+    __shared__ int qmeta[3 * kQCls];
     const Item it = items[blockIdx.x];
     int bi = it.tile / (g.nby * g.nbz);
     int rem = it.tile - bi * (g.nby * g.nbz);
@@ -326,69 +334,130 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
     else if (threadIdx.x < kBX + kBY + kBZ)
         zt[threadIdx.x - kBX - kBY] = g.z_min + (double)(K0 + (int)threadIdx.x - kBX - kBY) * g.pz;
     __syncthreads();
-    int lane = threadIdx.x & 63;
-    // unconditional prefetch (index clamped to the item's last record): a load under a
-    // branch makes the compiler wait for the batch just issued (vmcnt(0))
-    const int last = it.count - 1;
-    float4 r0 = recs[2 * (it.start + min((int)threadIdx.x, last))];
-    float4 r1 = recs[2 * (it.start + min((int)threadIdx.x, last)) + 1];
-    for (int base = 0; base < it.count; base += k3Block) {
-        int i = base + threadIdx.x;
-        const long long nx = it.start + min(i + k3Block, last);
-        float4 n0 = recs[2 * nx], n1 = recs[2 * nx + 1];
-        Rec3 R = {};  // fully initialised: a partly set struct went to scratch memory
-        bool live = false;
-        if (i < it.count && footprint3(g, r0.x, r0.y, r0.z, r0.w, R.b)) {
-            R.b.i0 = max(R.b.i0, I0) - I0;
-            R.b.i1 = min(R.b.i1, I0 + TW - 1) - I0;
-            R.b.j0 = max(R.b.j0, J0) - J0;
-            R.b.j1 = min(R.b.j1, J0 + TH - 1) - J0;
-            R.b.k0 = max(R.b.k0, K0) - K0;
-            R.b.k1 = min(R.b.k1, K0 + TD - 1) - K0;
-            live = R.b.i0 <= R.b.i1 && R.b.j0 <= R.b.j1 && R.b.k0 <= R.b.k1;
-            R.x = r0.x;
-            R.y = r0.y;
-            R.z = r0.z;
-            double t = 2.0 * (double)r0.w;
-            R.thr = t * t;
-            R.hinv = 1.0f / r0.w;
-            R.s = (float)term_coef<KID>(r1.x, r0.w);
-            R.kc = (float)((R.z - g.z_min) * g.ipz - (double)K0);
+    const int lane = threadIdx.x & 63;
+    // A record's state for the walk: its box clipped to the brick (brick-local), the fp64
+    // centre and threshold, 1/h, the term coefficient and the brick-local plane of z.
+    auto prep = [&](const float4& q0, const float4& q1, Rec3& R) -> bool {
+        if (!footprint3(g, q0.x, q0.y, q0.z, q0.w, R.b)) return false;
+        R.b.i0 = max(R.b.i0, I0) - I0;
+        R.b.i1 = min(R.b.i1, I0 + TW - 1) - I0;
+        R.b.j0 = max(R.b.j0, J0) - J0;
+        R.b.j1 = min(R.b.j1, J0 + TH - 1) - J0;
+        R.b.k0 = max(R.b.k0, K0) - K0;
+        R.b.k1 = min(R.b.k1, K0 + TD - 1) - K0;
+        R.x = q0.x;
+        R.y = q0.y;
+        R.z = q0.z;
+        double t = 2.0 * (double)q0.w;
+        R.thr = t * t;
+        R.hinv = 1.0f / q0.w;
+        R.s = (float)term_coef<KID>(q1.x, q0.w);
+        R.kc = (float)((R.z - g.z_min) * g.ipz - (double)K0);
+        return R.b.i0 <= R.b.i1 && R.b.j0 <= R.b.j1 && R.b.k0 <= R.b.k1;
+    };
+    // The item's records are taken in rounds of kRound.  Each round is first CLASSIFIED:
+    // boxes of more than lane_cols columns (a wave walks each) and four classes of the
+    // lane-per-record boxes by box volume; the record indices are counting-sorted by class
+    // into an LDS list.  Then every wave repeatedly claims a chunk of one class (the wave
+    // class first, then the lane classes from large to small boxes) until the round is
+    // exhausted: a wave's 64 lanes walk boxes of similar size, where records in arrival
+    // order put a wave at the pace of its largest box (modelled lane utilisation of the
+    // lane path 0.21 -> 0.5, tools/sim/cube_lanes.py).  No barrier inside a round.
+    int* qcnt = qmeta;             // records per class
+    int* qhead = qmeta + kQCls;    // claimed so far
+    int* qoff = qmeta + 2 * kQCls; // class start in qlist
+    for (int r0i = 0; r0i < it.count; r0i += kRound) {
+        const int nr = min(kRound, it.count - r0i);
+        if (threadIdx.x < kQCls) {
+            qcnt[threadIdx.x] = 0;
+            qhead[threadIdx.x] = 0;
         }
-        r0 = n0;
-        r1 = n1;
-        int bw = R.b.i1 - R.b.i0 + 1, bh = R.b.j1 - R.b.j0 + 1;
-        bool small = live && bw * bh <= g.lane_cols;
-        if (small) {
-            for (int li = R.b.i0; li <= R.b.i1; ++li)
-                for (int lj = R.b.j0; lj <= R.b.j1; ++lj)
-                    column3<KID>(g, R, li, lj, K0, xt, yt, zt, acc);
+        __syncthreads();
+        unsigned cr[kRound / k3Block];  // class << 16 | rank, per record of this thread
+#pragma unroll
+        for (int q = 0; q < kRound / k3Block; ++q) {
+            const int i = q * k3Block + (int)threadIdx.x;
+            const float4 q0 = recs[2 * (it.start + r0i + min(i, nr - 1))];
+            Box3 b;
+            int c = -1;
+            if (i < nr && footprint3(g, q0.x, q0.y, q0.z, q0.w, b)) {
+                const int bw = min(b.i1, I0 + TW - 1) - max(b.i0, I0) + 1;
+                const int bh = min(b.j1, J0 + TH - 1) - max(b.j0, J0) + 1;
+                const int bd = min(b.k1, K0 + TD - 1) - max(b.k0, K0) + 1;
+                if (bw > 0 && bh > 0 && bd > 0) {
+                    const int cols = bw * bh, vol = cols * bd;
+                    c = cols > g.lane_cols ? 0 : vol > 120 ? 1 : vol > 48 ? 2 : vol > 18 ? 3 : 4;
+                }
+            }
+            cr[q] = c < 0 ? 0xffffffffu : ((unsigned)c << 16) | (unsigned)atomicAdd(&qcnt[c], 1);
         }
-        unsigned long long big = __ballot(live && !small);
-        while (big) {
-            int l = __builtin_ctzll(big);
-            big &= big - 1;
-            Rec3 Q = {};
-            Q.x = __shfl(R.x, l);
-            Q.y = __shfl(R.y, l);
-            Q.z = __shfl(R.z, l);
-            Q.thr = __shfl(R.thr, l);
-            Q.hinv = bcast(R.hinv, l);
-            Q.s = bcast(R.s, l);
-            Q.kc = bcast(R.kc, l);
-            Q.b.i0 = bcast(R.b.i0, l);
-            Q.b.j0 = bcast(R.b.j0, l);
-            Q.b.k0 = bcast(R.b.k0, l);
-            Q.b.k1 = bcast(R.b.k1, l);
-            int qw = bcast(bw, l), qh = bcast(bh, l);
-            // lanes take the box's (i, j) columns
-            for (int c = lane; c < qw * qh; c += 64) {
-                int ci = c / qh, cj = c - ci * qh;
-                column3<KID>(g, Q, Q.b.i0 + ci, Q.b.j0 + cj, K0, xt, yt, zt, acc);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int o = 0;
+            for (int c = 0; c < kQCls; ++c) {
+                qoff[c] = o;
+                o += qcnt[c];
             }
         }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kRound / k3Block; ++q)
+            if (cr[q] != 0xffffffffu)
+                qlist[qoff[cr[q] >> 16] + (cr[q] & 0xffffu)] =
+                    (unsigned short)(q * k3Block + (int)threadIdx.x);
+        __syncthreads();
+        // claim chunks: the wave class 8 records at a time (each is walked by the whole
+        // wave), the lane classes 64 at a time (one per lane)
+        for (int c = 0; c < kQCls;) {
+            const int take = c == 0 ? 8 : 64;
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&qhead[c], take);
+            base = __shfl(base, 0);
+            const int cnt = qcnt[c];
+            if (base >= cnt) {
+                ++c;
+                continue;
+            }
+            const bool have = lane < take && base + lane < cnt;
+            const int i = have ? (int)qlist[qoff[c] + base + lane] : 0;
+            const long long ri = it.start + r0i + i;
+            const float4 q0 = recs[2 * ri], q1 = recs[2 * ri + 1];
+            Rec3 R = {};
+            const bool live = have && prep(q0, q1, R);
+            const int bw = R.b.i1 - R.b.i0 + 1, bh = R.b.j1 - R.b.j0 + 1;
+            if (c > 0) {  // lane classes: lane-per-record
+                if (live)
+                    for (int li = R.b.i0; li <= R.b.i1; ++li)
+                        for (int lj = R.b.j0; lj <= R.b.j1; ++lj)
+                            column3<KID>(g, R, li, lj, K0, xt, yt, zt, acc);
+                continue;
+            }
+            unsigned long long big = __ballot(live);
+            while (big) {
+                int l = __builtin_ctzll(big);
+                big &= big - 1;
+                Rec3 Q = {};
+                Q.x = __shfl(R.x, l);
+                Q.y = __shfl(R.y, l);
+                Q.z = __shfl(R.z, l);
+                Q.thr = __shfl(R.thr, l);
+                Q.hinv = bcast(R.hinv, l);
+                Q.s = bcast(R.s, l);
+                Q.kc = bcast(R.kc, l);
+                Q.b.i0 = bcast(R.b.i0, l);
+                Q.b.j0 = bcast(R.b.j0, l);
+                Q.b.k0 = bcast(R.b.k0, l);
+                Q.b.k1 = bcast(R.b.k1, l);
+                int qw = bcast(bw, l), qh = bcast(bh, l);
+                // lanes take the box's (i, j) columns
+                for (int cc = lane; cc < qw * qh; cc += 64) {
+                    int ci = cc / qh, cj = cc - ci * qh;
+                    column3<KID>(g, Q, Q.b.i0 + ci, Q.b.j0 + cj, K0, xt, yt, zt, acc);
+                }
+            }
+        }
+        __syncthreads();  // the round's list is reused by the next round
     }
-    __syncthreads();
     if (it.slab >= 0) {
         double* dst = slabs + (long long)it.slab * kBrickVox;
         for (int v = threadIdx.x; v < kBrickVox; v += k3Block) dst[v] = acc[lds_vox(v)];
