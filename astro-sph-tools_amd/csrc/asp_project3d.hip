@@ -55,7 +55,7 @@ constexpr int kMaxBricks = 16384;            // C1/C3 LDS: one int per brick (64
 static_assert(kMaxBricks <= kScanThreads * kScanPer, "k_tilescan holds <= kScanPer bricks per thread");
 constexpr int k3Block = 512;                 // count / scatter / deposit workgroup
 #ifndef ASP_CUBE_LANE_COLS
-#define ASP_CUBE_LANE_COLS 30
+#define ASP_CUBE_LANE_COLS 40
 #endif
 constexpr int kLaneCols = ASP_CUBE_LANE_COLS;  // boxes up to this many (i, j) columns:
                                                // lane-per-record, wider: a wave per record
@@ -64,6 +64,15 @@ constexpr int kLaneCols = ASP_CUBE_LANE_COLS;  // boxes up to this many (i, j) c
 // classes (0: boxes of more than lane_cols columns, 1-4: lane-per-record boxes by volume)
 constexpr int kRound = 4096;
 constexpr int kQCls = 5;
+#ifndef ASP_CUBE_WAVE_TAKE
+#define ASP_CUBE_WAVE_TAKE 32
+#endif
+constexpr int kWaveTake = ASP_CUBE_WAVE_TAKE;  // wave-class records claimed at a time
+#ifndef ASP_CUBE_VOL
+#define ASP_CUBE_VOL 80, 32, 12
+#endif
+constexpr int kVol[3] = {ASP_CUBE_VOL};  // lane classes: box volume above kV1, kV2, kV3, rest
+constexpr int kV1 = kVol[0], kV2 = kVol[1], kV3 = kVol[2];
 static_assert(kRound % k3Block == 0 && kRound <= 65536, "round of whole blocks, 16-bit index");
 
 struct Grid3 {
@@ -386,7 +395,7 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
                 const int bd = min(b.k1, K0 + TD - 1) - max(b.k0, K0) + 1;
                 if (bw > 0 && bh > 0 && bd > 0) {
                     const int cols = bw * bh, vol = cols * bd;
-                    c = cols > g.lane_cols ? 0 : vol > 120 ? 1 : vol > 48 ? 2 : vol > 18 ? 3 : 4;
+                    c = cols > g.lane_cols ? 0 : vol > kV1 ? 1 : vol > kV2 ? 2 : vol > kV3 ? 3 : 4;
                 }
             }
             cr[q] = c < 0 ? 0xffffffffu : ((unsigned)c << 16) | (unsigned)atomicAdd(&qcnt[c], 1);
@@ -406,55 +415,80 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
                 qlist[qoff[cr[q] >> 16] + (cr[q] & 0xffffu)] =
                     (unsigned short)(q * k3Block + (int)threadIdx.x);
         __syncthreads();
-        // claim chunks: the wave class 8 records at a time (each is walked by the whole
-        // wave), the lane classes 64 at a time (one per lane)
-        for (int c = 0; c < kQCls;) {
-            const int take = c == 0 ? 8 : 64;
-            int base = 0;
-            if (lane == 0) base = atomicAdd(&qhead[c], take);
-            base = __shfl(base, 0);
-            const int cnt = qcnt[c];
-            if (base >= cnt) {
-                ++c;
-                continue;
+        // claim chunks: the wave class kWaveTake records at a time (each is walked by the
+        // whole wave), the lane classes 64 at a time (one per lane).  The next chunk is
+        // claimed and its records loaded before the current one is walked.
+        int ccls = 0;  // claim cursor: the class being claimed from (wave-uniform)
+        auto claim = [&](int& cls, int& base) {
+            while (ccls < kQCls) {
+                int b0 = 0;
+                if (lane == 0) b0 = atomicAdd(&qhead[ccls], ccls == 0 ? kWaveTake : 64);
+                b0 = __shfl(b0, 0);
+                if (b0 < qcnt[ccls]) {
+                    cls = ccls;
+                    base = b0;
+                    return;
+                }
+                ++ccls;
             }
-            const bool have = lane < take && base + lane < cnt;
-            const int i = have ? (int)qlist[qoff[c] + base + lane] : 0;
-            const long long ri = it.start + r0i + i;
-            const float4 q0 = recs[2 * ri], q1 = recs[2 * ri + 1];
+            cls = kQCls;  // exhausted
+            base = 0;
+        };
+        auto fetch = [&](int cls, int base, int& i, float4& q0, float4& q1) {
+            const bool have = cls < kQCls && lane < (cls == 0 ? kWaveTake : 64) &&
+                              base + lane < qcnt[min(cls, kQCls - 1)];
+            i = have ? (int)qlist[qoff[cls] + base + lane] : -1;
+            const long long ri = it.start + r0i + max(i, 0);  // unconditional load
+            q0 = recs[2 * ri];
+            q1 = recs[2 * ri + 1];
+        };
+        int cls, base, i;
+        float4 q0, q1;
+        claim(cls, base);
+        fetch(cls, base, i, q0, q1);
+        while (cls < kQCls) {
+            int ncls, nbase, ni;
+            float4 n0, n1;
+            claim(ncls, nbase);
+            fetch(ncls, nbase, ni, n0, n1);
             Rec3 R = {};
-            const bool live = have && prep(q0, q1, R);
+            const bool live = i >= 0 && prep(q0, q1, R);
             const int bw = R.b.i1 - R.b.i0 + 1, bh = R.b.j1 - R.b.j0 + 1;
-            if (c > 0) {  // lane classes: lane-per-record
+            if (cls > 0) {  // lane classes: lane-per-record
                 if (live)
                     for (int li = R.b.i0; li <= R.b.i1; ++li)
                         for (int lj = R.b.j0; lj <= R.b.j1; ++lj)
                             column3<KID>(g, R, li, lj, K0, xt, yt, zt, acc);
-                continue;
-            }
-            unsigned long long big = __ballot(live);
-            while (big) {
-                int l = __builtin_ctzll(big);
-                big &= big - 1;
-                Rec3 Q = {};
-                Q.x = __shfl(R.x, l);
-                Q.y = __shfl(R.y, l);
-                Q.z = __shfl(R.z, l);
-                Q.thr = __shfl(R.thr, l);
-                Q.hinv = bcast(R.hinv, l);
-                Q.s = bcast(R.s, l);
-                Q.kc = bcast(R.kc, l);
-                Q.b.i0 = bcast(R.b.i0, l);
-                Q.b.j0 = bcast(R.b.j0, l);
-                Q.b.k0 = bcast(R.b.k0, l);
-                Q.b.k1 = bcast(R.b.k1, l);
-                int qw = bcast(bw, l), qh = bcast(bh, l);
-                // lanes take the box's (i, j) columns
-                for (int cc = lane; cc < qw * qh; cc += 64) {
-                    int ci = cc / qh, cj = cc - ci * qh;
-                    column3<KID>(g, Q, Q.b.i0 + ci, Q.b.j0 + cj, K0, xt, yt, zt, acc);
+            } else {
+                unsigned long long big = __ballot(live);
+                while (big) {
+                    int l = __builtin_ctzll(big);
+                    big &= big - 1;
+                    Rec3 Q = {};
+                    Q.x = __shfl(R.x, l);
+                    Q.y = __shfl(R.y, l);
+                    Q.z = __shfl(R.z, l);
+                    Q.thr = __shfl(R.thr, l);
+                    Q.hinv = bcast(R.hinv, l);
+                    Q.s = bcast(R.s, l);
+                    Q.kc = bcast(R.kc, l);
+                    Q.b.i0 = bcast(R.b.i0, l);
+                    Q.b.j0 = bcast(R.b.j0, l);
+                    Q.b.k0 = bcast(R.b.k0, l);
+                    Q.b.k1 = bcast(R.b.k1, l);
+                    int qw = bcast(bw, l), qh = bcast(bh, l);
+                    // lanes take the box's (i, j) columns
+                    for (int cc = lane; cc < qw * qh; cc += 64) {
+                        int ci = cc / qh, cj = cc - ci * qh;
+                        column3<KID>(g, Q, Q.b.i0 + ci, Q.b.j0 + cj, K0, xt, yt, zt, acc);
+                    }
                 }
             }
+            cls = ncls;
+            base = nbase;
+            i = ni;
+            q0 = n0;
+            q1 = n1;
         }
         __syncthreads();  // the round's list is reused by the next round
     }
