@@ -363,6 +363,34 @@ def test_bitwise_deterministic_and_permutation_invariant(gpu, oracle):
     assert_map_close(a, ref)
 
 
+def test_record_placement_trials(gpu, oracle, monkeypatch):
+    """Record-buffer placement trials (a freshly allocated record buffer: the call's
+    scatter is run into several candidate buffers and the fastest kept) leave
+    the deterministic maps bit-identical and the neighbour counts exact -- wide particles
+    and split tiles included (the wide-list cursor is reset before every trial)."""
+    from asp_amd import _lib
+    from asp_amd.tools.projections import create_image, create_weighted_image
+    from asp_amd.tools.projections import indicator_kernel
+    p = plummer_f32(300_000, seed=21, h_law="physical")
+    ext = (-4.0, 4.0, -4.0, 4.0)
+    kw = dict(deterministic=True)
+    monkeypatch.setenv("ASP_PLACEMENT_TRIALS", "0")
+    _lib.check(_lib.lib().asp_release(0))
+    a = create_weighted_image(p["pos"], p["h"], p["m"], p["T"], (512, 512), 64, 2, *ext, **kw)
+    monkeypatch.setenv("ASP_PLACEMENT_TRIALS", "4")
+    monkeypatch.setenv("ASP_PLACEMENT_MIN_MB", "0")
+    _lib.check(_lib.lib().asp_release(0))
+    b = create_weighted_image(p["pos"], p["h"], p["m"], p["T"], (512, 512), 64, 2, *ext, **kw)
+    assert np.array_equal(a, b)
+    _lib.check(_lib.lib().asp_release(0))
+    cnt = create_image(p["pos"], p["h"], np.ones_like(p["h"]), (512, 512), 64, 2, *ext,
+                       kernel_func=indicator_kernel)
+    want, _ = oracle.project_scatter(p["pos"][:, 0], p["pos"][:, 1], p["h"], np.ones_like(p["h"]),
+                                     None, (512, 512), 64, *ext, kernel="indicator")
+    assert np.array_equal(cnt, want)
+    _lib.check(_lib.lib().asp_release(0))
+
+
 def test_default_vs_deterministic_modes(gpu):
     """fp64 and int64 accumulation agree to fp32 rounding on the same inputs."""
     from asp_amd.tools.projections import create_image
