@@ -216,6 +216,63 @@ inline int ensure(Buf& b, size_t bytes) {
         if (rc_ != ASP_OK) return rc_; \
     } while (0)
 
+// Record-buffer placement trials.  The scatter's time depends on where the record buffer
+// lands in physical memory: the same call runs 1.88 or 2.38 ms at 10^8 depending on the
+// allocation (tools/alloc_probe.py: both modes within one process as the
+// buffer is re-allocated), while count, scans and deposit do not move.  When the buffer
+// is freshly allocated for a large call, the call's own scatter (`scatter()`: it must also reset any counter it advances) is run into up to
+// ASP_PLACEMENT_TRIALS candidate buffers (default 8; each allocated while the best so far
+// is still held, so it lands elsewhere), timed with events, and the fastest is kept -- it
+// then holds this call's records (the scatter's output does not depend on the buffer).
+// Used by the 2-D and the 3-D scatter (ws.recs).
+// A one-time cost on the first large call (~3 ms per trial at 10^8); 0 or 1 disables it.
+template <class F>
+inline int place_records(Workspace& ws, size_t bytes, hipStream_t st, F&& scatter, bool& placed) {
+    placed = false;
+    const char* e = getenv("ASP_PLACEMENT_TRIALS");
+    const int trials = e ? std::max(0, atoi(e)) : 8;
+    const char* mb = getenv("ASP_PLACEMENT_MIN_MB");  // tests lower it
+    if (trials < 2 || bytes < ((size_t)(mb ? atoi(mb) : 256) << 20)) return ASP_OK;
+    hipEvent_t t0, t1;
+    ASP_HIP(hipEventCreate(&t0));
+    ASP_HIP(hipEventCreate(&t1));
+    auto timed = [&](float& ms) -> int {
+        ASP_HIP(hipEventRecord(t0, st));
+        ASP_TRY(scatter());
+        ASP_HIP(hipEventRecord(t1, st));
+        ASP_HIP(hipEventSynchronize(t1));
+        ASP_HIP(hipEventElapsedTime(&ms, t0, t1));
+        return ASP_OK;
+    };
+    float best_ms = 0.0f;
+    int rc = timed(best_ms);  // the buffer ensure() just allocated
+    const float first_ms = best_ms;
+    // stop once a placement beats the first by 15 %: the modes are ~20 % apart
+    for (int t = 1; t < trials && rc == ASP_OK && best_ms > 0.85f * first_ms; ++t) {
+        Buf best = ws.recs, cand;  // cand is allocated while best is held: other pages
+        if (ensure(cand, bytes) != ASP_OK) {
+            (void)hipGetLastError();
+            break;  // no room for a candidate: keep the best
+        }
+        ws.recs = cand;
+        float ms = 0.0f;
+        rc = timed(ms);
+        if (rc == ASP_OK && ms < 0.97f * best_ms) {
+            (void)hipFree(best.p);  // the candidate wins and holds this call's records
+            best_ms = ms;
+        } else {
+            (void)hipFree(cand.p);  // the best still holds this call's records from its run
+            ws.recs = best;
+        }
+        if (getenv("ASP_PRINT_ALLOC"))
+            fprintf(stderr, "asp placement trial %d: %.3f ms (best %.3f)\n", t, ms, best_ms);
+    }
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    placed = rc == ASP_OK;
+    return rc;
+}
+
 #define ASP_LAUNCHED()                                                                    \
     do {                                                                                  \
         hipError_t e_ = hipGetLastError();                                                \

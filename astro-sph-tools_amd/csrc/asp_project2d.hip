@@ -1681,64 +1681,6 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
 }
 
 // Tunables read once per call (experiments; the defaults are the measured choices).
-// Record-buffer placement trials.  The scatter's time depends on where the record buffer
-// lands in physical memory: the same call runs 1.88 or 2.38 ms at 10^8 depending on the
-// allocation (tools/alloc_probe.py: both modes within one process as the
-// buffer is re-allocated), while count, scans and deposit do not move.  When the buffer
-// is freshly allocated for a large call, the call's own scatter is run into up to
-// ASP_PLACEMENT_TRIALS candidate buffers (default 8; each allocated while the best so far
-// is still held, so it lands elsewhere), timed with events, and the fastest is kept -- it
-// then holds this call's records (the scatter's output does not depend on the buffer).
-// A one-time cost on the first large call (~3 ms per trial at 10^8); 0 or 1 disables it.
-template <class F>
-static int place_records(Workspace& ws, long long n_recs, int* dc, hipStream_t st, F&& scatter,
-                         bool& placed) {
-    placed = false;
-    const char* e = getenv("ASP_PLACEMENT_TRIALS");
-    const int trials = e ? std::max(0, atoi(e)) : 8;
-    const size_t bytes = (size_t)n_recs * 2 * sizeof(float4);
-    const char* mb = getenv("ASP_PLACEMENT_MIN_MB");  // tests lower it
-    if (trials < 2 || bytes < ((size_t)(mb ? atoi(mb) : 256) << 20)) return ASP_OK;
-    hipEvent_t t0, t1;
-    ASP_HIP(hipEventCreate(&t0));
-    ASP_HIP(hipEventCreate(&t1));
-    auto timed = [&](float& ms) -> int {
-        // the wide-list cursor is the one counter the scatter advances
-        ASP_HIP(hipMemsetAsync(dc + cWideCursor, 0, sizeof(int), st));
-        ASP_HIP(hipEventRecord(t0, st));
-        ASP_TRY(scatter());
-        ASP_HIP(hipEventRecord(t1, st));
-        ASP_HIP(hipEventSynchronize(t1));
-        ASP_HIP(hipEventElapsedTime(&ms, t0, t1));
-        return ASP_OK;
-    };
-    float best_ms = 0.0f;
-    int rc = timed(best_ms);  // the buffer ensure() just allocated
-    for (int t = 1; t < trials && rc == ASP_OK; ++t) {
-        Buf best = ws.recs, cand;  // cand is allocated while best is held: other pages
-        if (ensure(cand, bytes) != ASP_OK) {
-            (void)hipGetLastError();
-            break;  // no room for a candidate: keep the best
-        }
-        ws.recs = cand;
-        float ms = 0.0f;
-        rc = timed(ms);
-        if (rc == ASP_OK && ms < 0.97f * best_ms) {
-            (void)hipFree(best.p);  // the candidate wins and holds this call's records
-            best_ms = ms;
-        } else {
-            (void)hipFree(cand.p);  // the best still holds this call's records from its run
-            ws.recs = best;
-        }
-        if (getenv("ASP_PRINT_ALLOC"))
-            fprintf(stderr, "asp placement trial %d: %.3f ms (best %.3f)\n", t, ms, best_ms);
-    }
-    (void)hipEventDestroy(t0);
-    (void)hipEventDestroy(t1);
-    placed = rc == ASP_OK;
-    return rc;
-}
-
 static void grid_tunables(Grid& g) {
     if (const char* e = getenv("ASP_WIDE_TILES")) g.wide_tiles = std::max(1, atoi(e));
     if (const char* e = getenv("ASP_GATHER_MIN")) g.gather_min = std::max(2, atoi(e));
@@ -1866,11 +1808,15 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     launch_scatter<K, N, A>(g, s, ws, pl, du, dv, dh, da0, da1, 0x7fffffffLL, 0x7fffffff, st)
 #define ASP_SC2(K, A) (nout == 1 ? ASP_SC(K, 1, A) : ASP_SC(K, 2, A))
 #define ASP_SC3(A) (kid == 0 ? ASP_SC2(0, A) : kid == 1 ? ASP_SC2(1, A) : ASP_SC2(2, A))
-        auto scatter = [&]() { return det ? ASP_SC3(kAccFix) : ASP_SC3(kAccF64); };
+        auto scatter = [&]() -> int {
+            // the wide-list cursor is the one counter the scatter advances
+            ASP_HIP(hipMemsetAsync(dc + cWideCursor, 0, sizeof(int), st));
+            return det ? ASP_SC3(kAccFix) : ASP_SC3(kAccF64);
+        };
 #undef ASP_SC3
 #undef ASP_SC2
 #undef ASP_SC
-        ASP_TRY(place_records(ws, pl.n_recs, dc, st, scatter, placed));
+        ASP_TRY(place_records(ws, (size_t)pl.n_recs * 2 * sizeof(float4), st, scatter, placed));
     }
     const bool pre_all = pre || placed;
     if (pr) {  // the plugin path: records, then the pairs of the requested tiles

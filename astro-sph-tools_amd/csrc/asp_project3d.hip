@@ -708,16 +708,22 @@ static int project3d(const float* x, const float* y, const float* z, const float
         n_merges = ws.h_counters[cMerges];
         if (n_recs >= 0x7fffffffLL)
             return fail(ASP_ERR_UNSUPPORTED, "more than 2^31 particle-brick records");
+        const void* recs_before = ws.recs.p;
         ASP_TRY(ensure(ws.recs, (size_t)n_recs * 2 * sizeof(float4)));
         ASP_TRY(ensure(ws.slabs, (size_t)n_slabs * kBrickVox * sizeof(double)));
-        {
+        auto scatter = [&]() -> int {
             StageMark m(ws, kS3Scatter, st);
             hipLaunchKernelGGL(k3_scatter, dim3((unsigned)nblk), dim3(k3Block), lds_bins, st, dx,
                                dy, dz, dh, da, n, per_block, g, (const int*)ws.hist.p,
                                (const long long*)ws.tile_start.p, (float4*)ws.recs.p);
             ASP_LAUNCHED();
             m.done();
-        }
+            return ASP_OK;
+        };
+        bool placed = false;  // a fresh record buffer: placement trials (asp_host.hpp)
+        if (ws.recs.p != recs_before)
+            ASP_TRY(place_records(ws, (size_t)n_recs * 2 * sizeof(float4), st, scatter, placed));
+        if (!placed) ASP_TRY(scatter());
         {
             StageMark m(ws, kS3Deposit, st);
             size_t lds = (size_t)kBrickLds * sizeof(double) + (kBX + kBY + kBZ) * sizeof(double);
