@@ -223,7 +223,9 @@ __device__ __forceinline__ void load_props(const float* __restrict__ a0,
 // callers), 1: the resident fp64 arrays, loaded with the batch (s.u64 != null), 2: decided
 // per particle (src_u: the chunk-cull kernels).  0 and 1 keep loads out of the per-particle
 // branches (the fp32 kernels carry no fp64 load path at all).
-template <int KID, int NOUT, int ACC, bool CULL, int SRC>
+// PROBE: 1 for the placement trials' launches (the same code under its own name, so that
+// profiles of the steady state show them apart).
+template <int KID, int NOUT, int ACC, bool CULL, int SRC, int PROBE>
 __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
     const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long nblk,
@@ -1591,12 +1593,16 @@ static inline size_t scatter_lds(const Grid& g, int nout, bool det) {
 template <int KID, int NOUT, int ACC>
 static int launch_scatter(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl,
                           const float* u, const float* v, const float* h, const float* a0,
-                          const float* a1, long long rec_cap, int wide_cap, hipStream_t st) {
+                          const float* a1, long long rec_cap, int wide_cap, hipStream_t st,
+                          bool probe = false) {
     int* dc = (int*)ws.counters.p;
     StageMark m(ws, kSScatter, st);
-    hipLaunchKernelGGL((g.nonsquare || g.mixed ? k_scatter<KID, NOUT, ACC, true, 2>
-                        : s.u64               ? k_scatter<KID, NOUT, ACC, false, 1>
-                                              : k_scatter<KID, NOUT, ACC, false, 0>),
+    hipLaunchKernelGGL((g.nonsquare || g.mixed ? (probe ? k_scatter<KID, NOUT, ACC, true, 2, 1>
+                                                        : k_scatter<KID, NOUT, ACC, true, 2, 0>)
+                        : s.u64 ? (probe ? k_scatter<KID, NOUT, ACC, false, 1, 1>
+                                         : k_scatter<KID, NOUT, ACC, false, 1, 0>)
+                                : (probe ? k_scatter<KID, NOUT, ACC, false, 0, 1>
+                                         : k_scatter<KID, NOUT, ACC, false, 0, 0>)),
                        dim3((unsigned)pl.nblk_s), dim3(kScatterBlock),
                        scatter_lds(g, NOUT, ACC == kAccFix), st, u, v, h, a0, a1, pl.n, pl.nblk,
                        g, s, (const int*)ws.hist.p, (const long long*)ws.tile_start.p,
@@ -1805,7 +1811,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     bool placed = false;  // the records are already scattered (by the placement trials)
     if (!pr && !pre && ws.recs.p != recs_before) {
 #define ASP_SC(K, N, A) \
-    launch_scatter<K, N, A>(g, s, ws, pl, du, dv, dh, da0, da1, 0x7fffffffLL, 0x7fffffff, st)
+    launch_scatter<K, N, A>(g, s, ws, pl, du, dv, dh, da0, da1, 0x7fffffffLL, 0x7fffffff, st, true)
 #define ASP_SC2(K, A) (nout == 1 ? ASP_SC(K, 1, A) : ASP_SC(K, 2, A))
 #define ASP_SC3(A) (kid == 0 ? ASP_SC2(0, A) : kid == 1 ? ASP_SC2(1, A) : ASP_SC2(2, A))
         auto scatter = [&]() -> int {

@@ -166,6 +166,7 @@ __global__ __launch_bounds__(k3Block) void k3_count(const float* __restrict__ x,
 // ----------------------------------------------------------------------------------
 // C3: scatter 32-byte records {x, y, z, h}, {a, 0, 0, 0} into the bricks' runs
 // ----------------------------------------------------------------------------------
+template <int PROBE>  // 1: the placement trials' launches (asp_project2d.hip k_scatter)
 __global__ __launch_bounds__(k3Block) void k3_scatter(
     const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
     const float* __restrict__ h, const float* __restrict__ a, long long n, long long per_block,
@@ -711,9 +712,10 @@ static int project3d(const float* x, const float* y, const float* z, const float
         const void* recs_before = ws.recs.p;
         ASP_TRY(ensure(ws.recs, (size_t)n_recs * 2 * sizeof(float4)));
         ASP_TRY(ensure(ws.slabs, (size_t)n_slabs * kBrickVox * sizeof(double)));
-        auto scatter = [&]() -> int {
+        auto scatter = [&](bool probe) -> int {
             StageMark m(ws, kS3Scatter, st);
-            hipLaunchKernelGGL(k3_scatter, dim3((unsigned)nblk), dim3(k3Block), lds_bins, st, dx,
+            hipLaunchKernelGGL(probe ? k3_scatter<1> : k3_scatter<0>, dim3((unsigned)nblk),
+                               dim3(k3Block), lds_bins, st, dx,
                                dy, dz, dh, da, n, per_block, g, (const int*)ws.hist.p,
                                (const long long*)ws.tile_start.p, (float4*)ws.recs.p);
             ASP_LAUNCHED();
@@ -722,8 +724,9 @@ static int project3d(const float* x, const float* y, const float* z, const float
         };
         bool placed = false;  // a fresh record buffer: placement trials (asp_host.hpp)
         if (ws.recs.p != recs_before)
-            ASP_TRY(place_records(ws, (size_t)n_recs * 2 * sizeof(float4), st, scatter, placed));
-        if (!placed) ASP_TRY(scatter());
+            ASP_TRY(place_records(ws, (size_t)n_recs * 2 * sizeof(float4), st,
+                                  [&]() { return scatter(true); }, placed));
+        if (!placed) ASP_TRY(scatter(false));
         {
             StageMark m(ws, kS3Deposit, st);
             size_t lds = (size_t)kBrickLds * sizeof(double) + (kBX + kBY + kBZ) * sizeof(double);

@@ -80,7 +80,9 @@ def main():
         stage = {}
         for k, row in out.items():
             s = STAGE_OF.get(k.split("<")[0])
-            if s and "hbm_bytes_per_launch" in row:
+            # the first (largest total time) kernel of a stage: the steady-state launches,
+            # not the placement trials' probe instantiation (k_scatter<..., 1>)
+            if s and s not in stage and "hbm_bytes_per_launch" in row:
                 stage[s] = {"hbm_bytes_per_launch": row["hbm_bytes_per_launch"],
                             "avg_us": row["avg_us"], "kernel": k}
         stage["source"] = a.source
