@@ -124,3 +124,24 @@ def test_cube_device_api_accumulate(gpu):
                    cube_size=size, extent=ext)
     assert torch.equal(c3 != 0, c1 != 0)
     assert torch.allclose(c3, c1, rtol=1e-5, atol=1e-6 * float(c1.abs().max()))
+
+
+def test_cube_record_placement_trials(gpu, oracle, monkeypatch):
+    """The placement trials of a fresh record buffer (the probe scatter run into several
+    candidate buffers, the fastest kept holding the call's records) leave the voxel counts
+    exact and the density within the bar."""
+    from asp_amd import _lib
+    from asp_amd.tools.projections import create_cube, indicator_kernel, wendland_c2_kernel
+    size = (48, 48, 64)
+    x, y, z, h, m = _plummer(30000, 9, size)
+    pos = np.stack([x, y, z], axis=1)
+    monkeypatch.setenv("ASP_PLACEMENT_TRIALS", "4")
+    monkeypatch.setenv("ASP_PLACEMENT_MIN_MB", "0")
+    _lib.check(_lib.lib().asp_release(0))
+    ones = np.ones_like(h)
+    g = create_cube(pos, h, ones, size, *EXT, kernel_func=indicator_kernel)
+    assert np.array_equal(g, oracle.project3d(x, y, z, h, ones, size, EXT, kernel="indicator"))
+    _lib.check(_lib.lib().asp_release(0))
+    d = create_cube(pos, h, m, size, *EXT, kernel_func=wendland_c2_kernel)
+    assert_map_close(d, oracle.project3d(x, y, z, h, m, size, EXT, kernel="wendland_c2"))
+    _lib.check(_lib.lib().asp_release(0))
