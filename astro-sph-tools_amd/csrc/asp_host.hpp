@@ -221,7 +221,7 @@ inline int ensure(Buf& b, size_t bytes) {
 // allocation (tools/alloc_probe.py: both modes within one process as the
 // buffer is re-allocated), while count, scans and deposit do not move.  When the buffer
 // is freshly allocated for a large call, the call's own scatter (`scatter()`: it must also reset any counter it advances) is run into up to
-// ASP_PLACEMENT_TRIALS candidate buffers (default 8; each allocated while the best so far
+// ASP_PLACEMENT_TRIALS candidate buffers (default 16; each allocated while the best so far
 // is still held, so it lands elsewhere), timed with events, and the fastest is kept -- it
 // then holds this call's records (the scatter's output does not depend on the buffer).
 // Used by the 2-D and the 3-D scatter (ws.recs).
@@ -230,7 +230,7 @@ template <class F>
 inline int place_records(Workspace& ws, size_t bytes, hipStream_t st, F&& scatter, bool& placed) {
     placed = false;
     const char* e = getenv("ASP_PLACEMENT_TRIALS");
-    const int trials = e ? std::max(0, atoi(e)) : 8;
+    const int trials = e ? std::max(0, atoi(e)) : 16;
     const char* mb = getenv("ASP_PLACEMENT_MIN_MB");  // tests lower it
     if (trials < 2 || bytes < ((size_t)(mb ? atoi(mb) : 256) << 20)) return ASP_OK;
     hipEvent_t t0, t1;
