@@ -57,9 +57,15 @@ constexpr int kCountUnroll = 8;    // particles per lane and batch in count
 // Scatter workgroup and how many consecutive count workgroups' particles it takes over:
 // fewer, wider scatter workgroups keep fewer partially written record lines open at a
 // time (each workgroup appends to its own segment of every tile).
-constexpr int kScatterBlock = 1024;
-constexpr int kScatterGroup = 4;
-constexpr int kUnroll = 2;         // particles per lane and batch in scatter
+#ifndef ASP_SCATTER_BLOCK
+#define ASP_SCATTER_BLOCK 1024
+#endif
+#ifndef ASP_SCATTER_GROUP_DEF
+#define ASP_SCATTER_GROUP_DEF 4
+#endif
+constexpr int kScatterBlock = ASP_SCATTER_BLOCK;
+constexpr int kScatterGroup = ASP_SCATTER_GROUP_DEF;
+constexpr int kUnroll = (int)(kCountBlock * kCountUnroll / kScatterBlock);  // particles per lane and batch in scatter
 // Particles per loop iteration of a count / scatter workgroup (a "batch").  Batches are
 // dealt to the count workgroups round-robin (batch j to workgroup j % nblk; the scatter
 // workgroup of count workgroups sb*grp.. takes their batches in order), so at any moment
