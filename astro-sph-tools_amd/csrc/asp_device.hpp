@@ -29,7 +29,10 @@
 namespace asp {
 
 constexpr int kBlock = 256;        // threads per workgroup for streaming kernels
-constexpr int kDepBlock = 512;     // deposit workgroup (8 waves; 2 per CU)
+#ifndef ASP_DEP_BLOCK
+#define ASP_DEP_BLOCK 512
+#endif
+constexpr int kDepBlock = ASP_DEP_BLOCK;  // deposit workgroup (8 waves; 2 per CU)
 constexpr int kTile = 64;          // GPU tile edge in pixels
 constexpr int kTileShift = 6;
 constexpr int kRow = kTile + 1;    // LDS tile row stride in words (one pad word per row)
