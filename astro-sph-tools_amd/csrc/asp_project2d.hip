@@ -53,12 +53,15 @@
 namespace asp {
 
 constexpr int kCountBlock = 256;   // count workgroup
-constexpr int kCountUnroll = 8;    // particles per lane and batch in count
+#ifndef ASP_COUNT_UNROLL
+#define ASP_COUNT_UNROLL 4
+#endif
+constexpr int kCountUnroll = ASP_COUNT_UNROLL;  // particles per lane and batch in count
 // Scatter workgroup and how many consecutive count workgroups' particles it takes over:
 // fewer, wider scatter workgroups keep fewer partially written record lines open at a
 // time (each workgroup appends to its own segment of every tile).
 #ifndef ASP_SCATTER_BLOCK
-#define ASP_SCATTER_BLOCK 1024
+#define ASP_SCATTER_BLOCK 512
 #endif
 #ifndef ASP_SCATTER_GROUP_DEF
 #define ASP_SCATTER_GROUP_DEF 4
