@@ -38,7 +38,7 @@ ASP_ERR_UNSUPPORTED = -4
 
 # Every symbol include/asp.h declares (tests check the library exports all of them).
 EXPORTS = ("asp_version", "asp_last_error", "asp_device_count", "asp_project2d",
-           "asp_project2d_f64", "asp_pairs_f64",
+           "asp_project2d_f64", "asp_pairs_begin", "asp_pairs_emit", "asp_pairs_end",
            "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges", "asp_pixel_neighbours", "asp_ratio",
            "asp_profile", "asp_profile_stages", "asp_profile_read", "asp_last_stats",
            "asp_release", "asp_stage_particles", "asp_periodic", "asp_wrapped_distance",
@@ -90,10 +90,11 @@ def lib():
                                     C.c_double, C.c_double, C.c_double, C.c_int32, C.c_int32,
                                     C.c_int32, C.c_int32, C.c_int32, _f, _f, C.c_int32,
                                     C.c_void_p]
-    L.asp_pairs_f64.argtypes = [_d, _d, C.c_int64, C.c_int32, C.c_double, C.c_double,
-                                C.c_double, C.c_double, C.c_int32, C.c_int32, C.c_int32,
-                                C.c_int32, C.c_int32, _i64, _i32, _d, C.c_int32, C.c_int32,
-                                C.c_void_p]
+    L.asp_pairs_begin.argtypes = [_d, _d, C.c_int64, C.c_int32, C.c_double, C.c_double,
+                                  C.c_double, C.c_double, C.c_int32, C.c_int32, C.c_int32,
+                                  C.c_int32, C.c_int32, C.c_void_p, _i64, C.POINTER(C.c_void_p)]
+    L.asp_pairs_emit.argtypes = [C.c_void_p, C.c_int32, C.c_int32, _i64, _i32, _d]
+    L.asp_pairs_end.argtypes = [C.c_void_p]
     L.asp_project3d.argtypes = ([_f] * 5 + [C.c_int64] + [C.c_double] * 6 + [C.c_int32] * 7
                                 + [_f, C.c_int32, C.c_void_p])
     L.asp_kernel_eval.argtypes = [C.c_int32, _d, _d, _d, C.c_int64, C.c_int32, C.c_int32,
@@ -125,7 +126,8 @@ def lib():
     L.asp_table_interp.argtypes = ([_d, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_void_p),
                                     _d, C.c_int32, C.c_int32, C.c_double, C.c_int64, C.c_double,
                                     C.c_int32, C.c_int32, _d, _d, _d, C.c_int32, C.c_void_p])
-    for name in ("asp_project2d", "asp_project2d_f64", "asp_pairs_f64", "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges",
+    for name in ("asp_project2d", "asp_project2d_f64", "asp_pairs_begin", "asp_pairs_emit",
+                 "asp_pairs_end", "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges",
                  "asp_pixel_neighbours", "asp_ratio", "asp_profile", "asp_profile_stages",
                  "asp_profile_read", "asp_last_stats", "asp_release", "asp_stage_particles",
                  "asp_periodic", "asp_wrapped_distance", "asp_knn_smoothing_lengths",
@@ -167,10 +169,11 @@ def ptr(a, t=_f):
 
 
 def last_stats(device: int = 0):
-    s = (C.c_int64 * 9)()
-    check(lib().asp_last_stats(device, s, 9))
+    s = (C.c_int64 * 13)()
+    check(lib().asp_last_stats(device, s, 13))
     return {"records": s[0], "items": s[1], "wide": s[2], "tile": s[3], "tiles": s[4],
-            "records_per_item": s[5], "merges": s[6], "slabs": s[7], "large": s[8]}
+            "records_per_item": s[5], "merges": s[6], "slabs": s[7], "large": s[8],
+            "evals": s[9], "evals_small": s[10], "evals_gather": s[11], "evals_wide": s[12]}
 
 
 def profile(device: int = 0, enable: bool = True, stages=None):

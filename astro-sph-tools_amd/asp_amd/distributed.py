@@ -96,11 +96,13 @@ class PendingMap:
     sum of map i overlaps the binning and deposit of map i + 1).
     """
 
-    def __init__(self, outs, works, ratio_here, gather=None):
+    def __init__(self, outs, works, ratio_here, gather=None, single=False, host_ok=False):
         self._outs = outs
         self._works = works
         self._ratio = ratio_here
         self._gather = gather  # (full-size destination, group): all-gather map 0's slabs
+        self._single = single  # reduce_scatter_gather: (out0, None) on every world size
+        self._host_ok = host_ok  # an injected projector may hand back host maps
         self._done = False
 
     def wait(self):
@@ -111,15 +113,22 @@ class PendingMap:
                 import torch
                 o0, o1 = self._outs
                 dev = o0.device
-                _lib.check(_lib.lib().asp_ratio(_lib.ptr(o0), _lib.ptr(o1), o0.numel(),
-                                                dev.index or 0,
-                                                torch.cuda.current_stream(dev).cuda_stream))
+                if not o0.is_cuda:  # host maps of an injected projector (the CPU tests)
+                    if not self._host_ok:
+                        raise RuntimeError("the projector's maps must be device tensors")
+                    o0.copy_(torch.where(o1 != 0, o0 / torch.where(o1 != 0, o1, 1), 0))
+                else:
+                    _lib.check(_lib.lib().asp_ratio(_lib.ptr(o0), _lib.ptr(o1), o0.numel(),
+                                                    dev.index or 0,
+                                                    torch.cuda.current_stream(dev).cuda_stream))
             if self._gather is not None:
                 import torch.distributed as dist
                 full, group = self._gather
                 dist.all_gather_into_tensor(full, self._outs[0].contiguous(), group=group)
                 self._outs = [full]
             self._done = True
+        if self._single:
+            return self._outs[0], None
         return self._outs[0], (self._outs[1] if len(self._outs) > 1 else None)
 
 
@@ -146,6 +155,9 @@ def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
         raise ValueError("ratio needs a1")
     if op not in ("reduce", "allreduce", "reduce_scatter", "reduce_scatter_gather"):
         raise ValueError(f"unknown op {op!r}")
+    if op == "reduce_scatter_gather" and a1 is not None and not ratio:
+        # one map is gathered: two component maps would need two all-gathers
+        raise ValueError("reduce_scatter_gather gathers ONE map: with a1 it needs ratio=True")
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     nx = int(image_size[0])
@@ -182,7 +194,8 @@ def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
         # all-gather of that one map: 2 maps reduce-scattered + 1 map gathered on the wire
         # instead of 2 maps reduced to one rank and the ratio there
         gather = (o0, group)
-    pending = PendingMap(outs, works, ratio_here, gather)
+    pending = PendingMap(outs, works, ratio_here, gather,
+                         single=op == "reduce_scatter_gather", host_ok=projector is not None)
     return pending if async_op else pending.wait()
 
 

@@ -71,7 +71,7 @@ def _run(positions, smoothing_lengths, props, projection_axis, image_size, chunk
 
 
 def _run_callable(positions, smoothing_lengths, props, projection_axis, image_size, chunk_size,
-                  extent, kernel_func, device):
+                  extent, kernel_func, device, mode, deterministic):
     nx, ny = int(image_size[0]), int(image_size[1])
     if nx <= 0 or ny <= 0 or chunk_size < 0:
         return [np.zeros((max(nx, 0), max(ny, 0))) for _ in props]
@@ -81,19 +81,24 @@ def _run_callable(positions, smoothing_lengths, props, projection_axis, image_si
     if pos.ndim != 2 or pos.shape[1] != 3:
         raise ValueError(f"positions must have shape (N, 3), got {pos.shape}")
     return project_callable(pos, smoothing_lengths, props, reference_axes(projection_axis),
-                            (nx, ny), chunk_size, extent, kernel_func, device=device)
+                            (nx, ny), chunk_size, extent, kernel_func, device=device, mode=mode,
+                            deterministic=deterministic)
 
 
 def create_image(positions: np.ndarray, smoothing_lengths: np.ndarray,
                  particle_properties: np.ndarray, image_size: tuple, chunk_size: int,
                  projection_axis, x_min: float, x_max: float, y_min: float, y_max: float,
                  kernel_func=quartic_spline_kernel, *, device: int = 0,
-                 dtype=np.float64, deterministic: bool = False) -> np.ndarray:
+                 dtype=np.float64, deterministic: bool = False,
+                 kernel_func_mode: str = "batch") -> np.ndarray:
     """Project particle property A onto an (Nx, Ny) pixel grid (reference semantics).
 
     ``device`` selects the GPU; ``dtype=np.float32`` skips the host upcast (opt-in);
     ``deterministic=True`` selects int64 fixed-point accumulation (bitwise reproducible,
-    input-order independent; see ASP_F_DETERMINISTIC in include/asp.h).
+    input-order independent; see ASP_F_DETERMINISTIC in include/asp.h) -- for an arbitrary
+    ``kernel_func``, per-pixel sums in particle order.  ``kernel_func_mode`` (arbitrary
+    callables only, _plugin.py): ``"batch"`` calls it on many pixels' pairs at once (it
+    must be element-wise), ``"per_pixel"`` once per pixel exactly as the reference does.
     """
     cs = _check_chunk_size(chunk_size)
     kid = kernel_id_of(kernel_func)
@@ -101,7 +106,7 @@ def create_image(positions: np.ndarray, smoothing_lengths: np.ndarray,
     if kid is None:  # an arbitrary Python kernel: the plugin path (_plugin.py)
         img, = _run_callable(positions, smoothing_lengths, [particle_properties],
                              projection_axis, image_size, cs, (x_min, x_max, y_min, y_max),
-                             kernel_func, device)
+                             kernel_func, device, kernel_func_mode, deterministic)
         return img.astype(dtype, copy=False)
     img, _ = _run(positions, smoothing_lengths, [particle_properties], projection_axis,
                   image_size, cs, (x_min, x_max, y_min, y_max), kid, False, deterministic,
@@ -113,7 +118,7 @@ def create_weighted_image(positions, smoothing_lengths, weights, values, image_s
                           chunk_size, projection_axis, x_min, x_max, y_min, y_max,
                           kernel_func=quartic_spline_kernel, *, device: int = 0,
                           return_components: bool = False, dtype=np.float64,
-                          deterministic: bool = False):
+                          deterministic: bool = False, kernel_func_mode: str = "batch"):
     """Weighted-average map, e.g. mass-weighted temperature.
 
     ``sum(w v W) / sum(w W)`` per pixel over the same neighbour sets as
@@ -132,7 +137,8 @@ def create_weighted_image(positions, smoothing_lengths, weights, values, image_s
     ext = (x_min, x_max, y_min, y_max)
     if kid is None:  # an arbitrary Python kernel: the plugin path (_plugin.py)
         s0, s1 = _run_callable(positions, smoothing_lengths, [w * vals, w], projection_axis,
-                               image_size, cs, ext, kernel_func, device)
+                               image_size, cs, ext, kernel_func, device, kernel_func_mode,
+                               deterministic)
         with np.errstate(divide="ignore", invalid="ignore"):
             ratio = np.where(s1 != 0, s0 / s1, 0.0)
         if return_components:

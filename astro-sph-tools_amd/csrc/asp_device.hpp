@@ -51,7 +51,10 @@ struct Grid {
     float ipsx, ipsy;     // fp32 reciprocal pitches (pixel pitches)
     float mg;         // bound on |corner coordinate|, absolute frame (error band)
     float mgl;        // the same for the records' box-origin / tile frames (128 pitches)
-    int nx, ny, cs;
+    int nx, ny, cs;   // nx: this call's WINDOW of image rows (== gnx without windows)
+    int gnx;          // the image's nx (pitches, S2 quirk, chunk cull)
+    int ox;           // first image row of the window (a multiple of kTile): images of
+                      // more than kMaxTiles GPU tiles are projected as row windows
     int ncx, ncy;     // reference chunks per axis
     int ntx, nty, ntiles;  // GPU tiles
     int nonsquare;    // nx != ny: the y chunk cull is not implied by the r2 test
@@ -110,19 +113,21 @@ struct Merge {      // a tile split over several items: sum their slabs
     int pad;
 };
 
-__device__ __forceinline__ double corner_x(const Grid& g, int xi) {
-    return g.x_min + (double)xi * g.psx;            // .pyx:13
+__device__ __forceinline__ double corner_x(const Grid& g, int xi) {  // xi: window row
+    return g.x_min + (double)(xi + g.ox) * g.psx;   // .pyx:13
 }
 __device__ __forceinline__ double corner_y(const Grid& g, int yi) {
     return g.y_min + (double)yi * g.psy_pix;        // .pyx:14
 }
 
-// _projector.py:38-48 for the chunk holding pixel (xi, yi).  fp64, reference order:
+// _projector.py:38-48 for the chunk holding pixel (xi, yi) (xi a window row).  fp64,
+// reference order:
 // (w_min + chunk_start * pitch) - 2*h  <=  w  <  (w_min + chunk_end * pitch) + 2*h.
 __device__ __forceinline__ bool cull_pass(const Grid& g, double u, double v, double h,
                                           int xi, int yi) {
+    xi += g.ox;
     int xi0 = (xi / g.cs) * g.cs, yi0 = (yi / g.cs) * g.cs;
-    int xe = min(xi0 + g.cs, g.nx), ye = min(yi0 + g.cs, g.ny);
+    int xe = min(xi0 + g.cs, g.gnx), ye = min(yi0 + g.cs, g.ny);
     double h2 = 2.0 * h;
     double xlo = g.x_min + (double)xi0 * g.psx, xhi = g.x_min + (double)xe * g.psx;
     double ylo = g.y_min + (double)yi0 * g.psy_cull, yhi = g.y_min + (double)ye * g.psy_cull;
@@ -211,13 +216,14 @@ __device__ __forceinline__ bool footprint(const Grid& g, const Src64& s, int p, 
     float cy = (v - g.yminf) * g.ipsy, ry = hd * g.ipsy;
     float dx = (fabsf(u) + fabsf(g.xminf) + hd) * g.ipsx * 0x1p-20f + 0x1p-12f;
     float dy = (fabsf(v) + fabsf(g.yminf) + hd) * g.ipsy * 0x1p-20f + 0x1p-12f;
-    float fx0 = fmaxf(ceilf(cx - rx - dx), 0.0f);
-    float fx1 = fminf(floorf(cx + rx + dx), (float)(g.nx - 1));
+    // image rows clipped to the window [ox, ox + nx), then window-relative
+    float fx0 = fmaxf(ceilf(cx - rx - dx), (float)g.ox);
+    float fx1 = fminf(floorf(cx + rx + dx), (float)(g.ox + g.nx - 1));
     float fy0 = fmaxf(ceilf(cy - ry - dy), 0.0f);
     float fy1 = fminf(floorf(cy + ry + dy), (float)(g.ny - 1));
     if (!(fx0 <= fx1) || !(fy0 <= fy1)) return false;
-    b.x0 = (int)fx0;
-    b.x1 = (int)fx1;
+    b.x0 = (int)fx0 - g.ox;
+    b.x1 = (int)fx1 - g.ox;
     b.y0 = (int)fy0;
     b.y1 = (int)fy1;
     if (CULL && (g.nonsquare || g.mixed)) {
@@ -228,9 +234,9 @@ __device__ __forceinline__ bool footprint(const Grid& g, const Src64& s, int p, 
         b.y1 = min(b.y1, min((c1 + 1) * g.cs, g.ny) - 1);
         if (b.y0 > b.y1) return false;
         if (g.mixed) {
-            chunk_range(x.CU, x.H, g.x_min, g.psx, g.nx, g.cs, c0, c1);
-            b.x0 = max(b.x0, c0 * g.cs);
-            b.x1 = min(b.x1, min((c1 + 1) * g.cs, g.nx) - 1);
+            chunk_range(x.CU, x.H, g.x_min, g.psx, g.gnx, g.cs, c0, c1);
+            b.x0 = max(b.x0, c0 * g.cs - g.ox);
+            b.x1 = min(b.x1, min((c1 + 1) * g.cs, g.gnx) - 1 - g.ox);
             if (b.x0 > b.x1) return false;
         }
     }

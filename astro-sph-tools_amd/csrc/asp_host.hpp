@@ -35,6 +35,7 @@ struct Buf {
 };
 
 constexpr int kStages = 17;
+constexpr int kNStats = 13;  // asp_last_stats
 constexpr int kMarks = 8;  // launches of one stage timed per call
 enum Stage {
     kSMemset = 0, kSCount, kSColscan, kSTilescan, kSScatter, kSScale, kSDeposit, kSMerge,
@@ -67,7 +68,7 @@ struct Workspace {
     int* h_counters = nullptr;  // pinned
     int morton_ntx = -1, morton_nty = -1;
     int morton3_key[3] = {-1, -1, -1};
-    long long stats[9] = {0};
+    long long stats[kNStats] = {0};
     // Side stream of the chunked host staging (asp_stage_particles).
     hipStream_t side = nullptr;
     hipEvent_t chunk_ev[kMarks] = {};
@@ -129,6 +130,22 @@ inline int ws_end(Workspace& ws, hipStream_t st) {
     ASP_HIP(hipEventRecord(ws.last_ev, st));
     return ASP_OK;
 }
+// Created right after ws_begin: every exit of the call -- error returns included, which
+// may already have enqueued work on st -- records the end event, so the next call on
+// another stream waits for that work.  finish() is the success path's (checked) record.
+struct WsEnd {
+    Workspace& ws;
+    hipStream_t st;
+    bool done = false;
+    WsEnd(Workspace& w, hipStream_t s) : ws(w), st(s) {}
+    int finish() {
+        done = true;
+        return ws_end(ws, st);
+    }
+    ~WsEnd() {
+        if (!done) (void)ws_end(ws, st);
+    }
+};
 
 // asp_stage.hip: reader arrays on the device -> the projector's fp32 working copies
 // (axis selection of _projector.py:38-46, round to nearest), enqueued on st.

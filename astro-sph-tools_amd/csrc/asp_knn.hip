@@ -496,6 +496,7 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     Workspace& ws = g_ws[device];
     std::lock_guard<std::mutex> lock(ws.mu);
     ASP_TRY(ws_begin(ws, st));
+    WsEnd ws_end_(ws, st);
     const bool dev = flags & ASP_F_DEVICE_PTRS;
     const double* dpos = pos;
     double* dh = h;
@@ -578,7 +579,7 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
         ASP_HIP(hipMemcpyAsync(h, dh, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st));
         ASP_HIP(hipStreamSynchronize(st));
     }
-    return ws_end(ws, st);
+    return ws_end_.finish();
 }
 
 }  // namespace asp

@@ -1350,6 +1350,91 @@ __global__ __launch_bounds__(kGatherThreads) void k_wide(
     gather_emit<NOUT, ACC>(g, ga, o, X0, Y0, -1, nullptr, k0, k1, out0, out1, kFlagAccumulate);
 }
 
+// ----------------------------------------------------------------------------------
+// Diagnostic (bench.py's compute roofline, ASP_COUNT_EVALS=1): the (pixel, particle)
+// lane-slots the deposit kernels spend, from the binned records, without evaluating any:
+//   K4 small / mid stream: 9 per packed <= 3 x 3 box (every slot of the packed body), the
+//      box area for 4 x 4 boxes, 64 per pass of a wave sweep;
+//   K4g / K6 gather form: 128 per met 8 x 16 half block row (edge kernels) or 64 per met
+//      8 x 8 block (decided path) -- as gather_entry_edge / gather_entry spend them.
+// evals[0] += small / mid, evals[1] += gather (records), evals[2] += wide particles.
+// ----------------------------------------------------------------------------------
+__device__ __forceinline__ long long gather_slots(const Grid& g, int kid, unsigned box) {
+    const int x0 = box & 255u, x1 = (box >> 8) & 255u, y0 = (box >> 16) & 255u, y1 = box >> 24;
+    const bool edge = kid != kKernelIndicator && !g.nonsquare && !g.mixed;
+    long long c = 0;
+    for (int w = 0; w < kGatherRegions; ++w) {
+        const int r0 = (w >> 1) * 16, c0 = (w & 1) * 32;
+        for (int r = 0; r < 2; ++r) {
+            const int br = r0 + 8 * r;
+            if (!(x0 <= br + 7 && x1 >= br)) continue;
+            if (edge) {
+                for (int k = 0; k < 2; ++k) {
+                    const int bc = c0 + 16 * k;
+                    if (y0 <= bc + 15 && y1 >= bc) c += 128;
+                }
+            } else {
+                for (int k = 0; k < 4; ++k) {
+                    const int bc = c0 + 8 * k;
+                    if (y0 <= bc + 7 && y1 >= bc) c += 64;
+                }
+            }
+        }
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(kBlock) void k_evals(Grid g, int kid, Src64 s,
+                                                  const float4* __restrict__ recs,
+                                                  const Item* __restrict__ items, int n_items,
+                                                  const float* __restrict__ u,
+                                                  const float* __restrict__ v,
+                                                  const float* __restrict__ h,
+                                                  const int* __restrict__ wide_list, int n_wide,
+                                                  unsigned long long* __restrict__ evals) {
+    long long c0 = 0, c1 = 0, c2 = 0;
+    if ((int)blockIdx.x < n_items) {
+        const Item it = items[blockIdx.x];
+        const int tx = it.tile / g.nty, ty = it.tile - (it.tile / g.nty) * g.nty;
+        const int X0 = tx * kTile, Y0 = ty * kTile;
+        for (int i = threadIdx.x; i < it.count; i += kBlock) {
+            float4 r0, r1;
+            load_rec(recs, it.start + i, r0, r1);
+            Prep P;
+            rec_prep<kAccF64>(r0, r1, X0, Y0, make_int2(0, 0), P);
+            const int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
+            if (it.mode == 1) {
+                c1 += gather_slots(g, kid, __float_as_uint(r1.w));
+            } else if (bw <= 3 && bh <= 3) {
+                c0 += 9;
+            } else if (is_small(bw, bh)) {
+                c0 += bw * bh;
+            } else {
+                const int passes = bh <= 64 ? (bw + 64 / bh - 1) / (64 / bh) : bw * ((bh + 63) / 64);
+                c0 += 64LL * passes;
+            }
+        }
+    } else {  // one workgroup per tile: the wide particles the tile's K6 gathers
+        const int t = blockIdx.x - n_items;
+        const int tx = t / g.nty, ty = t - (t / g.nty) * g.nty;
+        const int X0 = tx * kTile, Y0 = ty * kTile;
+        const int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
+        for (int i = threadIdx.x; i < n_wide; i += kBlock) {
+            const int p = wide_list[i];
+            Prep P;
+            if (prep_record<2>(g, s, p, u[p], v[p], h[p], 0.0f, 0.0f, 0, 0, P) &&
+                clip(P.b, X0, Y0, TW, TH)) {
+                const unsigned box = (unsigned)(P.b.x0 - X0) | ((unsigned)(P.b.x1 - X0) << 8) |
+                                     ((unsigned)(P.b.y0 - Y0) << 16) | ((unsigned)(P.b.y1 - Y0) << 24);
+                c2 += gather_slots(g, kid, box);
+            }
+        }
+    }
+    if (c0) atomicAdd(&evals[0], (unsigned long long)c0);
+    if (c1) atomicAdd(&evals[1], (unsigned long long)c1);
+    if (c2) atomicAdd(&evals[2], (unsigned long long)c2);
+}
+
 // K7: out0 <- out0 / out1 (0 where out1 == 0).
 __global__ __launch_bounds__(kBlock) void k_ratio(float* __restrict__ out0,
                                                   const float* __restrict__ out1, long long m) {
@@ -1362,41 +1447,88 @@ __global__ __launch_bounds__(kBlock) void k_ratio(float* __restrict__ out0,
 }
 
 // ----------------------------------------------------------------------------------
-// K8 pairs (the kernel_func plugin: _projector.py:26, 86; _pixel_calculations.pyx:30-33):
-// for the GPU tiles [t0, t0 + gridDim.x), every included (pixel, particle) pair -- the
-// deposit's exact decision -- written as the particle index and the reference's fp64
-// r^2 = dx^2 + dy^2 (dx = U - X, .pyx:13-14, :20-30) at the pixel's slot range
-// offsets[pixel] .. (pixels tile by tile, lx * 64 + ly inside a tile; order within a
-// pixel unspecified).  The caller evaluates its Python kernel on sqrt(r^2) and h.
+// K8 pairs (the kernel_func plugin: _projector.py:26, 86; _pixel_calculations.pyx:30-33),
+// one workgroup per GPU tile of a binned window, on the records the session keeps
+// resident.  Every included (pixel, particle) pair -- the deposit's exact decision -- is
+//   MODE 0: counted per pixel (int32 pixcnt[tile][lx * 64 + ly], int64 tile totals);
+//   MODE 1: written as the particle index and the reference's fp64 r^2 = dx^2 + dy^2
+//           (dx = U - X, .pyx:13-14, :20-30) at its pixel's slot range, the pixel offsets
+//           being the tile base + an exclusive scan of that tile's pixcnt (also written
+//           out for the host).  Order within a pixel unspecified.
+// The counts come from the same records and decisions as the pairs, so a pixel's slots
+// always suffice; a pair that would not fit (a broken invariant) is dropped and counted in
+// *overflow, which the host turns into an error.
 // ----------------------------------------------------------------------------------
 constexpr int kPairsBlock = 256;
+template <int MODE>
 __global__ __launch_bounds__(kPairsBlock) void k_pairs(
     Grid g, Src64 s, const float4* __restrict__ recs, const long long* __restrict__ tile_start,
     const int* __restrict__ tile_total, const int* __restrict__ wide_list, int n_wide,
     const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
-    int t0, const long long* __restrict__ offsets, int* __restrict__ particle,
-    double* __restrict__ r2out) {
+    int t0, int* __restrict__ pixcnt, long long* __restrict__ tile_pairs,
+    const long long* __restrict__ tile_base, long long* __restrict__ offsets,
+    int* __restrict__ particle, double* __restrict__ r2out, int* __restrict__ overflow) {
     __shared__ int cur[kTilePix];
     __shared__ float xt[kTile], yt[kTile];
+    __shared__ long long wsum[kPairsBlock / 64];
+    __shared__ long long soff[MODE == 1 ? kTilePix + 1 : 1];  // MODE 1: the pixel offsets
     const int t = t0 + blockIdx.x;
     const int tx = t / g.nty, ty = t - (t / g.nty) * g.nty;
     const int X0 = tx * kTile, Y0 = ty * kTile;
     const int TW = min(kTile, g.nx - X0), TH = min(kTile, g.ny - Y0);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int kPer = kTilePix / kPairsBlock;  // 16 consecutive pixels per thread
+    long long* off = offsets + (long long)blockIdx.x * kTilePix;  // MODE 1
+    if constexpr (MODE == 1) {
+        // exclusive scan of the tile's pixel counts + the tile's base: the pixel offsets
+        const int* c = pixcnt + (long long)t * kTilePix + threadIdx.x * kPer;
+        long long loc[kPer], run = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            loc[k] = run;
+            run += c[k];
+        }
+        long long x = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            long long y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wv] = x;
+        __syncthreads();
+        long long base = tile_base[blockIdx.x] + x - run;
+        for (int k = 0; k < wv; ++k) base += wsum[k];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            soff[threadIdx.x * kPer + k] = base + loc[k];
+            off[threadIdx.x * kPer + k] = base + loc[k];
+        }
+        if (threadIdx.x == kPairsBlock - 1) {  // = the next tile's base
+            soff[kTilePix] = base + run;
+            off[kTilePix] = base + run;
+        }
+    }
     for (int k = threadIdx.x; k < kTilePix; k += kPairsBlock) cur[k] = 0;
     corner_tables(g, X0, Y0, xt, yt);
     __syncthreads();
-    const long long* off = offsets + (long long)blockIdx.x * kTilePix;
     auto emit_box = [&](const Prep& P) {  // P in its box-origin frame
         for (int xi = P.b.x0; xi <= P.b.x1; ++xi)
             for (int yi = P.b.y0; yi <= P.b.y1; ++yi) {
                 float r2f;
                 if (!decide(g, s, P, xi, yi, xt[xi - P.b.x0], yt[yi - P.b.y0], r2f)) continue;
                 const int lp = (xi - X0) * kTile + (yi - Y0);
-                const long long slot = off[lp] + atomicAdd(&cur[lp], 1);
-                const Vals x = src_values(g, s, P.p);
-                const double dx = x.U - corner_x(g, xi), dy = x.V - corner_y(g, yi);
-                particle[slot] = P.p;
-                r2out[slot] = dx * dx + dy * dy;
+                const int k = atomicAdd(&cur[lp], 1);
+                if constexpr (MODE == 1) {
+                    const long long slot = soff[lp] + k;
+                    if (slot >= soff[lp + 1]) {
+                        atomicAdd(overflow, 1);
+                        continue;
+                    }
+                    const Vals x = src_values(g, s, P.p);
+                    const double dx = x.U - corner_x(g, xi), dy = x.V - corner_y(g, yi);
+                    particle[slot] = P.p;
+                    r2out[slot] = dx * dx + dy * dy;
+                }
             }
     };
     for (int stream = 0; stream < 2; ++stream) {
@@ -1419,6 +1551,23 @@ __global__ __launch_bounds__(kPairsBlock) void k_pairs(
         P.u = (float)(src_u(s, p, P.u) - corner_x(g, P.b.x0));  // box-origin frame
         P.v = (float)(src_v(s, p, P.v) - corner_y(g, P.b.y0));
         emit_box(P);
+    }
+    if constexpr (MODE == 0) {
+        __syncthreads();
+        long long tot = 0;
+        for (int k = threadIdx.x; k < kTilePix; k += kPairsBlock) {
+            pixcnt[(long long)t * kTilePix + k] = cur[k];
+            tot += cur[k];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+        if (lane == 0) wsum[wv] = tot;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            long long a = 0;
+            for (int k = 0; k < kPairsBlock / 64; ++k) a += wsum[k];
+            tile_pairs[t] = a;
+        }
     }
 }
 
@@ -1562,6 +1711,8 @@ bool make_grid(double x_min, double x_max, double y_min, double y_max, int nx, i
     g.mg = (float)(mg * (1.0 + 1e-6));
     g.mgl = (float)(mgl * (1.0 + 1e-6));
     g.nx = nx;
+    g.gnx = nx;
+    g.ox = 0;
     g.ny = ny;
     g.cs = cs;
     g.ncx = (nx + cs - 1) / cs;
@@ -1579,6 +1730,24 @@ bool make_grid(double x_min, double x_max, double y_min, double y_max, int nx, i
 constexpr int kMaxBinBlocks = 1024;  // count workgroups (hist rows)
 constexpr int kMaxTiles = 4096;  // K1/K3 LDS: cursors + per-tile max (12 B/tile at 2 maps)
 static_assert(kMaxTiles <= kScanThreads * 4, "k_tilescan holds <= 4 tiles per thread");
+
+// Images of more than kMaxTiles GPU tiles are projected as WINDOWS of whole tile rows
+// (image rows [ox, ox + nx) x all columns; kMaxTiles / nty tile rows each): every window
+// is one pass of the pipeline over all particles with the footprints clipped to it, and
+// its map is a contiguous part of the (nx, ny) C-order output.  Pixel corners, pitches
+// and the chunk cull stay those of the whole image (Grid::gnx, Grid::ox), so every
+// decision is the one-window decision.
+static inline int window_rows(const Grid& full) {  // tile rows per window
+    return std::max(1, std::min(full.ntx, kMaxTiles / full.nty));
+}
+static inline Grid window_grid(const Grid& full, int tx0, int tx1) {
+    Grid g = full;
+    g.ox = tx0 * kTile;
+    g.nx = std::min(tx1 * kTile, full.gnx) - g.ox;
+    g.ntx = tx1 - tx0;
+    g.ntiles = g.ntx * g.nty;
+    return g;
+}
 
 struct Plan {
     long long n, nblk;  // particles, count workgroups
@@ -1704,18 +1873,14 @@ static void grid_tunables(Grid& g) {
 // The projection on DEVICE arrays (fp32 working copies u, v, h, a0, a1; s: the caller's
 // fp64 arrays for exact re-decisions, or none) into DEVICE outputs, on stream st.  The
 // caller holds the workspace lock and has ordered st behind the previous call.
-// asp_pairs_f64: after binning, emit the pairs of tiles [t0, t1) instead of depositing.
-struct PairsReq {
-    int t0, t1;
-    const long long* offsets;  // device, (t1 - t0) * 4096 per-pixel slot offsets
-    int* particle;             // device outputs
-    double* r2;
-};
+// bin_only (the kernel_func plug-in session): stop after the scatter -- the records stay in
+// ws for k_pairs -- and return the number of wide particles there.
+constexpr int kRetSplit = 1;  // internal: >= 2^31 records in one pass, nothing written
 
 int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float* du,
                      const float* dv, const float* dh, const float* da0, const float* da1,
                      long long n, int kid, int flags, float* d0, float* d1, hipStream_t st,
-                     const PairsReq* pr = nullptr) {
+                     int* bin_only = nullptr) {
     Grid g = gin;
     const int nout = d1 ? 2 : 1;
     const long long npix = (long long)g.nx * g.ny;
@@ -1723,7 +1888,10 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     Plan pl{};
     pl.n = n;
     if (n == 0) {  // all-zero map(s) (the ratio map of 0 / 0 is 0 as well)
-        if (pr) return ASP_OK;
+        if (bin_only) {
+            *bin_only = 0;
+            return ASP_OK;
+        }
         if (!(flags & ASP_F_ACCUMULATE)) {
             StageMark m(ws, kSMemset, st);
             ASP_HIP(hipMemsetAsync(d0, 0, npix * sizeof(float), st));
@@ -1788,7 +1956,8 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, (size_t)cNum * sizeof(int), hipMemcpyDeviceToHost,
                            ws.side));
     ASP_HIP(hipEventRecord(ws.cnt_ev, ws.side));
-    const long long rec_cap = (long long)std::min<size_t>(ws.recs.cap / (2 * sizeof(float4)), 0x7fffffff);
+    // < 2^31 - 1: the tilescan's clamped record count always exceeds it when it overflows
+    const long long rec_cap = (long long)std::min<size_t>(ws.recs.cap / (2 * sizeof(float4)), 0x7ffffffe);
     const int wide_cap = (int)std::min<size_t>(ws.wide.cap / sizeof(int), 0x7fffffff);
     const bool spec = ws.recs.p && ws.wide.p && getenv("ASP_NO_SPECULATE") == nullptr;
     if (spec) {
@@ -1809,8 +1978,12 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     pl.n_slabs = hc[cSlabs];
     pl.n_wide = hc[cWideCount];
     pl.n_large = hc[cLarge];
-    if (pl.n_recs >= 0x7fffffffLL)
-        return fail(ASP_ERR_UNSUPPORTED, "more than 2^31 particle-tile records");
+    long long rec_limit = 0x7fffffffLL;  // 32-bit record cursors (ASP_MAX_RECORDS: tests)
+    if (const char* e = getenv("ASP_MAX_RECORDS")) rec_limit = std::max(1LL, atoll(e));
+    if (pl.n_recs >= rec_limit) {  // nothing written yet: the caller splits the batch
+        if (spec) ASP_HIP(hipStreamSynchronize(st));  // its (no-op) scatter is done
+        return kRetSplit;
+    }
     const bool pre = spec && pl.n_recs <= rec_cap && pl.n_wide <= wide_cap;
     if (spec && !pre) ASP_HIP(hipStreamSynchronize(st));  // its (no-op) scatter is done
     const void* recs_before = ws.recs.p;
@@ -1818,7 +1991,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     ASP_TRY(ensure(ws.wide, (size_t)pl.n_wide * sizeof(int)));
     ASP_TRY(ensure(ws.slabs, (size_t)pl.n_slabs * nout * kTilePix * sizeof(long long)));
     bool placed = false;  // the records are already scattered (by the placement trials)
-    if (!pr && !pre && ws.recs.p != recs_before) {
+    if (!bin_only && !pre && ws.recs.p != recs_before) {
 #define ASP_SC(K, N, A) \
     launch_scatter<K, N, A>(g, s, ws, pl, du, dv, dh, da0, da1, 0x7fffffffLL, 0x7fffffff, st, true)
 #define ASP_SC2(K, A) (nout == 1 ? ASP_SC(K, 1, A) : ASP_SC(K, 2, A))
@@ -1834,17 +2007,11 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
         ASP_TRY(place_records(ws, (size_t)pl.n_recs * 2 * sizeof(float4), st, scatter, placed));
     }
     const bool pre_all = pre || placed;
-    if (pr) {  // the plugin path: records, then the pairs of the requested tiles
+    if (bin_only) {  // the plugin session: the records, for k_pairs
         if (!pre)
             ASP_TRY((launch_scatter<2, 1, kAccF64>(g, s, ws, pl, du, dv, dh, da0, da1, 0x7fffffffLL,
                                                    0x7fffffff, st)));
-        if (pr->t1 > pr->t0) {
-            hipLaunchKernelGGL(k_pairs, dim3((unsigned)(pr->t1 - pr->t0)), dim3(kPairsBlock), 0, st,
-                               g, s, (const float4*)ws.recs.p, (const long long*)ws.tile_start.p,
-                               (const int*)ws.tile_total.p, (const int*)ws.wide.p, pl.n_wide, du,
-                               dv, dh, pr->t0, pr->offsets, pr->particle, pr->r2);
-            ASP_LAUNCHED();
-        }
+        *bin_only = pl.n_wide;
         return ASP_OK;
     }
     int rc;
@@ -1857,6 +2024,23 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
 #undef ASP_TAIL2
 #undef ASP_TAIL
     if (rc != ASP_OK) return rc;
+    ws.stats[9] = 0;
+    if (getenv("ASP_COUNT_EVALS")) {  // diagnostic: the deposit kernels' lane-slots
+        ASP_TRY(ensure(ws.aux[5], 3 * sizeof(unsigned long long)));
+        ASP_HIP(hipMemsetAsync(ws.aux[5].p, 0, 3 * sizeof(unsigned long long), st));
+        hipLaunchKernelGGL(k_evals, dim3((unsigned)(pl.n_items + (pl.n_wide ? g.ntiles : 0))),
+                           dim3(kBlock), 0, st, g, kid, s, (const float4*)ws.recs.p,
+                           (const Item*)ws.items.p, pl.n_items, du, dv, dh, (const int*)ws.wide.p,
+                           pl.n_wide, (unsigned long long*)ws.aux[5].p);
+        ASP_LAUNCHED();
+        unsigned long long e[3];
+        ASP_HIP(hipMemcpyAsync(e, ws.aux[5].p, sizeof(e), hipMemcpyDeviceToHost, st));
+        ASP_HIP(hipStreamSynchronize(st));
+        ws.stats[9] = (long long)(e[0] + e[1] + e[2]);
+        ws.stats[10] = (long long)e[0];
+        ws.stats[11] = (long long)e[1];
+        ws.stats[12] = (long long)e[2];
+    }
     ws.stats[0] = pl.n_recs;
     ws.stats[1] = pl.n_items;
     ws.stats[2] = pl.n_wide;
@@ -1866,6 +2050,86 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     ws.stats[6] = pl.n_merges;
     ws.stats[7] = pl.n_slabs;
     ws.stats[8] = pl.n_large;
+    return ASP_OK;
+}
+
+// Particles per pipeline pass: particle indices and record cursors are 32-bit, so larger
+// calls run as batches accumulating into the same maps (ASP_MAX_BATCH lowers it for tests).
+static long long max_batch() {
+    long long b = 1LL << 30;
+    if (const char* e = getenv("ASP_MAX_BATCH")) b = std::max(1LL, atoll(e));
+    return b;
+}
+
+static Src64 src_from(const Src64& s, long long b) {  // particles b.. of s
+    Src64 r = s;
+    if (s.u64) {
+        r.u64 += b * s.stride;
+        r.v64 += b * s.stride;
+        r.cu64 += b * s.stride;
+        r.cv64 += b * s.stride;
+        r.h64 += b;
+    }
+    r.u32 += b;
+    r.v32 += b;
+    r.h32 += b;
+    return r;
+}
+
+// The whole call: every window of the image (window_grid) and, inside it, particle
+// batches of < 2^31 particles, each batch split in two while its records reach 2^31.
+// Batches after the first accumulate; the ratio of a batched map is formed at the end.
+int project2d_full(Workspace& ws, const Grid& full, const Src64& s, const float* du,
+                   const float* dv, const float* dh, const float* da0, const float* da1,
+                   long long n, int kid, int flags, float* d0, float* d1, hipStream_t st) {
+    const int wr = window_rows(full);
+    const long long B = max_batch();
+    long long agg[kNStats] = {0};
+    for (int tx0 = 0; tx0 < full.ntx; tx0 += wr) {
+        const Grid g = window_grid(full, tx0, std::min(tx0 + wr, full.ntx));
+        const long long off = (long long)g.ox * full.ny;
+        float* w0 = d0 + off;
+        float* w1 = d1 ? d1 + off : nullptr;
+        std::vector<std::pair<long long, long long>> todo;  // batches, last first
+        for (long long a = ((n - 1) / B) * B; a >= 0; a -= B)
+            todo.push_back({a, std::min(n, a + B)});
+        if (todo.empty()) todo.push_back({0, 0});
+        bool batched = todo.size() > 1;
+        int passes = 0;
+        while (!todo.empty()) {
+            const auto [a, b] = todo.back();
+            todo.pop_back();
+            int f = flags;
+            if (batched || b - a < n) f &= ~ASP_F_RATIO;  // ratio after the last batch
+            if (passes > 0) f |= ASP_F_ACCUMULATE;
+            const int rc = project2d_device(ws, g, src_from(s, a), du + a, dv + a, dh + a,
+                                            da0 + a, da1 ? da1 + a : nullptr, b - a, kid, f,
+                                            w0, w1, st);
+            if (rc == kRetSplit) {
+                if (b - a < 2)
+                    return fail(ASP_ERR_UNSUPPORTED, "one particle makes >= 2^31 records");
+                const long long m = a + (b - a) / 2;
+                todo.push_back({m, b});
+                todo.push_back({a, m});
+                batched = true;
+                continue;
+            }
+            ASP_TRY(rc);
+            ++passes;
+            for (int k : {0, 1, 2, 6, 7, 8, 9, 10, 11, 12}) agg[k] += ws.stats[k];
+        }
+        if (passes > 1 && (flags & ASP_F_RATIO)) {
+            const long long npix = (long long)g.nx * g.ny;
+            const long long blocks = std::min<long long>((npix + kBlock - 1) / kBlock, 8192);
+            StageMark m(ws, kSRatio, st);
+            hipLaunchKernelGGL(k_ratio, dim3((unsigned)std::max<long long>(1, blocks)), dim3(kBlock),
+                               0, st, w0, (const float*)w1, npix);
+            ASP_LAUNCHED();
+            m.done();
+        }
+    }
+    for (int k : {0, 1, 2, 6, 7, 8, 9, 10, 11, 12}) ws.stats[k] = agg[k];
+    ws.stats[4] = full.ntiles;
     return ASP_OK;
 }
 
@@ -1879,7 +2143,6 @@ static int check_args(const void* a1, const float* out0, const float* out1, long
     if ((flags & ASP_F_RATIO) && !out1) return fail(ASP_ERR_INVALID, "ASP_F_RATIO needs out1");
     if ((flags & ASP_F_RATIO) && (flags & ASP_F_ACCUMULATE))
         return fail(ASP_ERR_INVALID, "ASP_F_RATIO cannot be combined with ASP_F_ACCUMULATE");
-    if (n > 0x7fffffffLL) return fail(ASP_ERR_UNSUPPORTED, "n >= 2^31 particles per call");
     return ASP_OK;
 }
 
@@ -1890,8 +2153,8 @@ static int setup_grid(double x_min, double x_max, double y_min, double y_max, in
                     "invalid grid: need nx, ny, chunk_size >= 1, finite x_max > x_min, "
                     "y_max > y_min");
     grid_tunables(g);
-    if (g.ntiles > kMaxTiles)
-        return fail(ASP_ERR_UNSUPPORTED, "grid too large (more than 4096 64x64 tiles)");
+    if (g.nty > kMaxTiles)
+        return fail(ASP_ERR_UNSUPPORTED, "image too wide (ny > 4096 * 64 pixels)");
     return ASP_OK;
 }
 
@@ -1930,6 +2193,7 @@ static int project2d(const float* u, const float* v, const float* h, const float
     std::lock_guard<std::mutex> lock(ws.mu);
     hipStream_t st = (hipStream_t)stream;
     ASP_TRY(ws_begin(ws, st));
+    WsEnd ws_end_(ws, st);
     const int nout = out1 ? 2 : 1;
     const bool dev = flags & ASP_F_DEVICE_PTRS;
     const long long npix = (long long)nx * ny;
@@ -1949,9 +2213,9 @@ static int project2d(const float* u, const float* v, const float* h, const float
         ASP_TRY(host_outputs(ws, out0, out1, npix, flags, st, d0, d1));
     }
     const Src64 s{nullptr, nullptr, nullptr, nullptr, nullptr, 0, du, dv, dh};
-    ASP_TRY(project2d_device(ws, g, s, du, dv, dh, da0, da1, n, kid, flags, d0, d1, st));
+    ASP_TRY(project2d_full(ws, g, s, du, dv, dh, da0, da1, n, kid, flags, d0, d1, st));
     if (!dev) ASP_TRY(host_results(out0, out1, d0, d1, npix, st));
-    return ws_end(ws, st);
+    return ws_end_.finish();
 }
 
 // create_image on the reader's fp64 arrays: stage (axis selection, fp32 working copies in
@@ -1975,6 +2239,7 @@ static int project2d_f64(const double* pos, const double* h, const double* a0,
     std::lock_guard<std::mutex> lock(ws.mu);
     hipStream_t st = (hipStream_t)stream;
     ASP_TRY(ws_begin(ws, st));
+    WsEnd ws_end_(ws, st);
     const int nout = out1 ? 2 : 1;
     const bool dev = flags & ASP_F_DEVICE_PTRS;
     const bool dev_out = dev || (flags & ASP_F_DEVICE_OUTPUTS);  // maps stay on the device
@@ -2002,21 +2267,80 @@ static int project2d_f64(const double* pos, const double* h, const double* a0,
     static const int cols[3][2] = {{1, 2}, {0, 2}, {0, 1}};  // _projector.py:38-46
     const Src64 s{dpos + cols[axis][0], dpos + cols[axis][1], dpos + cols[cull_axis][0],
                   dpos + cols[cull_axis][1], dh64, 3, f[0], f[1], f[2]};
-    ASP_TRY(project2d_device(ws, g, s, f[0], f[1], f[2], f[3], f[4], n, kid,
-                             (flags & ~ASP_F_DEVICE_OUTPUTS) | ASP_F_DEVICE_PTRS, d0, d1, st));
+    ASP_TRY(project2d_full(ws, g, s, f[0], f[1], f[2], f[3], f[4], n, kid,
+                           (flags & ~ASP_F_DEVICE_OUTPUTS) | ASP_F_DEVICE_PTRS, d0, d1, st));
     if (!dev_out) ASP_TRY(host_results(out0, out1, d0, d1, npix, st));
-    return ws_end(ws, st);
+    return ws_end_.finish();
 }
 
-// Pairs of GPU tiles [t0, t1) for the kernel_func plugin: stage, bin, emit.
-static int pairs_f64(const double* pos, const double* h, long long n, int axis, double x_min,
-                     double x_max, double y_min, double y_max, int nx, int ny, int cs, int t0,
-                     int t1, const long long* offsets, int* particle, double* r2, int flags,
-                     int device, void* stream) {
+// The kernel_func plug-in session (asp_pairs_begin / _emit / _end): the particles are
+// staged and binned ONCE per create_image call, window by window (window_grid); the
+// records of the current window stay resident in the session's own workspace between the
+// emits, so a map needing many host batches costs one binning per window, not one per
+// batch.
+struct PairsSession {
+    Workspace ws;  // the session's own buffers (a call on the device cannot evict them)
+    Grid full;
+    Src64 s{};
+    const float* f[3] = {nullptr, nullptr, nullptr};  // fp32 working copies u, v, h
+    long long n = 0;
+    int device = 0;
+    int flags = 0;
+    hipStream_t st = nullptr;
+    int wtx0 = -1, wtx1 = -1;  // tile rows binned now
+    int n_wide = 0;
+    std::vector<long long> tile_pairs;  // per GPU tile of the whole image
+};
+
+static inline int pairs_window_of(const PairsSession& S, int t) {  // first tile row of t's window
+    const int tx = t / S.full.nty, wr = window_rows(S.full);
+    return (tx / wr) * wr;
+}
+
+// Bin the window holding tile rows [tx0, ..) and count its pixels' pairs (MODE 0).
+static int pairs_bin(PairsSession& S, int tx0) {
+    Workspace& ws = S.ws;
+    const int wr = window_rows(S.full);
+    const int tx1 = std::min(tx0 + wr, S.full.ntx);
+    if (S.wtx0 == tx0) return ASP_OK;
+    const Grid g = window_grid(S.full, tx0, tx1);
+    S.wtx0 = -1;
+    ASP_TRY(ensure(ws.pairs[0], (size_t)g.ntiles * kTilePix * sizeof(int)));  // pixcnt
+    ASP_TRY(ensure(ws.pairs[3], (size_t)g.ntiles * sizeof(long long)));       // tile totals
+    if (S.n == 0) {
+        ASP_HIP(hipMemsetAsync(ws.pairs[3].p, 0, (size_t)g.ntiles * sizeof(long long), S.st));
+        S.n_wide = 0;
+    } else {
+        int nw = 0;
+        const int rc = project2d_device(ws, g, S.s, S.f[0], S.f[1], S.f[2], S.f[2], nullptr, S.n,
+                                        ASP_KERNEL_INDICATOR, 0, nullptr, nullptr, S.st, &nw);
+        if (rc == kRetSplit)
+            return fail(ASP_ERR_UNSUPPORTED, "kernel_func plug-in: >= 2^31 records in one window");
+        ASP_TRY(rc);
+        S.n_wide = nw;
+        hipLaunchKernelGGL(k_pairs<0>, dim3((unsigned)g.ntiles), dim3(kPairsBlock), 0, S.st, g,
+                           S.s, (const float4*)ws.recs.p, (const long long*)ws.tile_start.p,
+                           (const int*)ws.tile_total.p, (const int*)ws.wide.p, nw, S.f[0], S.f[1],
+                           S.f[2], 0, (int*)ws.pairs[0].p, (long long*)ws.pairs[3].p,
+                           (const long long*)nullptr, (long long*)nullptr, (int*)nullptr,
+                           (double*)nullptr, (int*)nullptr);
+        ASP_LAUNCHED();
+    }
+    S.wtx0 = tx0;
+    S.wtx1 = tx1;
+    return ASP_OK;
+}
+
+static int pairs_begin(const double* pos, const double* h, long long n, int axis, double x_min,
+                       double x_max, double y_min, double y_max, int nx, int ny, int cs,
+                       int flags, int device, void* stream, long long* tile_pairs,
+                       PairsSession** out) {
+    *out = nullptr;
     if (n < 0) return fail(ASP_ERR_INVALID, "n < 0");
-    if (n > 0x7fffffffLL) return fail(ASP_ERR_UNSUPPORTED, "n >= 2^31 particles per call");
+    if (n > 0x7fffffffLL)
+        return fail(ASP_ERR_UNSUPPORTED, "kernel_func plug-in: n >= 2^31 particles per call");
     if (n > 0 && (!pos || !h)) return fail(ASP_ERR_INVALID, "NULL particle array");
-    if (!offsets) return fail(ASP_ERR_INVALID, "NULL offsets");
+    if (!tile_pairs) return fail(ASP_ERR_INVALID, "NULL tile_pairs");
     const int cull_axis = (axis >> 4) ? (axis >> 4) - 1 : (axis & 15);
     axis &= 15;
     if (axis < 0 || axis > 2 || cull_axis < 0 || cull_axis > 2)
@@ -2024,58 +2348,152 @@ static int pairs_f64(const double* pos, const double* h, long long n, int axis, 
     Grid g;
     ASP_TRY(setup_grid(x_min, x_max, y_min, y_max, nx, ny, cs, g));
     g.mixed = cull_axis != axis;
-    if (t0 < 0 || t1 > g.ntiles || t0 > t1) return fail(ASP_ERR_INVALID, "bad tile range");
     ASP_TRY(set_device(device));
-    Workspace& ws = g_ws[device];
-    std::lock_guard<std::mutex> lock(ws.mu);
-    hipStream_t st = (hipStream_t)stream;
-    ASP_TRY(ws_begin(ws, st));
+    PairsSession* S = new (std::nothrow) PairsSession();
+    if (!S) return fail(ASP_ERR_NOMEM, "session");
+    S->full = g;
+    S->n = n;
+    S->device = device;
+    S->flags = flags;
+    S->st = (hipStream_t)stream;
+    Workspace& ws = S->ws;
+    auto bail = [&](int rc) {
+        (void)hipStreamSynchronize(S->st);
+        for (Buf* b : ws.all_bufs())
+            if (b->p) (void)hipFree(b->p);
+        release_pinned(ws);
+        delete S;
+        return rc;
+    };
     const bool dev = flags & ASP_F_DEVICE_PTRS;
-    const long long nt = t1 - t0, npx = nt * kTilePix;
-    long long total = 0;
-    if (dev) {
-        ASP_HIP(hipMemcpyAsync(&total, offsets + npx, sizeof(long long), hipMemcpyDeviceToHost, st));
-        ASP_HIP(hipStreamSynchronize(st));
-    } else {
-        total = offsets[npx];
-    }
     const double *dpos = pos, *dh64 = h;
-    const long long* doff = offsets;
+    if (!dev && n > 0) {
+        int rc = ensure(ws.in64[0], (size_t)n * 3 * sizeof(double));
+        if (rc == ASP_OK) rc = ensure(ws.in64[1], (size_t)n * sizeof(double));
+        if (rc == ASP_OK) rc = h2d_staged(ws, ws.in64[0].p, pos, (size_t)n * 3 * sizeof(double), S->st);
+        if (rc == ASP_OK) rc = h2d_staged(ws, ws.in64[1].p, h, (size_t)n * sizeof(double), S->st);
+        if (rc != ASP_OK) return bail(rc);
+        dpos = (const double*)ws.in64[0].p;
+        dh64 = (const double*)ws.in64[1].p;
+    }
+    for (int k = 0; k < 3; ++k) {
+        const int rc = ensure(ws.in[k], (size_t)n * sizeof(float));
+        if (rc != ASP_OK) return bail(rc);
+    }
+    float* f[3] = {(float*)ws.in[0].p, (float*)ws.in[1].p, (float*)ws.in[2].p};
+    if (n > 0) {
+        const int rc = stage_device(dpos, dh64, nullptr, nullptr, n, axis, f[0], f[1], f[2],
+                                    nullptr, nullptr, S->st);
+        if (rc != ASP_OK) return bail(rc);
+    }
+    static const int cols[3][2] = {{1, 2}, {0, 2}, {0, 1}};  // _projector.py:38-46
+    S->s = Src64{dpos + cols[axis][0], dpos + cols[axis][1], dpos + cols[cull_axis][0],
+                 dpos + cols[cull_axis][1], dh64, 3, f[0], f[1], f[2]};
+    for (int k = 0; k < 3; ++k) S->f[k] = f[k];
+    // every window once: its per-tile pair totals (the last window stays binned)
+    S->tile_pairs.assign((size_t)g.ntiles, 0);
+    const int wr = window_rows(g);
+    for (int tx0 = 0; tx0 < g.ntx; tx0 += wr) {
+        int rc = pairs_bin(*S, tx0);
+        const Grid w = window_grid(g, tx0, std::min(tx0 + wr, g.ntx));
+        if (rc == ASP_OK)
+            rc = hipMemcpyAsync(S->tile_pairs.data() + (size_t)tx0 * g.nty, ws.pairs[3].p,
+                                (size_t)w.ntiles * sizeof(long long), hipMemcpyDeviceToHost,
+                                S->st) == hipSuccess ? ASP_OK : fail(ASP_ERR_HIP, "tile totals");
+        if (rc == ASP_OK)
+            rc = hipStreamSynchronize(S->st) == hipSuccess ? ASP_OK : fail(ASP_ERR_HIP, "sync");
+        if (rc != ASP_OK) return bail(rc);
+    }
+    std::copy(S->tile_pairs.begin(), S->tile_pairs.end(), tile_pairs);
+    *out = S;
+    return ASP_OK;
+}
+
+// Pairs of the GPU tiles [t0, t1) (global row-major tile ids), pixels tile by tile and
+// lx * 64 + ly inside a tile: offsets ((t1 - t0) * 4096 + 1, from 0), particle, r2.
+static int pairs_emit(PairsSession& S, int t0, int t1, long long* offsets, int* particle,
+                      double* r2) {
+    if (t0 < 0 || t1 > S.full.ntiles || t0 > t1) return fail(ASP_ERR_INVALID, "bad tile range");
+    if (!offsets) return fail(ASP_ERR_INVALID, "NULL offsets");
+    Workspace& ws = S.ws;
+    ASP_HIP(hipSetDevice(S.device));
+    const bool dev = S.flags & ASP_F_DEVICE_PTRS;
+    const long long npx = (long long)(t1 - t0) * kTilePix;
+    long long total = 0;
+    for (int t = t0; t < t1; ++t) total += S.tile_pairs[t];
+    if (total > 0 && (!particle || !r2)) return fail(ASP_ERR_INVALID, "NULL pair outputs");
+    long long* doff = offsets;
     int* dpart = particle;
     double* dr2 = r2;
     if (!dev) {
-        ASP_TRY(ensure(ws.in64[0], (size_t)n * 3 * sizeof(double)));
-        ASP_TRY(ensure(ws.in64[1], (size_t)n * sizeof(double)));
-        if (n > 0) {
-            ASP_TRY(h2d_staged(ws, ws.in64[0].p, pos, (size_t)n * 3 * sizeof(double), st));
-            ASP_TRY(h2d_staged(ws, ws.in64[1].p, h, (size_t)n * sizeof(double), st));
+        ASP_TRY(ensure(ws.aux[0], (size_t)(npx + 1) * sizeof(long long)));
+        ASP_TRY(ensure(ws.aux[1], (size_t)std::max(total, 1LL) * sizeof(int)));
+        ASP_TRY(ensure(ws.aux[2], (size_t)std::max(total, 1LL) * sizeof(double)));
+        doff = (long long*)ws.aux[0].p;
+        dpart = (int*)ws.aux[1].p;
+        dr2 = (double*)ws.aux[2].p;
+    }
+    ASP_TRY(ensure(ws.aux[3], (size_t)(t1 - t0 + 1) * sizeof(long long)));
+    ASP_TRY(ensure(ws.aux[4], sizeof(int)));
+    int* dovf = (int*)ws.aux[4].p;
+    ASP_HIP(hipMemsetAsync(dovf, 0, sizeof(int), S.st));
+    if (npx == 0) {
+        if (!dev) offsets[0] = 0;
+        else ASP_HIP(hipMemsetAsync(offsets, 0, sizeof(long long), S.st));
+    }
+    // window by window (the session re-bins only when the range moves to another window)
+    long long done = 0;
+    for (int a = t0; a < t1;) {
+        const int tx0 = pairs_window_of(S, a);
+        ASP_TRY(pairs_bin(S, tx0));
+        const int wt0 = tx0 * S.full.nty;                          // window's first tile
+        const int b = std::min(t1, S.wtx1 * S.full.nty);
+        std::vector<long long> base((size_t)(b - a));
+        for (int t = a; t < b; ++t) {
+            base[t - a] = done;
+            done += S.tile_pairs[t];
         }
-        dpos = (const double*)ws.in64[0].p;
-        dh64 = (const double*)ws.in64[1].p;
-        ASP_TRY(ensure(ws.pairs[0], (size_t)(npx + 1) * sizeof(long long)));
-        ASP_TRY(ensure(ws.pairs[1], (size_t)std::max(total, 1LL) * sizeof(int)));
-        ASP_TRY(ensure(ws.pairs[2], (size_t)std::max(total, 1LL) * sizeof(double)));
-        ASP_HIP(hipMemcpyAsync(ws.pairs[0].p, offsets, (size_t)(npx + 1) * sizeof(long long),
-                               hipMemcpyHostToDevice, st));
-        doff = (const long long*)ws.pairs[0].p;
-        dpart = (int*)ws.pairs[1].p;
-        dr2 = (double*)ws.pairs[2].p;
+        long long* dbase = (long long*)ws.aux[3].p;
+        ASP_HIP(hipMemcpyAsync(dbase, base.data(), base.size() * sizeof(long long),
+                               hipMemcpyHostToDevice, S.st));
+        const Grid g = window_grid(S.full, S.wtx0, S.wtx1);
+        hipLaunchKernelGGL(k_pairs<1>, dim3((unsigned)(b - a)), dim3(kPairsBlock), 0, S.st, g,
+                           S.s, (const float4*)ws.recs.p, (const long long*)ws.tile_start.p,
+                           (const int*)ws.tile_total.p, (const int*)ws.wide.p, S.n_wide, S.f[0],
+                           S.f[1], S.f[2], a - wt0, (int*)ws.pairs[0].p, (long long*)nullptr,
+                           (const long long*)dbase, doff + (long long)(a - t0) * kTilePix, dpart,
+                           dr2, dovf);
+        ASP_LAUNCHED();
+        ASP_HIP(hipStreamSynchronize(S.st));  // dbase is reused by the next window's launch
+        a = b;
     }
-    for (int k = 0; k < 4; ++k) ASP_TRY(ensure(ws.in[k], (size_t)n * sizeof(float)));
-    float* f[4] = {(float*)ws.in[0].p, (float*)ws.in[1].p, (float*)ws.in[2].p, (float*)ws.in[3].p};
-    ASP_TRY(stage_device(dpos, dh64, dh64, nullptr, n, axis, f[0], f[1], f[2], f[3], nullptr, st));
-    static const int cols[3][2] = {{1, 2}, {0, 2}, {0, 1}};  // _projector.py:38-46
-    const Src64 s{dpos + cols[axis][0], dpos + cols[axis][1], dpos + cols[cull_axis][0],
-                  dpos + cols[cull_axis][1], dh64, 3, f[0], f[1], f[2]};
-    const PairsReq pr{t0, t1, doff, dpart, dr2};
-    ASP_TRY(project2d_device(ws, g, s, f[0], f[1], f[2], f[3], nullptr, n, ASP_KERNEL_INDICATOR, 0,
-                             nullptr, nullptr, st, &pr));
-    if (!dev && total > 0) {
-        ASP_HIP(hipMemcpyAsync(particle, dpart, (size_t)total * sizeof(int), hipMemcpyDeviceToHost, st));
-        ASP_HIP(hipMemcpyAsync(r2, dr2, (size_t)total * sizeof(double), hipMemcpyDeviceToHost, st));
+    int ovf = 0;
+    ASP_HIP(hipMemcpyAsync(&ovf, dovf, sizeof(int), hipMemcpyDeviceToHost, S.st));
+    if (!dev) {
+        ASP_HIP(hipMemcpyAsync(offsets, doff, (size_t)(npx + 1) * sizeof(long long),
+                               hipMemcpyDeviceToHost, S.st));
+        if (total > 0) {
+            ASP_HIP(hipMemcpyAsync(particle, dpart, (size_t)total * sizeof(int),
+                                   hipMemcpyDeviceToHost, S.st));
+            ASP_HIP(hipMemcpyAsync(r2, dr2, (size_t)total * sizeof(double), hipMemcpyDeviceToHost,
+                                   S.st));
+        }
     }
-    ASP_HIP(hipStreamSynchronize(st));
-    return ws_end(ws, st);
+    ASP_HIP(hipStreamSynchronize(S.st));
+    if (ovf) return fail(ASP_ERR_INVALID, "pair slots overflowed (counts and pairs disagree)");
+    return ASP_OK;
+}
+
+static int pairs_end(PairsSession* S) {
+    if (!S) return ASP_OK;
+    (void)hipSetDevice(S->device);
+    (void)hipStreamSynchronize(S->st);
+    for (Buf* b : S->ws.all_bufs())
+        if (b->p) (void)hipFree(b->p);
+    if (S->ws.h_counters) (void)hipHostFree(S->ws.h_counters);
+    release_pinned(S->ws);
+    delete S;
+    return ASP_OK;
 }
 
 }  // namespace asp
@@ -2116,14 +2534,29 @@ int asp_project2d_f64(const double* positions, const double* h, const double* a0
                          chunk_size, kernel_id, flags, out0, out1, device, stream);
 }
 
-int asp_pairs_f64(const double* positions, const double* h, int64_t n, int32_t axis,
-                  double u_min, double u_max, double v_min, double v_max, int32_t nx, int32_t ny,
-                  int32_t chunk_size, int32_t tile_lo, int32_t tile_hi, const int64_t* offsets,
-                  int32_t* particle, double* r2, int32_t flags, int32_t device, void* stream) {
+int asp_pairs_begin(const double* positions, const double* h, int64_t n, int32_t axis,
+                    double u_min, double u_max, double v_min, double v_max, int32_t nx,
+                    int32_t ny, int32_t chunk_size, int32_t flags, int32_t device, void* stream,
+                    int64_t* tile_pairs, void** session) {
     t_err.clear();
-    return pairs_f64(positions, h, n, axis, u_min, u_max, v_min, v_max, nx, ny, chunk_size,
-                     tile_lo, tile_hi, (const long long*)offsets, particle, r2, flags, device,
-                     stream);
+    if (!session) return fail(ASP_ERR_INVALID, "NULL session");
+    PairsSession* S = nullptr;
+    const int rc = pairs_begin(positions, h, n, axis, u_min, u_max, v_min, v_max, nx, ny,
+                               chunk_size, flags, device, stream, (long long*)tile_pairs, &S);
+    *session = S;
+    return rc;
+}
+
+int asp_pairs_emit(void* session, int32_t tile_lo, int32_t tile_hi, int64_t* offsets,
+                   int32_t* particle, double* r2) {
+    t_err.clear();
+    if (!session) return fail(ASP_ERR_INVALID, "NULL session");
+    return pairs_emit(*(PairsSession*)session, tile_lo, tile_hi, (long long*)offsets, particle, r2);
+}
+
+int asp_pairs_end(void* session) {
+    t_err.clear();
+    return pairs_end((PairsSession*)session);
 }
 
 int asp_kernel_eval(int32_t kernel_id, const double* r, const double* h, double* w, int64_t n,
@@ -2137,6 +2570,7 @@ int asp_kernel_eval(int32_t kernel_id, const double* r, const double* h, double*
     std::lock_guard<std::mutex> lock(ws.mu);
     hipStream_t st = (hipStream_t)stream;
     ASP_TRY(ws_begin(ws, st));
+    WsEnd ws_end_(ws, st);
     const double *dr = r, *dh = h;
     double* dw = w;
     bool dev = flags & ASP_F_DEVICE_PTRS;
@@ -2157,7 +2591,7 @@ int asp_kernel_eval(int32_t kernel_id, const double* r, const double* h, double*
         ASP_HIP(hipMemcpyAsync(w, dw, n * sizeof(double), hipMemcpyDeviceToHost, st));
         ASP_HIP(hipStreamSynchronize(st));
     }
-    return ws_end(ws, st);
+    return ws_end_.finish();
 }
 
 int asp_chunk_ranges(const float* u, const float* v, const float* h, int64_t n, double u_min,
@@ -2175,6 +2609,7 @@ int asp_chunk_ranges(const float* u, const float* v, const float* h, int64_t n, 
     std::lock_guard<std::mutex> lock(ws.mu);
     hipStream_t st = (hipStream_t)stream;
     ASP_TRY(ws_begin(ws, st));
+    WsEnd ws_end_(ws, st);
     bool dev = flags & ASP_F_DEVICE_PTRS;
     const float *du = u, *dv = v, *dh = h;
     int* o[4] = {cx0, cx1, cy0, cy1};
@@ -2202,7 +2637,7 @@ int asp_chunk_ranges(const float* u, const float* v, const float* h, int64_t n, 
             ASP_HIP(hipMemcpyAsync(dst[k], o[k], n * sizeof(int), hipMemcpyDeviceToHost, st));
         ASP_HIP(hipStreamSynchronize(st));
     }
-    return ws_end(ws, st);
+    return ws_end_.finish();
 }
 
 int asp_pixel_neighbours(const float* u, const float* v, const float* h, int64_t n,
@@ -2230,6 +2665,7 @@ int asp_pixel_neighbours(const float* u, const float* v, const float* h, int64_t
     std::lock_guard<std::mutex> lock(ws.mu);
     hipStream_t st = nullptr;
     ASP_TRY(ws_begin(ws, st));
+    WsEnd ws_end_(ws, st);
     const float* src[3] = {u, v, h};
     for (int k = 0; k < 3; ++k) {
         ASP_TRY(ensure(ws.in[k], n * sizeof(float)));
@@ -2268,7 +2704,7 @@ int asp_pixel_neighbours(const float* u, const float* v, const float* h, int64_t
         ASP_HIP(hipMemcpyAsync(index, ws.aux[3].p, wcap * sizeof(int), hipMemcpyDeviceToHost, st));
         ASP_HIP(hipStreamSynchronize(st));
     }
-    return ws_end(ws, st);
+    return ws_end_.finish();
 }
 
 int asp_ratio(float* out0, const float* out1, int64_t n, int32_t device, void* stream) {
@@ -2328,7 +2764,7 @@ int asp_profile_read(int32_t device, double* ms_sum, int64_t* launches, int32_t 
 
 int asp_last_stats(int32_t device, int64_t* stats, int32_t nstats) {
     if (device < 0 || device >= 64 || !stats) return fail(ASP_ERR_INVALID, "bad argument");
-    for (int k = 0; k < nstats && k < 9; ++k) stats[k] = g_ws[device].stats[k];
+    for (int k = 0; k < nstats && k < kNStats; ++k) stats[k] = g_ws[device].stats[k];
     return ASP_OK;
 }
 

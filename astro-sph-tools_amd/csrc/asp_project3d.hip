@@ -625,6 +625,7 @@ static int project3d(const float* x, const float* y, const float* z, const float
     std::lock_guard<std::mutex> lock(ws.mu);
     hipStream_t st = (hipStream_t)stream;
     ASP_TRY(ws_begin(ws, st));
+    WsEnd ws_end_(ws, st);
     const bool dev = flags & ASP_F_DEVICE_PTRS;
     const int acc = (flags & ASP_F_ACCUMULATE) ? 1 : 0;
     const long long nvox = (long long)nx * ny * g.nzl;
@@ -758,7 +759,7 @@ static int project3d(const float* x, const float* y, const float* z, const float
     ws.stats[6] = n_merges;
     ws.stats[7] = n_slabs;
     ws.stats[8] = n > 0 ? 1 : 0;
-    return ws_end(ws, st);
+    return ws_end_.finish();
 }
 
 }  // namespace asp

@@ -240,6 +240,7 @@ static int stage_particles(const double* pos, const double* h, const double* a0,
     Workspace& ws = g_ws[device];
     std::lock_guard<std::mutex> lock(ws.mu);
     ASP_TRY(ws_begin(ws, st));
+    WsEnd ws_end_(ws, st);
     ASP_TRY(ensure(ws.aux[5], 2 * sizeof(unsigned long long)));
     unsigned long long* dimg = (unsigned long long*)ws.aux[5].p;
     ASP_HIP(hipMemsetAsync(dimg, 0, 2 * sizeof(unsigned long long), st));
@@ -280,7 +281,7 @@ static int stage_particles(const double* pos, const double* h, const double* a0,
     unsigned long long nimg[2] = {0, 0};
     ASP_HIP(hipMemcpyAsync(nimg, dimg, sizeof(nimg), hipMemcpyDeviceToHost, st));
     ASP_HIP(hipStreamSynchronize(st));
-    ASP_TRY(ws_end(ws, st));
+    ASP_TRY(ws_end_.finish());
     if (nimg[1])
         return fail(ASP_ERR_UNSUPPORTED, std::to_string(nimg[1]) + " particles reach beyond " +
                                              std::to_string(kMaxImageShift) +

@@ -29,6 +29,16 @@ sys.path.insert(0, os.path.join(REPO, "astro-sph-tools_amd"))
 
 METRIC = "Mpixels/s + particles/s, 10^8-particle 4096² projection at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table: peak FP32 (vector), spec
+# Algorithmic fp32 flops per included (pixel, particle) pair, an FMA counted as 2
+# (DESIGN.md §4 "compute roofline"): dx, dy (2), r^2 = dx dx + dy dy (3), sqrt (1),
+# q = r / h (1), the shape, and a * W added into each map (2 per map).
+SHAPE_FLOPS = {"wendland_c2": 7, "cubic": 10, "indicator": 0}
+COMPUTE_BOUND = ("gather", "wide", "cube_deposit")  # kernels priced against the VALU peak
+
+
+def pair_flops(kernel, nout):
+    return 8 + SHAPE_FLOPS[kernel] + 2 * nout
 
 
 def parse():
@@ -184,6 +194,12 @@ def run_cube(args, world, rank, local, dev):
     dom = max(prof, key=lambda k: prof[k][0])
     dom_ms = prof[dom][0] / max(1, prof[dom][1])
     bytes_alg = args.n * 20 + C ** 3 * 4  # x, y, z, h, m + the cube (SURVEY §8(d) cfg 5)
+    pairs = None
+    if dom in COMPUTE_BOUND:  # untimed: the exact voxel pairs (indicator cube, summed)
+        cnt = project3d(x, y, z, h, torch.ones_like(h), cube_size=(C, C, C), extent=ext,
+                        kernel="indicator", planes=(K[rank], K[rank + 1]))
+        pairs = float(cnt.double().sum().item())
+        del cnt
     res = {
         "metric": "Mvoxels/s + particles/s, 10^8-particle 512^3 density cube",
         "value": round(C ** 3 * args.steps / elapsed / 1e6, 3), "unit": "Mvoxels/s",
@@ -204,6 +220,14 @@ def run_cube(args, world, rank, local, dev):
         "records_per_particle": round(st["records"] / max(1, n_local), 4),
         "work_items": st["items"], "output_ok": ok,
     }
+    if pairs is not None:  # compute-bound: the VALU roofline, the HBM one beside it
+        F = 11 + SHAPE_FLOPS[kernel] + 2  # dx, dy, dz (3), r^2 (5), sqrt, q, shape, a W
+        tf = pairs * F / (dom_ms * 1e-3) / 1e12
+        res["roofline_hbm"] = res["roofline"]
+        res["roofline"] = {"bound": "valu", "kernel": dom, "achieved": round(tf, 3),
+                           "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(tf / VALU_PEAK_TFLOPS, 4), "included_pairs": int(pairs),
+                           "flops_per_pair": F, "pairs_per_s": pairs / (dom_ms * 1e-3)}
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -398,6 +422,49 @@ def run_ion(args, dev):
     print(json.dumps(res), flush=True)
 
 
+def pair_work(u, v, h, G, ext, kernel, world, dev):
+    """Untimed: the map's exact included pairs (the indicator kernel's per-pixel neighbour
+    counts, summed; every pixel's count is exact in fp32 below 2^24) and the (pixel,
+    particle) lane-slots the deposit kernels spend (the library's ASP_COUNT_EVALS
+    diagnostic), of this rank's particles."""
+    import torch
+    import torch.distributed as dist
+    from asp_amd.device import project2d, stats
+    ones = torch.ones_like(h)
+    cnt, _ = project2d(u, v, h, ones, image_size=(G, G), extent=ext, kernel="indicator")
+    os.environ["ASP_COUNT_EVALS"] = "1"
+    try:
+        project2d(u, v, h, ones, image_size=(G, G), extent=ext, kernel=kernel)
+        torch.cuda.synchronize()
+        st = stats(dev.index or 0)
+    finally:
+        del os.environ["ASP_COUNT_EVALS"]
+    del world, dist  # per rank: priced against this rank's own kernel time
+    return [float(cnt.double().sum().item()), float(st["evals"]), float(st["evals_small"]),
+            float(st["evals_gather"]), float(st["evals_wide"])]
+
+
+def valu_roofline(valu, kernel, nout, dom, dom_ms, pm_stage):
+    """The compute bound of SURVEY §8(d): included pairs x algorithmic flops per pair over
+    the dominant kernel's time, against the FP32 vector peak (157.3 TFLOPS)."""
+    pairs, evals, ev_small, ev_gather, ev_wide = valu
+    F = pair_flops(kernel, nout)
+    tflops = pairs * F / (dom_ms * 1e-3) / 1e12 if dom_ms > 0 else 0.0
+    r = {"bound": "valu", "kernel": dom, "achieved": round(tflops, 3), "peak": VALU_PEAK_TFLOPS,
+         "unit": "TFLOP/s", "frac": round(tflops / VALU_PEAK_TFLOPS, 4),
+         "included_pairs": int(pairs), "evaluated_lane_pairs": int(evals),
+         "evaluated_per_included": round(evals / pairs, 3) if pairs else None,
+         "evaluated_split": {"small_mid": int(ev_small), "gather": int(ev_gather),
+                             "wide": int(ev_wide)},
+         "flops_per_pair": F, "pairs_per_s": pairs / (dom_ms * 1e-3) if dom_ms > 0 else None,
+         "note": "pairs and flops of the whole map (all deposit kernels) over the dominant "
+                 "kernel's time: an upper bound on that kernel's rate"}
+    if pm_stage and "SQ_INSTS_VALU" in pm_stage and pairs:
+        r["valu_lane_instr_per_pair"] = round(pm_stage["SQ_INSTS_VALU"] * 64 / pairs, 3)
+        r["valu_lane_instr_source"] = "SQ_INSTS_VALU of the dominant kernel (PMC pass) x 64"
+    return r
+
+
 def output_check(out0, out1, a0, a1, ratio, world=1, gathered_ratio=False):
     """Size-independent sanity of the timed map (the parity proper is tests/): finite,
     non-negative component sums (W >= 0, m > 0), and for the mass-weighted map every pixel a
@@ -487,8 +554,9 @@ def main():
             for _ in range(nbuf)]
     pending = [None]
     it = [0]
+    last = [None]  # the last completed map's (out0, out1) as the collective returns them
 
-    def step():
+    def step(pipelined=nbuf > 1):
         maps = bufs[it[0] % nbuf]
         it[0] += 1
         o0, o1 = maps[0], (maps[1] if a1 is not None else None)
@@ -496,18 +564,20 @@ def main():
             p = project2d_sharded(u, v, h, a0, a1, image_size=(G, G), extent=ext,
                                   kernel=args.kernel, ratio=ratio, op=args.op, out0=o0,
                                   out1=o1, deterministic=args.deterministic,
-                                  async_op=nbuf > 1)
-            if nbuf > 1:
+                                  async_op=pipelined)
+            if pipelined:
                 if pending[0] is not None:
-                    pending[0].wait()  # map i - 1: stream-ordered, the host does not block
+                    last[0] = pending[0].wait()  # map i - 1: stream-ordered, no host block
                 pending[0] = p
+            else:
+                last[0] = p
             return
-        project2d(u, v, h, a0, a1, image_size=(G, G), extent=ext, kernel=args.kernel,
-                  ratio=ratio, out0=o0, out1=o1, deterministic=args.deterministic)
+        last[0] = project2d(u, v, h, a0, a1, image_size=(G, G), extent=ext, kernel=args.kernel,
+                            ratio=ratio, out0=o0, out1=o1, deterministic=args.deterministic)
 
     def drain():
         if pending[0] is not None:
-            pending[0].wait()
+            last[0] = pending[0].wait()
             pending[0] = None
 
     for _ in range(args.warmup):
@@ -536,20 +606,36 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t
-    last = bufs[(it[0] - 1) % nbuf]
-    out0, out1 = last[0], (last[1] if a1 is not None else None)
+    out0, out1 = last[0]
     prof = _lib.profile_read(local)  # timed region: the dominant kernel only
     _lib.profile(local, False)
+    # N > 1: the single-map LATENCY as well (each map's collective completed before the
+    # next map starts), beside the overlapped throughput of the timed region
+    latency_ms = None
+    if world > 1 and nbuf > 1:
+        k_lat = max(1, min(args.steps, 5))
+        dist.barrier()
+        torch.cuda.synchronize()
+        tl = time.perf_counter()
+        for _ in range(k_lat):
+            step(pipelined=False)
+            torch.cuda.synchronize()
+        dist.barrier()
+        tt = torch.tensor([time.perf_counter() - tl], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        latency_ms = float(tt.item()) / k_lat * 1e3
+        out0, out1 = last[0]
     st = stats(local)
+    valu = None
+    if dom in COMPUTE_BOUND:
+        valu = pair_work(u, v, h, G, ext, args.kernel, world, dev)
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    if world > 1 and args.op == "reduce_scatter":
-        ok = None  # the reduced map lives as row slabs returned to step(); not checked here
-    else:
-        ok = output_check(out0, out1, a0, a1, ratio, world,
-                          gathered_ratio=world > 1 and args.op == "reduce_scatter_gather")
+    # reduce_scatter: out0 / out1 are this rank's reduced row slab (ratio formed there)
+    ok = output_check(out0, out1, a0, a1, ratio, world,
+                      gathered_ratio=world > 1 and args.op == "reduce_scatter_gather")
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -569,13 +655,15 @@ def main():
     achieved = bytes_alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic = None
     traffic_src = None
+    pm_stage = None
     try:
         with open(args.pmc) as f:
             pm = json.load(f)
         # per-rank traffic: keyed on THIS rank's particle count (a profile of the shard)
         key = f"n{n_local}_g{G}_{args.kernel}_{args.h_law}_{args.map}"
         if key in pm and dom in pm[key]:
-            traffic = pm[key][dom]["hbm_bytes_per_launch"]
+            pm_stage = pm[key][dom]
+            traffic = pm_stage.get("hbm_bytes_per_launch")
             traffic_src = pm[key].get("source")
     except (OSError, ValueError, KeyError):
         pass
@@ -600,8 +688,14 @@ def main():
                    "map": args.map, "parallelism": f"zslab{world}" if world > 1 else "single",
                    "accumulation": "int64 fixed point" if args.deterministic else "fp64",
                    "collective_overlap": nbuf > 1,
-                   **({"slab_weight": args.slab_weight, "collective": args.op} if world > 1 else {})},
+                   **({"slab_weight": args.slab_weight, "collective": args.op,
+                       "partition": "Z-slab split of the generated particles before the "
+                                    "timed region (untimed, as a reader-split snapshot "
+                                    "needs none)"} if world > 1 else {})},
         "particles_per_s": pps,
+        **({"latency_ms_per_map": round(latency_ms, 4),
+            "latency_note": "one map at a time (--no-pipeline form): binning + deposit + "
+                            "collective + ratio, max over ranks"} if latency_ms else {}),
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
@@ -614,6 +708,11 @@ def main():
         "work_items": st["items"], "wide_particles": st["wide"], "large_records": st["large"],
         "output_ok": ok,
     }
+    if valu is not None:  # compute-bound regime: the VALU roofline, the HBM one beside it
+        res["roofline_hbm"] = res["roofline"]
+        res["roofline"] = valu_roofline(valu, args.kernel, nout, dom, dom_ms, pm_stage)
+        res["roofline"]["pipeline_frac"] = round(
+            valu[0] * pair_flops(args.kernel, nout) / (ms_step * 1e-3) / 1e12 / VALU_PEAK_TFLOPS, 4)
     want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
     if want_cpu:
         try:

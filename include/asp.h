@@ -117,24 +117,38 @@ int asp_project2d_f64(const double *positions, const double *h, const double *a0
                       void *stream);
 
 /*
- * The kernel_func plugin point (_projector.py:26, 86; _pixel_calculations.pyx:30-33):
- * for an arbitrary user kernel W(r, h) -- Python code that cannot run on the device --
- * the device produces the neighbour pairs and the host evaluates W on them.  For the
- * GPU tiles tile_lo <= t < tile_hi (64 x 64 pixels, t = tx * ceil(ny/64) + ty), every
- * (pixel, particle) pair create_image includes (the same exact decision as
- * asp_project2d_f64) is written at the pixel's slot range: particle[k] (index into the
- * inputs) and r2[k] = dx*dx + dy*dy in fp64 as the reference forms it (.pyx:13-14,
- * :20-30), k in [offsets[q], offsets[q+1]) for the q-th pixel of the range, pixels
- * tile by tile and (lx * 64 + ly) inside a tile (pixels outside the image: empty).
- * offsets ((tile_hi - tile_lo) * 4096 + 1 entries, non-decreasing) come from the
- * per-pixel neighbour counts (asp_project2d_f64 with ASP_KERNEL_INDICATOR and a = 1).
- * Order inside a pixel is unspecified.  positions / h / axis / extent / chunk_size as
- * asp_project2d_f64.  Host pointers unless ASP_F_DEVICE_PTRS.
+ * The kernel_func plugin point (_projector.py:26, 86; _pixel_calculations.pyx:30-33): for
+ * an arbitrary user kernel W(r, h) -- Python code that cannot run on the device -- the
+ * device produces the neighbour pairs and the host evaluates W on them, in a SESSION that
+ * stages and bins the particles once per map:
+ *
+ *   asp_pairs_begin: stage positions (n, 3) / h (axis, extent, chunk_size as
+ *     asp_project2d_f64), bin them and count every GPU tile's pairs: tile_pairs[t] for the
+ *     ceil(nx/64) * ceil(ny/64) tiles t = tx * ceil(ny/64) + ty (host array).  *session
+ *     receives the handle (NULL on error).  With ASP_F_DEVICE_PTRS positions / h are device
+ *     arrays that must stay alive until asp_pairs_end, and the emit outputs are device
+ *     pointers too.
+ *   asp_pairs_emit: for the tiles tile_lo <= t < tile_hi, every (pixel, particle) pair
+ *     create_image includes (the exact decision of asp_project2d_f64): particle[k] (index
+ *     into the inputs) and r2[k] = dx*dx + dy*dy in fp64 as the reference forms it
+ *     (.pyx:13-14, :20-30), k in [offsets[q], offsets[q+1]) for the q-th pixel of the
+ *     range -- pixels tile by tile, (lx * 64 + ly) inside a tile, pixels outside the image
+ *     empty; offsets ((tile_hi - tile_lo) * 4096 + 1 entries) start at 0 and end at the
+ *     sum of tile_pairs over the range, the size particle / r2 must have.  Order inside a
+ *     pixel unspecified.  The session keeps the binned records resident between emits
+ *     (images of more than 4096 tiles: per window of tile rows, re-binned when a range
+ *     moves to the next window).
+ *   asp_pairs_end: release the session (NULL is a no-op).
+ * A session is used by one thread at a time; it owns its buffers, so other calls on the
+ * device may run between its emits.
  */
-int asp_pairs_f64(const double *positions, const double *h, int64_t n, int32_t axis,
-                  double u_min, double u_max, double v_min, double v_max, int32_t nx, int32_t ny,
-                  int32_t chunk_size, int32_t tile_lo, int32_t tile_hi, const int64_t *offsets,
-                  int32_t *particle, double *r2, int32_t flags, int32_t device, void *stream);
+int asp_pairs_begin(const double *positions, const double *h, int64_t n, int32_t axis,
+                    double u_min, double u_max, double v_min, double v_max, int32_t nx,
+                    int32_t ny, int32_t chunk_size, int32_t flags, int32_t device, void *stream,
+                    int64_t *tile_pairs, void **session);
+int asp_pairs_emit(void *session, int32_t tile_lo, int32_t tile_hi, int64_t *offsets,
+                   int32_t *particle, double *r2);
+int asp_pairs_end(void *session);
 
 /*
  * 3-D voxel cube (build-defined; SURVEY.md §8(a) "512^3 cube" -- no reference
@@ -306,7 +320,11 @@ int asp_table_interp(const double *table, int32_t ndim, const int32_t *shape,
  * stats[0] = records binned (particle x GPU-tile insertions), stats[1] = work items,
  * stats[2] = wide particles, stats[3] = GPU tile edge (pixels), stats[4] = GPU tiles,
  * stats[5] = records per work item, stats[6] = split tiles, stats[7] = partial slabs,
- * stats[8] = records in the large (gathered) stream.
+ * stats[8] = records in the large (gathered) stream; with the environment variable
+ * ASP_COUNT_EVALS set (diagnostic: one extra kernel, a host sync), the (pixel, particle)
+ * lane-slots the deposit kernels spend: stats[9] total = stats[10] small / mid-size stream
+ * + stats[11] gathered large stream + stats[12] wide particles (else 0).  Images of more
+ * than 4096 tiles and batched calls: the sums over all passes.
  */
 int asp_last_stats(int32_t device, int64_t *stats, int32_t nstats);
 

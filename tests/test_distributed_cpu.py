@@ -72,11 +72,27 @@ def _worker(rank, world, port, q):
                                        image_size=(G, G), extent=EXT, chunk_size=16,
                                        kernel="cubic", op=op, projector=_oracle_projector)
             res[op] = (o0.numpy().copy(), o1.numpy().copy())
-        o0, _ = project2d_sharded(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3],
-                                  image_size=(G, G), extent=EXT, chunk_size=16, kernel="cubic",
-                                  op="reduce_scatter_gather", projector=_oracle_projector,
-                                  out0=torch.empty((G, G)), out1=torch.empty((G, G)))
+        # reduce-scatter + ONE all-gather: the ratio map of two components ...
+        o0, o1 = project2d_sharded(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3],
+                                   image_size=(G, G), extent=EXT, chunk_size=16, kernel="cubic",
+                                   op="reduce_scatter_gather", ratio=True,
+                                   projector=_oracle_projector, out0=torch.empty((G, G)),
+                                   out1=torch.empty((G, G)))
+        res["rsg_ratio"] = o0.numpy().copy()
+        res["rsg_o1"] = o1
+        # ... or a single map
+        o0, o1 = project2d_sharded(sl[0], sl[1], sl[2], sl[3] * sl[4], None,
+                                   image_size=(G, G), extent=EXT, chunk_size=16, kernel="cubic",
+                                   op="reduce_scatter_gather", projector=_oracle_projector,
+                                   out0=torch.empty((G, G)))
         res["rsg"] = o0.numpy().copy()
+        try:  # two components but one gather: refused, not silently dropped
+            project2d_sharded(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3], image_size=(G, G),
+                              extent=EXT, chunk_size=16, kernel="cubic",
+                              op="reduce_scatter_gather", projector=_oracle_projector)
+            res["rsg_two_maps"] = "accepted"
+        except ValueError:
+            res["rsg_two_maps"] = "refused"
         maps = torch.empty((2, G, G))  # adjacent maps: one fused collective
         for op in ("reduce", "allreduce"):
             o0, o1 = project2d_sharded(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3],
@@ -143,6 +159,10 @@ def test_zslab_sharded_sum_world2():
         np.testing.assert_allclose(out[r]["reduce_scatter"][0], full0[rows], atol=tol, rtol=0)
         # reduce-scatter, then the one map all-gathered: the full map on every rank
         np.testing.assert_allclose(out[r]["rsg"], full0, atol=tol, rtol=0)
+        cov = full1 > 1e-3 * full1.max()
+        np.testing.assert_allclose(out[r]["rsg_ratio"][cov], (full0 / np.where(cov, full1, 1))[cov],
+                                   rtol=1e-4)
+        assert out[r]["rsg_o1"] is None and out[r]["rsg_two_maps"] == "refused"
     # the slabs really are partial maps: neither rank alone holds the full map
     assert not np.allclose(out[1]["reduce"][0], full0, atol=tol)
 

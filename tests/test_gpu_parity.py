@@ -535,3 +535,53 @@ def test_plugin_matches_native_kernels(gpu):
     r1 = create_weighted_image(pos, h, A, T, size, cs, 2, *ext, kernel_func=cubic)
     r2 = create_weighted_image(pos, h, A, T, size, cs, 2, *ext, kernel_func=quartic_spline_kernel)
     np.testing.assert_allclose(r1, r2, rtol=2e-5)
+
+
+def test_plugin_per_pixel_mode_is_the_reference(gpu):
+    """kernel_func_mode="per_pixel": one call per pixel in the reference's chunk order, on
+    the pixel's pairs in particle order (empty arrays included, S15), summed by np.sum as
+    .pyx:34 -- G6 (the reference's own output for this callable) reproduced BIT FOR BIT."""
+    from asp_amd.tools.projections import create_image
+    pos, h, A, size, cs, ext, _ = g3()
+    ref = golden("g6_wendland_c2.npz")["img"]
+    seen = []
+
+    def kern(r, hh):
+        seen.append(r.size)
+        return wendland_c2_numpy(r, hh)
+
+    img = create_image(pos, h, A, size, cs, 2, *ext, kernel_func=kern,
+                       kernel_func_mode="per_pixel")
+    assert len(seen) == size[0] * size[1]  # every pixel, empty ones too
+    assert 0 in seen
+    np.testing.assert_array_equal(img, ref)
+
+
+def test_plugin_bins_once_many_batches(gpu, monkeypatch):
+    """The plug-in session stages and bins once and emits >= 4 tile-range batches from the
+    resident records; deterministic=True (pairs in particle order per pixel) makes the map
+    bitwise reproducible and equal to the per-batch-free result within rounding."""
+    from asp_amd.tools.projections import _plugin, create_image
+    pos, h, A, size, cs, ext, _ = g3()
+    ref = golden("g6_wendland_c2.npz")["img"]
+    calls = []
+    begins = []
+    real = _plugin._Session.__init__
+
+    def counting_init(self, *a, **k):
+        begins.append(1)
+        real(self, *a, **k)
+
+    monkeypatch.setattr(_plugin._Session, "__init__", counting_init)
+    monkeypatch.setattr(_plugin, "MAX_PAIRS", 1 << 18)
+
+    def kern(r, hh):
+        calls.append(r.size)
+        return wendland_c2_numpy(r, hh)
+
+    a = create_image(pos, h, A, size, cs, 2, *ext, kernel_func=kern, deterministic=True)
+    assert len(begins) == 1 and len(calls) >= 4
+    b = create_image(pos, h, A[::-1].copy()[::-1], size, cs, 2, *ext, kernel_func=kern,
+                     deterministic=True)
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_allclose(a, ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())

@@ -80,11 +80,15 @@ def main():
         stage = {}
         for k, row in out.items():
             s = STAGE_OF.get(k.split("<")[0])
-            # the first (largest total time) kernel of a stage: the steady-state launches,
-            # not the placement trials' probe instantiation (k_scatter<..., 1>)
+            # the placement trials' probe instantiation (k_scatter<..., 1>, last template
+            # argument PROBE = 1) is not the steady state: never the stage's record
+            if k.startswith("k_scatter<") and k.rstrip(">").split(",")[-1].strip() == "1":
+                continue
+            # the first (largest total time) kernel of a stage
             if s and s not in stage and "hbm_bytes_per_launch" in row:
                 stage[s] = {"hbm_bytes_per_launch": row["hbm_bytes_per_launch"],
                             "avg_us": row["avg_us"], "kernel": k}
+                stage[s].update({c: v for c, v in row.items() if c.startswith("SQ_")})
         stage["source"] = a.source
         db[a.key] = stage
         json.dump(db, open(a.json, "w"), indent=1)
