@@ -81,6 +81,8 @@ struct Grid3 {
     double ipx, ipy, ipz;    // reciprocals (candidate boxes only)
     int nx, ny, nz;
     int k_lo, nzl;           // output planes [k_lo, k_lo + nzl)
+    int i_lo, nxl;           // this pass's window of x planes [i_lo, i_lo + nxl) (i_lo a
+                             // multiple of kBX; the whole slab unless it has > kMaxBricks)
     int nbx, nby, nbz, nb;   // bricks over the output slab
     int lane_cols;           // deposit: boxes up to this many columns lane-per-record
 };
@@ -109,7 +111,7 @@ __device__ __forceinline__ bool footprint3(const Grid3& g, float x, float y, flo
     double rad = fabs(2.0 * (double)h);
     if (!(rad > 0.0) || !__builtin_isfinite(rad)) return false;  // h == 0: r2 < 0 never holds
     if (!__builtin_isfinite(x) || !__builtin_isfinite(y) || !__builtin_isfinite(z)) return false;
-    return axis_cells(x, rad, g.x_min, g.ipx, 0, g.nx - 1, b.i0, b.i1) &&
+    return axis_cells(x, rad, g.x_min, g.ipx, g.i_lo, g.i_lo + g.nxl - 1, b.i0, b.i1) &&
            axis_cells(y, rad, g.y_min, g.ipy, 0, g.ny - 1, b.j0, b.j1) &&
            axis_cells(z, rad, g.z_min, g.ipz, g.k_lo, g.k_lo + g.nzl - 1, b.k0, b.k1);
 }
@@ -146,7 +148,8 @@ __global__ __launch_bounds__(k3Block) void k3_count(const float* __restrict__ x,
         load3(x, y, z, h, base + k3Block + threadIdx.x, p1, nx_, ny_, nz_, nh_);
         Box3 b;
         if (footprint3(g, cx, cy, cz, ch, b)) {
-            int bi0 = b.i0 >> kBXs, bi1 = b.i1 >> kBXs, bj0 = b.j0 >> kBYs, bj1 = b.j1 >> kBYs;
+            int bi0 = (b.i0 - g.i_lo) >> kBXs, bi1 = (b.i1 - g.i_lo) >> kBXs;
+            int bj0 = b.j0 >> kBYs, bj1 = b.j1 >> kBYs;
             int bk0 = (b.k0 - g.k_lo) >> kBZs, bk1 = (b.k1 - g.k_lo) >> kBZs;
             for (int bi = bi0; bi <= bi1; ++bi)
                 for (int bj = bj0; bj <= bj1; ++bj)
@@ -189,7 +192,8 @@ __global__ __launch_bounds__(k3Block) void k3_scatter(
         Box3 b;
         if (footprint3(g, cx, cy, cz, ch, b)) {
             float4 r0 = make_float4(cx, cy, cz, ch), r1 = make_float4(ca, 0.0f, 0.0f, 0.0f);
-            int bi0 = b.i0 >> kBXs, bi1 = b.i1 >> kBXs, bj0 = b.j0 >> kBYs, bj1 = b.j1 >> kBYs;
+            int bi0 = (b.i0 - g.i_lo) >> kBXs, bi1 = (b.i1 - g.i_lo) >> kBXs;
+            int bj0 = b.j0 >> kBYs, bj1 = b.j1 >> kBYs;
             int bk0 = (b.k0 - g.k_lo) >> kBZs, bk1 = (b.k1 - g.k_lo) >> kBZs;
             for (int bi = bi0; bi <= bi1; ++bi)
                 for (int bj = bj0; bj <= bj1; ++bj)
@@ -322,12 +326,12 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
     int bi = it.tile / (g.nby * g.nbz);
     int rem = it.tile - bi * (g.nby * g.nbz);
     int bj = rem / g.nbz, bk = rem - (rem / g.nbz) * g.nbz;
-    int I0 = bi * kBX, J0 = bj * kBY, K0 = g.k_lo + bk * kBZ;
-    int TW = min(kBX, g.nx - I0), TH = min(kBY, g.ny - J0), TD = min(kBZ, g.k_lo + g.nzl - K0);
+    int I0 = g.i_lo + bi * kBX, J0 = bj * kBY, K0 = g.k_lo + bk * kBZ;
+    int TW = min(kBX, g.i_lo + g.nxl - I0), TH = min(kBY, g.ny - J0), TD = min(kBZ, g.k_lo + g.nzl - K0);
     auto out_index = [&](int v) -> long long {
         int li = v >> (kBYs + kBZs), lj = (v >> kBZs) & (kBY - 1), lk = v & (kBZ - 1);
         if (li >= TW || lj >= TH || lk >= TD) return -1;
-        return ((long long)(I0 + li) * g.ny + (J0 + lj)) * g.nzl + (K0 - g.k_lo + lk);
+        return ((long long)(I0 - g.i_lo + li) * g.ny + (J0 + lj)) * g.nzl + (K0 - g.k_lo + lk);
     };
     if (it.count == 0) {  // empty brick
         if (accumulate) return;
@@ -514,14 +518,14 @@ __global__ __launch_bounds__(k3Block) void k3_merge(Grid3 g, const Merge* __rest
     int bi = m.tile / (g.nby * g.nbz);
     int rem = m.tile - bi * (g.nby * g.nbz);
     int bj = rem / g.nbz, bk = rem - (rem / g.nbz) * g.nbz;
-    int I0 = bi * kBX, J0 = bj * kBY, K0 = g.k_lo + bk * kBZ;
-    int TW = min(kBX, g.nx - I0), TH = min(kBY, g.ny - J0), TD = min(kBZ, g.k_lo + g.nzl - K0);
+    int I0 = g.i_lo + bi * kBX, J0 = bj * kBY, K0 = g.k_lo + bk * kBZ;
+    int TW = min(kBX, g.i_lo + g.nxl - I0), TH = min(kBY, g.ny - J0), TD = min(kBZ, g.k_lo + g.nzl - K0);
     for (int v = threadIdx.x; v < kBrickVox; v += k3Block) {
         int li = v >> (kBYs + kBZs), lj = (v >> kBZs) & (kBY - 1), lk = v & (kBZ - 1);
         if (li >= TW || lj >= TH || lk >= TD) continue;
         double s = 0.0;
         for (int j = 0; j < m.nslab; ++j) s += slabs[(long long)(m.slab0 + j) * kBrickVox + v];
-        long long o = ((long long)(I0 + li) * g.ny + (J0 + lj)) * g.nzl + (K0 - g.k_lo + lk);
+        long long o = ((long long)(I0 - g.i_lo + li) * g.ny + (J0 + lj)) * g.nzl + (K0 - g.k_lo + lk);
         float val = (float)s;
         out[o] = accumulate ? out[o] + val : val;
     }
@@ -585,15 +589,122 @@ static bool make_grid3(const double* ext, int nx, int ny, int nz, int k_lo, int 
     g.nz = nz;
     g.k_lo = k_lo;
     g.nzl = k_hi - k_lo;
+    g.i_lo = 0;
+    g.nxl = nx;
     g.nbx = (nx + kBX - 1) / kBX;
     g.nby = (ny + kBY - 1) / kBY;
     g.nbz = (g.nzl + kBZ - 1) / kBZ;
     long long nb = (long long)g.nbx * g.nby * g.nbz;
-    g.nb = nb > kMaxBricks ? -1 : (int)nb;
+    // more bricks than one pass holds: windows of whole brick columns in x (window3); -1:
+    // not even one brick column fits
+    g.nb = (long long)g.nby * g.nbz > kMaxBricks ? -1 : (int)std::min<long long>(nb, 0x7fffffff);
     g.lane_cols = kLaneCols;
     if (const char* e = getenv("ASP_CUBE_LANE_COLS")) g.lane_cols = std::max(0, atoi(e));
 
     return true;
+}
+
+constexpr int kRetSplit3 = 1;  // internal: >= 2^31 records in one pass, nothing written
+
+// One window (w.i_lo, w.nxl; <= kMaxBricks bricks) of the cube on stream st: count,
+// scans, scatter (placement trials on a fresh record buffer), deposit, merge.
+static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float* dy,
+                     const float* dz, const float* dh, const float* da, long long n, int kid,
+                     int acc, float* dout, hipStream_t st, long long* agg) {
+    long long n_recs = 0;
+    int n_items = 0, n_merges = 0, n_slabs = 0;
+    ASP_TRY(ensure_morton3(ws, g, st));
+    long long nblk = std::min<long long>(512, std::max<long long>(1, (n + 8191) / 8192));
+    long long per_block = (n + nblk - 1) / nblk;
+    nblk = (n + per_block - 1) / per_block;
+    ASP_TRY(ensure(ws.hist, (size_t)nblk * g.nb * sizeof(int)));
+    ASP_TRY(ensure(ws.tile_total, (size_t)g.nb * sizeof(int)));
+    ASP_TRY(ensure(ws.tile_start, (size_t)g.nb * sizeof(long long)));
+    ASP_TRY(ensure(ws.items, (size_t)(g.nb + kTargetItems + 16) * sizeof(Item)));
+    ASP_TRY(ensure(ws.merges, (size_t)(g.nb + 16) * sizeof(Merge)));
+    ASP_TRY(ensure(ws.counters, cNum * sizeof(int)));
+    if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, kMarks * cNum * sizeof(int)));
+    int* dc = (int*)ws.counters.p;
+    ASP_HIP(hipMemsetAsync(dc, 0, cNum * sizeof(int), st));
+    const size_t lds_bins = (size_t)g.nb * sizeof(int);
+    {
+        StageMark m(ws, kS3Count, st);
+        hipLaunchKernelGGL(k3_count, dim3((unsigned)nblk), dim3(k3Block), lds_bins, st, dx, dy,
+                           dz, dh, n, per_block, g, (int*)ws.hist.p);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    {
+        StageMark m(ws, kS3Colscan, st);
+        hipLaunchKernelGGL(k_colscan, dim3((g.nb + 63) / 64), dim3(kColscanBlock), 0, st,
+                           (int*)ws.hist.p, (int)nblk, g.nb, (int*)ws.tile_total.p, (int)nblk);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    {
+        StageMark m(ws, kS3Tilescan, st);
+        if (g.nb <= 4 * kScanThreads)
+            hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
+                           (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1,
+                           (long long*)ws.tile_start.p, (Item*)ws.items.p,
+                           (Merge*)ws.merges.p, dc);
+        else
+            hipLaunchKernelGGL(k_tilescan<kScanPer>, dim3(1), dim3(kScanThreads), 0, st,
+                           (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1,
+                           (long long*)ws.tile_start.p, (Item*)ws.items.p,
+                           (Merge*)ws.merges.p, dc);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, cNum * sizeof(int), hipMemcpyDeviceToHost, st));
+    ASP_HIP(hipStreamSynchronize(st));
+    n_items = ws.h_counters[cItems];
+    n_recs = ws.h_counters[cRecs];
+    n_slabs = ws.h_counters[cSlabs];
+    n_merges = ws.h_counters[cMerges];
+    long long rec_limit = 0x7fffffffLL;  // 32-bit record cursors (ASP_MAX_RECORDS: tests)
+    if (const char* e = getenv("ASP_MAX_RECORDS")) rec_limit = std::max(1LL, atoll(e));
+    if (n_recs >= rec_limit) return kRetSplit3;  // nothing written: the caller splits
+    const void* recs_before = ws.recs.p;
+    ASP_TRY(ensure(ws.recs, (size_t)n_recs * 2 * sizeof(float4)));
+    ASP_TRY(ensure(ws.slabs, (size_t)n_slabs * kBrickVox * sizeof(double)));
+    auto scatter = [&](bool probe) -> int {
+        StageMark m(ws, kS3Scatter, st);
+        hipLaunchKernelGGL(probe ? k3_scatter<1> : k3_scatter<0>, dim3((unsigned)nblk),
+                           dim3(k3Block), lds_bins, st, dx,
+                           dy, dz, dh, da, n, per_block, g, (const int*)ws.hist.p,
+                           (const long long*)ws.tile_start.p, (float4*)ws.recs.p);
+        ASP_LAUNCHED();
+        m.done();
+        return ASP_OK;
+    };
+    bool placed = false;  // a fresh record buffer: placement trials (asp_host.hpp)
+    if (ws.recs.p != recs_before)
+        ASP_TRY(place_records(ws, (size_t)n_recs * 2 * sizeof(float4), st,
+                              [&]() { return scatter(true); }, placed));
+    if (!placed) ASP_TRY(scatter(false));
+    {
+        StageMark m(ws, kS3Deposit, st);
+        size_t lds = (size_t)kBrickLds * sizeof(double) + (kBX + kBY + kBZ) * sizeof(double);
+        auto kern = kid == 0 ? k3_deposit<0> : kid == 1 ? k3_deposit<1> : k3_deposit<2>;
+        hipLaunchKernelGGL(kern, dim3(n_items), dim3(k3Block), lds, st, g,
+                           (const float4*)ws.recs.p, (const Item*)ws.items.p,
+                           (double*)ws.slabs.p, dout, acc);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    if (n_merges > 0) {
+        StageMark m(ws, kS3Merge, st);
+        hipLaunchKernelGGL(k3_merge, dim3(n_merges), dim3(k3Block), 0, st, g,
+                           (const Merge*)ws.merges.p, (const double*)ws.slabs.p, dout, acc);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    agg[0] += n_recs;
+    agg[1] += n_items;
+    agg[2] += n_merges;
+    agg[3] += n_slabs;
+    return ASP_OK;
 }
 
 static int project3d(const float* x, const float* y, const float* z, const float* h,
@@ -607,15 +718,14 @@ static int project3d(const float* x, const float* y, const float* z, const float
         return fail(ASP_ERR_UNSUPPORTED, "asp_project3d supports ASP_F_DEVICE_PTRS and "
                                          "ASP_F_ACCUMULATE only");
     if (n > 0 && (!x || !y || !z || !h || !a)) return fail(ASP_ERR_INVALID, "NULL particle array");
-    if (n > 0x7fffffffLL) return fail(ASP_ERR_UNSUPPORTED, "n >= 2^31 particles per call");
     Grid3 g;
     if (!make_grid3(ext, nx, ny, nz, k_lo, k_hi, g))
         return fail(ASP_ERR_INVALID,
                     "invalid cube: need nx, ny, nz >= 1, 0 <= k_lo < k_hi <= nz and finite "
                     "max > min on every axis");
     if (g.nb < 0)
-        return fail(ASP_ERR_UNSUPPORTED, "cube slab too large for one call (more than 16384 "
-                                         "16x16x32 bricks): split the planes [k_lo, k_hi)");
+        return fail(ASP_ERR_UNSUPPORTED, "cube slab too wide: ny x (k_hi - k_lo) spans more than "
+                                         "16384 16x32 brick columns; split the planes [k_lo, k_hi)");
     if (device < 0 || device >= 64) return fail(ASP_ERR_INVALID, "bad device");
     int ndev = 0;
     ASP_HIP(hipGetDeviceCount(&ndev));
@@ -650,8 +760,7 @@ static int project3d(const float* x, const float* y, const float* z, const float
             ASP_HIP(hipMemcpyAsync(dout, out, nvox * sizeof(float), hipMemcpyHostToDevice, st));
     }
     if (ws.prof) ASP_TRY(prof_next(ws));
-    long long n_recs = 0;
-    int n_items = 0, n_merges = 0, n_slabs = 0;
+    long long agg[4] = {0, 0, 0, 0};  // records, items, merges, slabs over the windows
     if (n == 0) {
         if (!acc) {
             StageMark m(ws, kSMemset, st);
@@ -659,105 +768,53 @@ static int project3d(const float* x, const float* y, const float* z, const float
             m.done();
         }
     } else {
-        ASP_TRY(ensure_morton3(ws, g, st));
-        long long nblk = std::min<long long>(512, std::max<long long>(1, (n + 8191) / 8192));
-        long long per_block = (n + nblk - 1) / nblk;
-        nblk = (n + per_block - 1) / per_block;
-        ASP_TRY(ensure(ws.hist, (size_t)nblk * g.nb * sizeof(int)));
-        ASP_TRY(ensure(ws.tile_total, (size_t)g.nb * sizeof(int)));
-        ASP_TRY(ensure(ws.tile_start, (size_t)g.nb * sizeof(long long)));
-        ASP_TRY(ensure(ws.items, (size_t)(g.nb + kTargetItems + 16) * sizeof(Item)));
-        ASP_TRY(ensure(ws.merges, (size_t)(g.nb + 16) * sizeof(Merge)));
-        ASP_TRY(ensure(ws.counters, cNum * sizeof(int)));
-        if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, kMarks * cNum * sizeof(int)));
-        int* dc = (int*)ws.counters.p;
-        ASP_HIP(hipMemsetAsync(dc, 0, cNum * sizeof(int), st));
-        const size_t lds_bins = (size_t)g.nb * sizeof(int);
-        {
-            StageMark m(ws, kS3Count, st);
-            hipLaunchKernelGGL(k3_count, dim3((unsigned)nblk), dim3(k3Block), lds_bins, st, dx, dy,
-                               dz, dh, n, per_block, g, (int*)ws.hist.p);
-            ASP_LAUNCHED();
-            m.done();
-        }
-        {
-            StageMark m(ws, kS3Colscan, st);
-            hipLaunchKernelGGL(k_colscan, dim3((g.nb + 63) / 64), dim3(kColscanBlock), 0, st,
-                               (int*)ws.hist.p, (int)nblk, g.nb, (int*)ws.tile_total.p, (int)nblk);
-            ASP_LAUNCHED();
-            m.done();
-        }
-        {
-            StageMark m(ws, kS3Tilescan, st);
-            if (g.nb <= 4 * kScanThreads)
-                hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
-                               (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1,
-                               (long long*)ws.tile_start.p, (Item*)ws.items.p,
-                               (Merge*)ws.merges.p, dc);
-            else
-                hipLaunchKernelGGL(k_tilescan<kScanPer>, dim3(1), dim3(kScanThreads), 0, st,
-                               (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1,
-                               (long long*)ws.tile_start.p, (Item*)ws.items.p,
-                               (Merge*)ws.merges.p, dc);
-            ASP_LAUNCHED();
-            m.done();
-        }
-        ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, cNum * sizeof(int), hipMemcpyDeviceToHost, st));
-        ASP_HIP(hipStreamSynchronize(st));
-        n_items = ws.h_counters[cItems];
-        n_recs = ws.h_counters[cRecs];
-        n_slabs = ws.h_counters[cSlabs];
-        n_merges = ws.h_counters[cMerges];
-        if (n_recs >= 0x7fffffffLL)
-            return fail(ASP_ERR_UNSUPPORTED, "more than 2^31 particle-brick records");
-        const void* recs_before = ws.recs.p;
-        ASP_TRY(ensure(ws.recs, (size_t)n_recs * 2 * sizeof(float4)));
-        ASP_TRY(ensure(ws.slabs, (size_t)n_slabs * kBrickVox * sizeof(double)));
-        auto scatter = [&](bool probe) -> int {
-            StageMark m(ws, kS3Scatter, st);
-            hipLaunchKernelGGL(probe ? k3_scatter<1> : k3_scatter<0>, dim3((unsigned)nblk),
-                               dim3(k3Block), lds_bins, st, dx,
-                               dy, dz, dh, da, n, per_block, g, (const int*)ws.hist.p,
-                               (const long long*)ws.tile_start.p, (float4*)ws.recs.p);
-            ASP_LAUNCHED();
-            m.done();
-            return ASP_OK;
-        };
-        bool placed = false;  // a fresh record buffer: placement trials (asp_host.hpp)
-        if (ws.recs.p != recs_before)
-            ASP_TRY(place_records(ws, (size_t)n_recs * 2 * sizeof(float4), st,
-                                  [&]() { return scatter(true); }, placed));
-        if (!placed) ASP_TRY(scatter(false));
-        {
-            StageMark m(ws, kS3Deposit, st);
-            size_t lds = (size_t)kBrickLds * sizeof(double) + (kBX + kBY + kBZ) * sizeof(double);
-            auto kern = kid == 0 ? k3_deposit<0> : kid == 1 ? k3_deposit<1> : k3_deposit<2>;
-            hipLaunchKernelGGL(kern, dim3(n_items), dim3(k3Block), lds, st, g,
-                               (const float4*)ws.recs.p, (const Item*)ws.items.p,
-                               (double*)ws.slabs.p, dout, acc);
-            ASP_LAUNCHED();
-            m.done();
-        }
-        if (n_merges > 0) {
-            StageMark m(ws, kS3Merge, st);
-            hipLaunchKernelGGL(k3_merge, dim3(n_merges), dim3(k3Block), 0, st, g,
-                               (const Merge*)ws.merges.p, (const double*)ws.slabs.p, dout, acc);
-            ASP_LAUNCHED();
-            m.done();
+        // windows of whole brick columns in x, each <= kMaxBricks bricks: every window one
+        // pass over all particles with the footprints clipped to it; its slab of the output
+        // is contiguous ((nx, ny, nzl) C-order, x slowest)
+        const int wb = std::max(1, kMaxBricks / (g.nby * g.nbz));
+        for (int bx0 = 0; bx0 < g.nbx; bx0 += wb) {
+            Grid3 w = g;
+            w.i_lo = bx0 * kBX;
+            w.nxl = std::min((bx0 + wb) * kBX, nx) - w.i_lo;
+            w.nbx = std::min(wb, g.nbx - bx0);
+            w.nb = w.nbx * g.nby * g.nbz;
+            // particle batches of < 2^31 (ASP_MAX_BATCH), halved while a pass would reach
+            // 2^31 records; batches after the first accumulate
+            long long B = 1LL << 30;
+            if (const char* e = getenv("ASP_MAX_BATCH")) B = std::max(1LL, atoll(e));
+            std::vector<std::pair<long long, long long>> todo;
+            for (long long a = ((n - 1) / B) * B; a >= 0; a -= B) todo.push_back({a, std::min(n, a + B)});
+            int passes = 0;
+            while (!todo.empty()) {
+                const auto [a, b] = todo.back();
+                todo.pop_back();
+                const int rc = cube_pass(ws, w, dx + a, dy + a, dz + a, dh + a, da + a, b - a,
+                                         kid, passes ? 1 : acc,
+                                         dout + (long long)w.i_lo * ny * g.nzl, st, agg);
+                if (rc == kRetSplit3) {
+                    if (b - a < 2)
+                        return fail(ASP_ERR_UNSUPPORTED, "one particle makes >= 2^31 records");
+                    todo.push_back({a + (b - a) / 2, b});
+                    todo.push_back({a, a + (b - a) / 2});
+                    continue;
+                }
+                ASP_TRY(rc);
+                ++passes;
+            }
         }
     }
     if (!dev) {
         ASP_HIP(hipMemcpyAsync(out, dout, nvox * sizeof(float), hipMemcpyDeviceToHost, st));
         ASP_HIP(hipStreamSynchronize(st));
     }
-    ws.stats[0] = n_recs;
-    ws.stats[1] = n_items;
+    ws.stats[0] = agg[0];
+    ws.stats[1] = agg[1];
     ws.stats[2] = 0;
     ws.stats[3] = kBrickVox;
-    ws.stats[4] = g.nb;
+    ws.stats[4] = (long long)g.nbx * g.nby * g.nbz;
     ws.stats[5] = n > 0 ? ws.h_counters[cChunk] : 0;
-    ws.stats[6] = n_merges;
-    ws.stats[7] = n_slabs;
+    ws.stats[6] = agg[2];
+    ws.stats[7] = agg[3];
     ws.stats[8] = n > 0 ? 1 : 0;
     return ws_end_.finish();
 }

@@ -103,8 +103,8 @@ def test_cube_edge_cases(gpu, oracle):
     assert_map_close(g, r)
     with pytest.raises(ValueError):
         create_cube(pos, [0.1], [1.0], size, 1.0, -1.0, *EXT[2:])
-    with pytest.raises(NotImplementedError):  # > 16384 bricks in one call
-        create_cube(pos, [0.1], [1.0], (4096, 4096, 8), *EXT)
+    with pytest.raises(NotImplementedError):  # one brick column of > 16384 bricks
+        create_cube(pos, [0.1], [1.0], (16, 8192, 2048), *EXT)
 
 
 def test_cube_device_api_accumulate(gpu):
@@ -145,3 +145,37 @@ def test_cube_record_placement_trials(gpu, oracle, monkeypatch):
     d = create_cube(pos, h, m, size, *EXT, kernel_func=wendland_c2_kernel)
     assert_map_close(d, oracle.project3d(x, y, z, h, m, size, EXT, kernel="wendland_c2"))
     _lib.check(_lib.lib().asp_release(0))
+
+
+def test_cube_x_windows_beyond_16384_bricks(gpu, oracle):
+    """A 640 x 512 x 512 cube (20480 bricks): two x windows of whole brick columns, each a
+    pass over all particles; counts bit-exact and density within the bar across the seam."""
+    from asp_amd.tools.projections import create_cube, indicator_kernel
+    size = (640, 512, 512)
+    x, y, z, h, m = _plummer(150_000, 12, size)
+    pos = np.stack([x, y, z], 1)
+    ext = (-3.0, 3.0, -2.4, 2.4, -2.4, 2.4)
+    ones = np.ones_like(h)
+    g = create_cube(pos, h, ones, size, *ext, kernel_func=indicator_kernel)
+    r = oracle.project3d(x, y, z, h, ones, size, ext, kernel="indicator")
+    assert np.array_equal(g, r), f"{np.count_nonzero(g != r)} voxels differ"
+    seam = 16 * (16384 // (32 * 16))  # first x plane of the second window
+    assert r[seam - 1].sum() > 0 and r[seam].sum() > 0
+    del g, r
+    d = create_cube(pos, h, m, size, *ext)
+    assert_map_close(d, oracle.project3d(x, y, z, h, m, size, ext))
+
+
+@pytest.mark.parametrize("knob", [("ASP_MAX_BATCH", "7000"), ("ASP_MAX_RECORDS", "9000")])
+def test_cube_particle_batches(gpu, oracle, monkeypatch, knob):
+    from asp_amd.tools.projections import create_cube, indicator_kernel
+    size = (40, 48, 64)
+    x, y, z, h, m = _plummer(30000, 13, size)
+    pos = np.stack([x, y, z], 1)
+    monkeypatch.setenv(*knob)
+    ones = np.ones_like(h)
+    g = create_cube(pos, h, ones, size, *EXT, kernel_func=indicator_kernel)
+    d = create_cube(pos, h, m, size, *EXT)
+    monkeypatch.delenv(knob[0])
+    assert np.array_equal(g, oracle.project3d(x, y, z, h, ones, size, EXT, kernel="indicator"))
+    assert_map_close(d, oracle.project3d(x, y, z, h, m, size, EXT))

@@ -552,8 +552,7 @@ def test_plugin_per_pixel_mode_is_the_reference(gpu):
 
     img = create_image(pos, h, A, size, cs, 2, *ext, kernel_func=kern,
                        kernel_func_mode="per_pixel")
-    assert len(seen) == size[0] * size[1]  # every pixel, empty ones too
-    assert 0 in seen
+    assert len(seen) == size[0] * size[1]  # every pixel (empty ones too: S15)
     np.testing.assert_array_equal(img, ref)
 
 
