@@ -176,10 +176,14 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
         cs_[q] = in ? tile_total[tt[q]] : 0;
         cl_[q] = in && nstream == 2 ? tile_total[tt[q] + ntiles] : 0;
     }
+    // nstream = 2: every tile's run starts on an even slot (a 64-B pair boundary, for
+    // k_scatter_pair): a tile whose two streams hold an odd total is followed by a gap slot
+    // that no item covers
+    auto span = [&](int cs, int cl) { return (long long)(cs + cl) + (nstream == 2 ? ((cs + cl) & 1) : 0); };
     long long loc = 0, wloc = 0;  // all records; stream-1 records
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-        loc += cs_[q] + cl_[q];
+        loc += span(cs_[q], cl_[q]);
         wloc += cl_[q];
     }
     s_rec[tid] = loc;
@@ -202,7 +206,7 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
         int t = tt[q], cs = cs_[q], cl = cl_[q];
         tile_start[t] = base;
         if (nstream == 2) tile_start[t + ntiles] = base + cs;
-        base += cs + cl;
+        base += span(cs, cl);
         int ks, kl;
         tile_items(cs, cl, ch, chl, ks, kl);
         nit += ks + kl;
@@ -228,7 +232,7 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
         tile_items(cs, cl, ch, chl, ks, kl);
         int k = ks + kl;
         long long s0 = base;
-        base += cs + cl;
+        base += span(cs, cl);
         for (int j = 0; j < k; ++j) {
             Item it;
             bool lg = j >= ks;

@@ -197,9 +197,15 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
     }
     if (nwide) atomicAdd(&ctr[cWideCount], nwide);
     __syncthreads();
+    // small / mid-size runs padded to even counts: every run starts and ends on a 64-B pair
+    // boundary (k_scatter_pair; the padding slots are written as holes)
     int* row = hist + (long long)blockIdx.x * 2 * g.ntiles;
-    for (int t = threadIdx.x; t < 2 * g.ntiles; t += kCountBlock) row[t] = lh[t];
+    for (int t = threadIdx.x; t < 2 * g.ntiles; t += kCountBlock)
+        row[t] = t < g.ntiles ? (lh[t] + 1) & ~1 : lh[t];
 }
+
+// A hole record (padding slot of a small / mid-size run): box x0 = 255 > x1 = 0, no pixel.
+constexpr unsigned kHoleBox = 0x00ff00ffu;
 
 // Record stores of the scatter: plain stores (non-temporal ones measured 2x slower, the
 // L2 merges the 32-B halves of a line).
@@ -239,8 +245,9 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
     const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long nblk,
     Grid g, Src64 s, const int* __restrict__ hist, const long long* __restrict__ tile_start,
-    float4* __restrict__ recs, unsigned* __restrict__ cmx, int* __restrict__ wide_list,
-    int* __restrict__ ctr, int grp, long long rec_cap, int wide_cap) {
+    const int* __restrict__ tile_total, float4* __restrict__ recs, unsigned* __restrict__ cmx,
+    int* __restrict__ wide_list, int* __restrict__ ctr, int grp, long long rec_cap,
+    int wide_cap) {
     // Speculative launch (enqueued before the host has read the counters): the record and
     // wide-list buffers were sized by an earlier call; if this call needs more, every
     // workgroup leaves at once and the host relaunches after growing them.
@@ -413,10 +420,287 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             pV[k] = nV[k];
         }
     }
+    __syncthreads();
     if constexpr (ACC == kAccFix) {
-        __syncthreads();
         unsigned* out = cmx + (long long)blockIdx.x * g.ntiles * NOUT;  // per scatter block
         for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kScatterBlock) out[t] = cm[t];
+    }
+    // the small / mid-size runs' padding slots (k_count) become holes (an empty box)
+    const long long nrow = min((sb + 1) * grp, nblk);
+    for (int t = threadIdx.x; t < g.ntiles; t += kScatterBlock) {
+        const int end = (int)tile_start[t] + (nrow < nblk ? hist[nrow * 2 * g.ntiles + t] : tile_total[t]);
+        for (int cc = cur[t]; cc < end; ++cc) {
+            rec_store(&recs[2 * (long long)cc], make_float4(0.0f, 0.0f, 1.0f, 0.0f));
+            rec_store(&recs[2 * (long long)cc + 1],
+                      make_float4(0.0f, __int_as_float(0), 0.0f, __uint_as_float(kHoleBox)));
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// K3p: the scatter writing the small / mid-size stream as 64-B PAIRS (fp64 accumulation).
+// The scatter's cost is the number of scattered write locations: the same
+// records written as 64-B-aligned pairs of consecutive slots of a (workgroup, tile) run
+// take half the locations (tools/microbench/pairs.hip: 1.83 vs 2.40 ms for 10^8 records).
+// Runs of the small / mid-size stream are even (k_count pads every count workgroup's
+// count, k_tilescan aligns every tile's start), so slot s pairs with s ^ 1.  Per round
+// each lane offers up to kPairRU records; their per-tile ranks q come from 16-bit LDS
+// counters, slots = run cursor + q, and sub-round j handles the records of rank j: an
+// even slot parks its record in the tile's LDS slot, the odd slot (its partner, rank
+// j + 1 or a later round) writes both.  A record left parked at the end is flushed with
+// a hole (an empty box), as are the padding slots.  Large-stream records are written
+// directly (their cursors in LDS too).  LDS: 28 B parked + 2 cursors + 2 B rank counter
+// per tile (38 B: 152 KiB at 4096 tiles), one workgroup per CU as before.
+// ----------------------------------------------------------------------------------
+constexpr int kPairRU = 2;  // small / mid-size records a lane offers per round
+static inline size_t scatter_pair_lds(const Grid& g) {
+    return (size_t)g.ntiles * (16 + 4 + 4 + 4 + 8) + ((size_t)g.ntiles + 1) / 2 * 4 + 16;
+}
+
+template <int KID, int NOUT, bool CULL, int SRC, int PROBE>
+__global__ __launch_bounds__(kScatterBlock) void k_scatter_pair(
+    const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
+    const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long nblk,
+    Grid g, Src64 s, const int* __restrict__ hist, const long long* __restrict__ tile_start,
+    const int* __restrict__ tile_total, float4* __restrict__ recs, int* __restrict__ wide_list,
+    int* __restrict__ ctr, int grp, long long rec_cap, int wide_cap) {
+    // speculative launch: see k_scatter
+    if (ctr[cRecs] > rec_cap || ctr[cWideCount] > wide_cap) return;
+    extern __shared__ __attribute__((aligned(16))) float4 pa[];  // parked {lu, lv, h, c0}
+    const int nt = g.ntiles;
+    float* pc1 = (float*)(pa + nt);              // parked c1
+    int* pp = (int*)(pc1 + nt);                  // parked particle index
+    unsigned* pbox = (unsigned*)(pp + nt);       // parked box
+    int* cur = (int*)(pbox + nt);                // run cursors: small / mid, then large
+    unsigned* bc = (unsigned*)(cur + 2 * nt);    // per-round rank counters, 16 bits per tile
+    int* shared_q = (int*)(bc + (nt + 1) / 2);   // [0]: max rank of the round
+    const long long sb = blockIdx.x;
+    const int* row = hist + sb * grp * 2 * nt;
+    for (int t = threadIdx.x; t < 2 * nt; t += kScatterBlock) cur[t] = (int)tile_start[t] + row[t];
+    for (int t = threadIdx.x; t < (nt + 1) / 2; t += kScatterBlock) bc[t] = 0u;
+    if (threadIdx.x == 0) shared_q[0] = 0;
+    __syncthreads();
+    const long long gcnt = min((long long)grp, nblk - sb * grp);
+    auto batch_base = [&](long long c) { return ((c / gcnt) * nblk + sb * grp + c % gcnt) * kBatch; };
+    auto load_src = [&](long long b, double* dU, double* dV) {
+        if constexpr (SRC == 1) {
+#pragma unroll
+            for (int k = 0; k < kUnroll; ++k) {
+                const long long q = min(b + (long long)threadIdx.x * kUnroll + k, n - 1) * s.stride;
+                dU[k] = s.u64[q];
+                dV[k] = s.v64[q];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kUnroll; ++k) dU[k] = dV[k] = 0.0;
+        }
+    };
+    const bool al = aligned_vec<kUnroll>(u, v, h) && aligned_vec<kUnroll>(a0, NOUT == 2 ? a1 : a0, a0);
+    float pu[kUnroll], pv[kUnroll], ph[kUnroll], pa0[kUnroll], pa1[kUnroll];
+    double pU[kUnroll], pV[kUnroll];
+    long long c = 0;
+    const long long p0 = batch_base(0);
+    load_batch<kUnroll>(u, v, h, p0, n, al, pu, pv, ph);
+    load_props<NOUT>(a0, a1, p0, n, al, pa0, pa1);
+    load_src(p0, pU, pV);
+    for (long long base = p0, next; base < n; base = next) {
+        next = batch_base(++c);
+        float nu[kUnroll], nv[kUnroll], nh[kUnroll], na0[kUnroll], na1[kUnroll];
+        load_batch<kUnroll>(u, v, h, next, n, al, nu, nv, nh);
+        load_props<NOUT>(a0, a1, next, n, al, na0, na1);
+        double nU[kUnroll], nV[kUnroll];
+        load_src(next, nU, nV);
+        // this lane's particles: footprint, coefficients, exact frame coordinates
+        Box bx[kUnroll];
+        float cf0[kUnroll], cf1[kUnroll];
+        double Ux[kUnroll], Vx[kUnroll];
+        bool mb[kUnroll];
+        // record iterator over the lane's particles' tiles: particle k, tile (tx, ty)
+        int ik = 0, itx = 0, ity = 0;
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k) {
+            const int p = (int)(base + (long long)threadIdx.x * kUnroll + k);
+            bx[k] = Box{0, -1, 0, -1};
+            cf0[k] = cf1[k] = 0.0f;
+            Ux[k] = Vx[k] = 0.0;
+            mb[k] = false;
+            Box b;
+            if (!footprint<CULL>(g, s, p, pu[k], pv[k], ph[k], b)) continue;
+            const int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
+            const int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
+            if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > g.wide_tiles) {
+                wide_list[atomicAdd(&ctr[cWideCursor], 1)] = p;
+                continue;
+            }
+            bx[k] = b;
+            cf0[k] = (float)term_coef<KID>(pa0[k], ph[k]);
+            cf1[k] = NOUT == 2 ? (float)term_coef<KID>(pa1[k], ph[k]) : 0.0f;
+            Ux[k] = SRC == 0 ? (double)pu[k] : SRC == 1 ? pU[k] : src_u(s, p, pu[k]);
+            Vx[k] = SRC == 0 ? (double)pv[k] : SRC == 1 ? pV[k] : src_v(s, p, pv[k]);
+            mb[k] = maybe_large(g, b);
+        }
+        // the current particle's fields (static register indices: no scratch)
+        Box cb{0, -1, 0, -1};
+        float cph = 0.0f, ccf0 = 0.0f, ccf1 = 0.0f;
+        double cU = 0.0, cV = 0.0;
+        bool cmb = false;
+        auto take = [&]() {
+#pragma unroll
+            for (int k = 0; k < kUnroll; ++k)
+                if (k == ik) {
+                    cb = bx[k];
+                    cph = ph[k];
+                    ccf0 = cf0[k];
+                    ccf1 = cf1[k];
+                    cU = Ux[k];
+                    cV = Vx[k];
+                    cmb = mb[k];
+                }
+        };
+        // the next particle with a box (from ik on); tiles walked ty fastest
+        auto seek = [&]() {
+            for (; ik < kUnroll; ++ik) {
+                take();
+                if (cb.x0 <= cb.x1) break;
+            }
+            if (ik < kUnroll) {
+                itx = cb.x0 >> kTileShift;
+                ity = cb.y0 >> kTileShift;
+            }
+        };
+        seek();
+        for (;;) {
+            // gather up to kPairRU small / mid-size records; large ones are written here
+            int rt[kPairRU], rq[kPairRU], rslot[kPairRU];
+            float4 r0[kPairRU], r1[kPairRU];
+            int cnt = 0;
+#pragma unroll
+            for (int j = 0; j < kPairRU; ++j) {
+                rt[j] = -1;
+                rq[j] = -1;
+                rslot[j] = -1;
+            }
+            while (cnt < kPairRU && ik < kUnroll) {
+                const Box b = cb;
+                const int p = (int)(base + (long long)threadIdx.x * kUnroll + ik);
+                const int t = itx * g.nty + ity;
+                const unsigned bp = tile_box(b, itx, ity);
+                const bool large = cmb && box_large(bp, g.gather_min);
+                const float4 q0 = make_float4((float)(cU - corner_x(g, max(b.x0, itx * kTile))),
+                                              (float)(cV - corner_y(g, max(b.y0, ity * kTile))),
+                                              cph, ccf0);
+                const float4 q1 = make_float4(ccf1, __int_as_float(p), rec_band(g.mgl, cph),
+                                              __uint_as_float(bp));
+                if (large) {
+                    const int slot = atomicAdd(&cur[t + nt], 1);
+                    rec_store(&recs[2 * (long long)slot], q0);
+                    rec_store(&recs[2 * (long long)slot + 1], q1);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < kPairRU; ++j)
+                        if (j == cnt) {
+                            rt[j] = t;
+                            r0[j] = q0;
+                            r1[j] = q1;
+                        }
+                    ++cnt;
+                }
+                // next tile of this particle, or the next particle
+                if (++ity > (b.y1 >> kTileShift)) {
+                    ity = b.y0 >> kTileShift;
+                    if (++itx > (b.x1 >> kTileShift)) {
+                        ++ik;
+                        seek();
+                    }
+                }
+            }
+            if (!__syncthreads_or(cnt > 0)) break;
+            // ranks within the round, per tile
+#pragma unroll
+            for (int j = 0; j < kPairRU; ++j)
+                if (rt[j] >= 0) {
+                    const int sh = 16 * (rt[j] & 1);
+                    rq[j] = (int)((atomicAdd(&bc[rt[j] >> 1], 1u << sh) >> sh) & 0xffffu);
+                    if (rq[j] > 0) atomicMax(&shared_q[0], rq[j]);
+                }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kPairRU; ++j)
+                if (rt[j] >= 0) rslot[j] = cur[rt[j]] + rq[j];
+            const int mq = shared_q[0];
+            __syncthreads();  // every lane has its slot and the round's max rank
+#pragma unroll
+            for (int j = 0; j < kPairRU; ++j)
+                if (rq[j] == 0) {  // one lane per tile: advance the cursor, clear the counter
+                    const int sh = 16 * (rt[j] & 1);
+                    cur[rt[j]] += (int)((bc[rt[j] >> 1] >> sh) & 0xffffu);
+                    atomicAnd(&bc[rt[j] >> 1], ~(0xffffu << sh));
+                }
+            if (threadIdx.x == 0) shared_q[0] = 0;
+            for (int r = 0; r <= mq; ++r) {
+#pragma unroll
+                for (int j = 0; j < kPairRU; ++j)
+                    if (rq[j] == r && !(rslot[j] & 1)) {  // first of its pair: park it
+                        const int t = rt[j];
+                        pa[t] = r0[j];
+                        pc1[t] = r1[j].x;
+                        pp[t] = __float_as_int(r1[j].y);
+                        pbox[t] = __float_as_uint(r1[j].w);
+                    }
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < kPairRU; ++j)
+                    if (rq[j] == r && (rslot[j] & 1)) {  // second: both records, 64 B
+                        const int t = rt[j];
+                        const float4 f0 = pa[t];
+                        const float4 f1 = make_float4(pc1[t], __int_as_float(pp[t]),
+                                                      rec_band(g.mgl, f0.z), __uint_as_float(pbox[t]));
+                        float4* d = recs + 2 * (long long)(rslot[j] - 1);
+                        rec_store(d, f0);
+                        rec_store(d + 1, f1);
+                        rec_store(d + 2, r0[j]);
+                        rec_store(d + 3, r1[j]);
+                    }
+                __syncthreads();
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k) {
+            pu[k] = nu[k];
+            pv[k] = nv[k];
+            ph[k] = nh[k];
+            pa0[k] = na0[k];
+            pa1[k] = na1[k];
+            pU[k] = nU[k];
+            pV[k] = nV[k];
+        }
+    }
+    // flush: a parked record gets a hole as its partner; the padding slots up to the run's
+    // end (the next scatter workgroup's first count row, or the tile's end) become holes
+    const float4 hole0 = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
+    const float4 hole1 = make_float4(0.0f, __int_as_float(0), 0.0f, __uint_as_float(kHoleBox));
+    const long long nrow = min((sb + 1) * grp, nblk);
+    for (int t = threadIdx.x; t < nt; t += kScatterBlock) {
+        int cc = cur[t];
+        const int end = (int)tile_start[t] + (nrow < nblk ? hist[nrow * 2 * nt + t] : tile_total[t]);
+        if (cc & 1) {
+            const float4 f0 = pa[t];
+            const float4 f1 = make_float4(pc1[t], __int_as_float(pp[t]), rec_band(g.mgl, f0.z),
+                                          __uint_as_float(pbox[t]));
+            float4* d = recs + 2 * (long long)(cc - 1);
+            rec_store(d, f0);
+            rec_store(d + 1, f1);
+            rec_store(d + 2, hole0);
+            rec_store(d + 3, hole1);
+            ++cc;
+        }
+        for (; cc < end; cc += 2) {
+            float4* d = recs + 2 * (long long)cc;
+            rec_store(d, hole0);
+            rec_store(d + 1, hole1);
+            rec_store(d + 2, hole0);
+            rec_store(d + 3, hole1);
+        }
     }
 }
 
@@ -1149,8 +1433,9 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
             load_rec(recs, it.start + min(i + 2 * kDepBlock, last), n0, n1);
             Prep P;
             P.b = Box{0, -1, 0, -1};
-            const bool live = i < it.count;
+            bool live = i < it.count;
             if (live) rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
+            live = live && P.b.x0 <= P.b.x1;  // not a hole (padding slot)
             r0 = q0;
             r1 = q1;
             q0 = n0;
@@ -1403,6 +1688,7 @@ __global__ __launch_bounds__(kBlock) void k_evals(Grid g, int kid, Src64 s,
             Prep P;
             rec_prep<kAccF64>(r0, r1, X0, Y0, make_int2(0, 0), P);
             const int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
+            if (bw <= 0) continue;  // a hole (padding slot)
             if (it.mode == 1) {
                 c1 += gather_slots(g, kid, __float_as_uint(r1.w));
             } else if (bw <= 3 && bh <= 3) {
@@ -1766,27 +2052,64 @@ static inline size_t scatter_lds(const Grid& g, int nout, bool det) {
            (det ? (size_t)g.ntiles * nout * sizeof(unsigned) : 0);
 }
 
+// Dynamic LDS above the 64 KiB default needs the kernel's attribute raised once.
+template <class K>
+static int allow_lds(K kern, size_t bytes) {
+    static bool done = false;  // per kernel instantiation
+    if (!done && bytes > 65536) {
+        ASP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)bytes));
+        done = true;
+    }
+    return ASP_OK;
+}
+
 // K3 on stream st.  rec_cap / wide_cap: the capacities the kernel checks against the
-// device counters (speculative launch; see project2d).
+// device counters (speculative launch; see project2d).  fp64 accumulation scatters the
+// small / mid-size stream as 64-B pairs (k_scatter_pair); fixed point keeps k_scatter,
+// whose per-tile maxima need the LDS the pairs take (ASP_SCATTER_PAIRS=0 forces it).
+template <int KID, int NOUT, int ACC, bool CULL, int SRC, int PROBE>
+static int scatter_variant(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl,
+                           const float* u, const float* v, const float* h, const float* a0,
+                           const float* a1, long long rec_cap, int wide_cap, hipStream_t st) {
+    int* dc = (int*)ws.counters.p;
+    static const bool pairs_off = [] {
+        const char* e = getenv("ASP_SCATTER_PAIRS");
+        return e && atoi(e) == 0;
+    }();
+    if (ACC == kAccF64 && !pairs_off && scatter_pair_lds(g) <= 163840) {
+        auto kern = k_scatter_pair<KID, NOUT, CULL, SRC, PROBE>;
+        ASP_TRY(allow_lds(kern, scatter_pair_lds(g)));
+        hipLaunchKernelGGL(kern, dim3((unsigned)pl.nblk_s), dim3(kScatterBlock),
+                           scatter_pair_lds(g), st, u, v, h, a0, a1, pl.n, pl.nblk, g, s,
+                           (const int*)ws.hist.p, (const long long*)ws.tile_start.p,
+                           (const int*)ws.tile_total.p, (float4*)ws.recs.p, (int*)ws.wide.p, dc,
+                           pl.grp, rec_cap, wide_cap);
+    } else {
+        hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC, CULL, SRC, PROBE>), dim3((unsigned)pl.nblk_s),
+                           dim3(kScatterBlock), scatter_lds(g, NOUT, ACC == kAccFix), st, u, v, h,
+                           a0, a1, pl.n, pl.nblk, g, s, (const int*)ws.hist.p,
+                           (const long long*)ws.tile_start.p, (const int*)ws.tile_total.p,
+                           (float4*)ws.recs.p, (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc, pl.grp,
+                           rec_cap, wide_cap);
+    }
+    ASP_LAUNCHED();
+    return ASP_OK;
+}
+
 template <int KID, int NOUT, int ACC>
 static int launch_scatter(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl,
                           const float* u, const float* v, const float* h, const float* a0,
                           const float* a1, long long rec_cap, int wide_cap, hipStream_t st,
                           bool probe = false) {
-    int* dc = (int*)ws.counters.p;
     StageMark m(ws, kSScatter, st);
-    hipLaunchKernelGGL((g.nonsquare || g.mixed ? (probe ? k_scatter<KID, NOUT, ACC, true, 2, 1>
-                                                        : k_scatter<KID, NOUT, ACC, true, 2, 0>)
-                        : s.u64 ? (probe ? k_scatter<KID, NOUT, ACC, false, 1, 1>
-                                         : k_scatter<KID, NOUT, ACC, false, 1, 0>)
-                                : (probe ? k_scatter<KID, NOUT, ACC, false, 0, 1>
-                                         : k_scatter<KID, NOUT, ACC, false, 0, 0>)),
-                       dim3((unsigned)pl.nblk_s), dim3(kScatterBlock),
-                       scatter_lds(g, NOUT, ACC == kAccFix), st, u, v, h, a0, a1, pl.n, pl.nblk,
-                       g, s, (const int*)ws.hist.p, (const long long*)ws.tile_start.p,
-                       (float4*)ws.recs.p, (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc, pl.grp,
-                       rec_cap, wide_cap);
-    ASP_LAUNCHED();
+#define ASP_SV(C, S, P) scatter_variant<KID, NOUT, ACC, C, S, P>(g, s, ws, pl, u, v, h, a0, a1, rec_cap, wide_cap, st)
+    int rc;
+    if (g.nonsquare || g.mixed) rc = probe ? ASP_SV(true, 2, 1) : ASP_SV(true, 2, 0);
+    else if (s.u64) rc = probe ? ASP_SV(false, 1, 1) : ASP_SV(false, 1, 0);
+    else rc = probe ? ASP_SV(false, 0, 1) : ASP_SV(false, 0, 0);
+#undef ASP_SV
+    ASP_TRY(rc);
     m.done();
     return ASP_OK;
 }
