@@ -23,6 +23,7 @@ enum Ctr {
     cWideMax0 = 7,  // max |c0| over wide particles, fp32 bits (K3)
     cWideMax1 = 8,  // max |c1| over wide particles, fp32 bits (K3)
     cLarge = 9,     // records in the large stream (K2b)
+    cPairFail = 10, // k_scatter_pair records dropped by its retry bound (never expected)
     cNum = 16
 };
 
@@ -264,6 +265,37 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
         ctr[cMerges] = (int)s_merge[kScanThreads - 1];
         ctr[cLarge] = (int)min(total1, (long long)0x7fffffff);
     }
+}
+
+// ----------------------------------------------------------------------------------
+// K2c: dispatch order of the deposit work items -- largest first (longest-processing-time
+// scheduling: the items of the dense central tiles used to start late in Morton order and
+// finish last).  One workgroup; items bucketed by floor(log2(count)), buckets in
+// decreasing size, order within a bucket unspecified.  order[b] = the item workgroup b
+// takes.
+// ----------------------------------------------------------------------------------
+constexpr int kOrderBuckets = 33;  // log2 classes of counts < 2^31, plus empty items
+[[maybe_unused]] static __global__ __launch_bounds__(kScanThreads) void k_item_order(
+    const Item* __restrict__ items, int n, int* __restrict__ order, int identity) {
+    __shared__ int cnt[kOrderBuckets], start[kOrderBuckets];
+    if (identity) {  // A/B switch (ASP_ITEM_ORDER=0): Morton order as produced
+        for (int i = threadIdx.x; i < n; i += kScanThreads) order[i] = i;
+        return;
+    }
+    if (threadIdx.x < kOrderBuckets) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    auto bucket = [](int c) { return c <= 0 ? kOrderBuckets - 1 : __builtin_clz((unsigned)c) - 1; };
+    for (int i = threadIdx.x; i < n; i += kScanThreads) atomicAdd(&cnt[bucket(items[i].count)], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int s = 0;
+        for (int b = 0; b < kOrderBuckets; ++b) {
+            start[b] = s;
+            s += cnt[b];
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += kScanThreads) order[atomicAdd(&start[bucket(items[i].count)], 1)] = i;
 }
 
 }  // namespace asp

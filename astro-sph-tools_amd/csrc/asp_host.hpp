@@ -62,7 +62,7 @@ struct Workspace {
     long long stage_n[kStages] = {};
     Buf knn[8];  // asp_knn_smoothing_lengths (knn[7]: the level-L cell table)
     Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
-        wide, slabs, morton, aux[6];
+        wide, slabs, morton, aux[6], iorder;
     Buf in64[4];     // asp_project2d_f64: the caller's fp64 arrays, resident for exact decisions
     Buf pairs[4];    // asp_pair_list
     int* h_counters = nullptr;  // pinned
@@ -87,7 +87,7 @@ struct Workspace {
     int pin_next = 0;
     std::vector<Buf*> all_bufs() {
         std::vector<Buf*> v = {&hist, &cmx, &tile_total, &tile_start, &tile_k, &items, &merges,
-                               &counters, &recs, &wide, &slabs, &morton, &morton3};
+                               &counters, &recs, &wide, &slabs, &morton, &morton3, &iorder};
         for (auto& b : in) v.push_back(&b);
         for (auto& b : out) v.push_back(&b);
         for (auto& b : aux) v.push_back(&b);

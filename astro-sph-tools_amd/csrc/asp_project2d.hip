@@ -209,7 +209,12 @@ constexpr unsigned kHoleBox = 0x00ff00ffu;
 
 // Record stores of the scatter: plain stores (non-temporal ones measured 2x slower, the
 // L2 merges the 32-B halves of a line).
-__device__ __forceinline__ void rec_store(float4* dst, float4 v) { *dst = v; }
+__device__ __forceinline__ void rec_store(float4* dst, float4 v) {
+    // one global_store_dwordx4 per half record: the empty asm keeps the vectorizer from
+    // regrouping two halves as dwordx3 + unaligned dwordx4 + dword
+    *dst = v;
+    asm volatile("" ::: "memory");
+}
 
 template <int NOUT>
 __device__ __forceinline__ void load_props(const float* __restrict__ a0,
@@ -440,22 +445,30 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
 // ----------------------------------------------------------------------------------
 // K3p: the scatter writing the small / mid-size stream as 64-B PAIRS (fp64 accumulation).
 // The scatter's cost is the number of scattered write locations: the same
-// records written as 64-B-aligned pairs of consecutive slots of a (workgroup, tile) run
-// take half the locations (tools/microbench/pairs.hip: 1.83 vs 2.40 ms for 10^8 records).
-// Runs of the small / mid-size stream are even (k_count pads every count workgroup's
-// count, k_tilescan aligns every tile's start), so slot s pairs with s ^ 1.  Per round
-// each lane offers up to kPairRU records; their per-tile ranks q come from 16-bit LDS
-// counters, slots = run cursor + q, and sub-round j handles the records of rank j: an
-// even slot parks its record in the tile's LDS slot, the odd slot (its partner, rank
-// j + 1 or a later round) writes both.  A record left parked at the end is flushed with
-// a hole (an empty box), as are the padding slots.  Large-stream records are written
-// directly (their cursors in LDS too).  LDS: 28 B parked + 2 cursors + 2 B rank counter
-// per tile (38 B: 152 KiB at 4096 tiles), one workgroup per CU as before.
+// records written as 64-B-aligned pairs of a (workgroup, tile) run take half the
+// locations.  Each tile has one LDS park slot and one 64-bit word {run cursor, state}
+// (state: empty, busy, or the parked record's particle index).  A record EXCHANGES the
+// word with "busy" -- one LDS atomic decides everything: empty -> it parks its record and
+// stores {cursor, its index}; parked -> it takes the partner, stores {cursor + 2, empty}
+// and writes both records to slots cursor, cursor + 1; busy (another lane mid-handoff) ->
+// retry.  No barriers (tools/microbench/pairs.hip: 10^8 records 1.11 ms, vs 2.40 for
+// single 32-B records and 1.83 for barrier-synchronised rank rounds).  Runs of the small /
+// mid-size stream are even (k_count pads every count workgroup's count, k_tilescan aligns
+// every tile's start); a record still parked at the end is written with a hole (an empty
+// box) as its partner, and the run's remaining padding slots become holes.  Large-stream
+// records are written directly.  LDS per tile: the parked record (24 B: p lives in the
+// state, band is recomputed from h), the word, the large stream's cursor -- 36 B, 144 KiB
+// at 4096 tiles; one workgroup per CU as before.
 // ----------------------------------------------------------------------------------
-constexpr int kPairRU = 2;  // small / mid-size records a lane offers per round
-static inline size_t scatter_pair_lds(const Grid& g) {
-    return (size_t)g.ntiles * (16 + 4 + 4 + 4 + 8) + ((size_t)g.ntiles + 1) / 2 * 4 + 16;
-}
+// Compiler ordering of LDS accesses only.  A wave's LDS operations execute in issue
+// order, so a park slot's record stores precede its state store (and a taker's reads
+// precede its release) without a fence -- a release fence would also wait for every
+// global load in flight (s_waitcnt vmcnt(0)): the next batch's prefetch, every record.
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+constexpr unsigned kParkEmpty = 0xffffffffu;  // park states; a parked record: its index
+constexpr unsigned kParkBusy = 0xfffffffeu;
+static inline size_t scatter_pair_lds(const Grid& g) { return (size_t)g.ntiles * 36; }
 
 template <int KID, int NOUT, bool CULL, int SRC, int PROBE>
 __global__ __launch_bounds__(kScatterBlock) void k_scatter_pair(
@@ -468,18 +481,59 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter_pair(
     if (ctr[cRecs] > rec_cap || ctr[cWideCount] > wide_cap) return;
     extern __shared__ __attribute__((aligned(16))) float4 pa[];  // parked {lu, lv, h, c0}
     const int nt = g.ntiles;
-    float* pc1 = (float*)(pa + nt);              // parked c1
-    int* pp = (int*)(pc1 + nt);                  // parked particle index
-    unsigned* pbox = (unsigned*)(pp + nt);       // parked box
-    int* cur = (int*)(pbox + nt);                // run cursors: small / mid, then large
-    unsigned* bc = (unsigned*)(cur + 2 * nt);    // per-round rank counters, 16 bits per tile
-    int* shared_q = (int*)(bc + (nt + 1) / 2);   // [0]: max rank of the round
+    unsigned long long* wd = (unsigned long long*)(pa + nt);  // {small / mid cursor, state}
+    float* pc1 = (float*)(wd + nt);                           // parked c1
+    unsigned* pbox = (unsigned*)(pc1 + nt);                   // parked box
+    int* cur1 = (int*)(pbox + nt);                            // large-stream cursors
     const long long sb = blockIdx.x;
     const int* row = hist + sb * grp * 2 * nt;
-    for (int t = threadIdx.x; t < 2 * nt; t += kScatterBlock) cur[t] = (int)tile_start[t] + row[t];
-    for (int t = threadIdx.x; t < (nt + 1) / 2; t += kScatterBlock) bc[t] = 0u;
-    if (threadIdx.x == 0) shared_q[0] = 0;
+    for (int t = threadIdx.x; t < nt; t += kScatterBlock) {
+        wd[t] = ((unsigned long long)(unsigned)((int)tile_start[t] + row[t]) << 32) | kParkEmpty;
+        cur1[t] = (int)tile_start[t + nt] + row[t + nt];
+    }
     __syncthreads();
+    // One small / mid-size record (tile t, particle p) into the pairs.  The retry loop
+    // exits only when EVERY participating lane of the wave is done (a wave-uniform exit):
+    // a lane that takes the word completes its hand-off inside the same iteration, so a
+    // lane of the same wave retrying on that tile's busy state never waits on code the
+    // compiler would otherwise sink behind a divergent loop exit (which hangs).  The retry
+    // count is bounded (a never-reached safety net: the record is dropped and counted).
+    auto pair_insert = [&](int t, int p, float4 q0, float4 q1) {
+        bool done = false;
+        int tries = 0;
+        do {
+            if (!done) {
+                const unsigned long long x = atomicExch(&wd[t], (unsigned long long)kParkBusy);
+                const unsigned st = (unsigned)x;
+                const unsigned cc = (unsigned)(x >> 32);
+                if (st == kParkEmpty) {  // park
+                    pa[t] = q0;
+                    pc1[t] = q1.x;
+                    pbox[t] = __float_as_uint(q1.w);
+                    lds_order();  // the record before the state (LDS executes a wave's ops in order)
+                    __hip_atomic_store(&wd[t], ((unsigned long long)cc << 32) | (unsigned)p,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    done = true;
+                } else if (st != kParkBusy) {  // take the parked partner (particle st)
+                    const float4 f0 = pa[t];
+                    const float4 f1 = make_float4(pc1[t], __int_as_float((int)st),
+                                                  rec_band(g.mgl, f0.z), __uint_as_float(pbox[t]));
+                    lds_order();  // the partner's reads before the slot is released
+                    __hip_atomic_store(&wd[t], ((unsigned long long)(cc + 2) << 32) | kParkEmpty,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    float4* d = recs + 2 * (long long)cc;
+                    rec_store(d, f0);
+                    rec_store(d + 1, f1);
+                    rec_store(d + 2, q0);
+                    rec_store(d + 3, q1);
+                    done = true;
+                } else if (++tries > (1 << 22)) {  // busy far too long: give up
+                    atomicAdd(&ctr[cPairFail], 1);
+                    done = true;
+                }
+            }
+        } while (__ballot(!done) != 0ull);
+    };
     const long long gcnt = min((long long)grp, nblk - sb * grp);
     auto batch_base = [&](long long c) { return ((c / gcnt) * nblk + sb * grp + c % gcnt) * kBatch; };
     auto load_src = [&](long long b, double* dU, double* dV) {
@@ -510,20 +564,9 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter_pair(
         load_props<NOUT>(a0, a1, next, n, al, na0, na1);
         double nU[kUnroll], nV[kUnroll];
         load_src(next, nU, nV);
-        // this lane's particles: footprint, coefficients, exact frame coordinates
-        Box bx[kUnroll];
-        float cf0[kUnroll], cf1[kUnroll];
-        double Ux[kUnroll], Vx[kUnroll];
-        bool mb[kUnroll];
-        // record iterator over the lane's particles' tiles: particle k, tile (tx, ty)
-        int ik = 0, itx = 0, ity = 0;
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
             const int p = (int)(base + (long long)threadIdx.x * kUnroll + k);
-            bx[k] = Box{0, -1, 0, -1};
-            cf0[k] = cf1[k] = 0.0f;
-            Ux[k] = Vx[k] = 0.0;
-            mb[k] = false;
             Box b;
             if (!footprint<CULL>(g, s, p, pu[k], pv[k], ph[k], b)) continue;
             const int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
@@ -532,137 +575,28 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter_pair(
                 wide_list[atomicAdd(&ctr[cWideCursor], 1)] = p;
                 continue;
             }
-            bx[k] = b;
-            cf0[k] = (float)term_coef<KID>(pa0[k], ph[k]);
-            cf1[k] = NOUT == 2 ? (float)term_coef<KID>(pa1[k], ph[k]) : 0.0f;
-            Ux[k] = SRC == 0 ? (double)pu[k] : SRC == 1 ? pU[k] : src_u(s, p, pu[k]);
-            Vx[k] = SRC == 0 ? (double)pv[k] : SRC == 1 ? pV[k] : src_v(s, p, pv[k]);
-            mb[k] = maybe_large(g, b);
-        }
-        // the current particle's fields (static register indices: no scratch)
-        Box cb{0, -1, 0, -1};
-        float cph = 0.0f, ccf0 = 0.0f, ccf1 = 0.0f;
-        double cU = 0.0, cV = 0.0;
-        bool cmb = false;
-        auto take = [&]() {
-#pragma unroll
-            for (int k = 0; k < kUnroll; ++k)
-                if (k == ik) {
-                    cb = bx[k];
-                    cph = ph[k];
-                    ccf0 = cf0[k];
-                    ccf1 = cf1[k];
-                    cU = Ux[k];
-                    cV = Vx[k];
-                    cmb = mb[k];
-                }
-        };
-        // the next particle with a box (from ik on); tiles walked ty fastest
-        auto seek = [&]() {
-            for (; ik < kUnroll; ++ik) {
-                take();
-                if (cb.x0 <= cb.x1) break;
-            }
-            if (ik < kUnroll) {
-                itx = cb.x0 >> kTileShift;
-                ity = cb.y0 >> kTileShift;
-            }
-        };
-        seek();
-        for (;;) {
-            // gather up to kPairRU small / mid-size records; large ones are written here
-            int rt[kPairRU], rq[kPairRU], rslot[kPairRU];
-            float4 r0[kPairRU], r1[kPairRU];
-            int cnt = 0;
-#pragma unroll
-            for (int j = 0; j < kPairRU; ++j) {
-                rt[j] = -1;
-                rq[j] = -1;
-                rslot[j] = -1;
-            }
-            while (cnt < kPairRU && ik < kUnroll) {
-                const Box b = cb;
-                const int p = (int)(base + (long long)threadIdx.x * kUnroll + ik);
-                const int t = itx * g.nty + ity;
-                const unsigned bp = tile_box(b, itx, ity);
-                const bool large = cmb && box_large(bp, g.gather_min);
-                const float4 q0 = make_float4((float)(cU - corner_x(g, max(b.x0, itx * kTile))),
-                                              (float)(cV - corner_y(g, max(b.y0, ity * kTile))),
-                                              cph, ccf0);
-                const float4 q1 = make_float4(ccf1, __int_as_float(p), rec_band(g.mgl, cph),
-                                              __uint_as_float(bp));
-                if (large) {
-                    const int slot = atomicAdd(&cur[t + nt], 1);
-                    rec_store(&recs[2 * (long long)slot], q0);
-                    rec_store(&recs[2 * (long long)slot + 1], q1);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < kPairRU; ++j)
-                        if (j == cnt) {
-                            rt[j] = t;
-                            r0[j] = q0;
-                            r1[j] = q1;
-                        }
-                    ++cnt;
-                }
-                // next tile of this particle, or the next particle
-                if (++ity > (b.y1 >> kTileShift)) {
-                    ity = b.y0 >> kTileShift;
-                    if (++itx > (b.x1 >> kTileShift)) {
-                        ++ik;
-                        seek();
+            const float cf0 = (float)term_coef<KID>(pa0[k], ph[k]);
+            const float cf1 = NOUT == 2 ? (float)term_coef<KID>(pa1[k], ph[k]) : 0.0f;
+            const float band = rec_band(g.mgl, ph[k]);
+            const double U = SRC == 0 ? (double)pu[k] : SRC == 1 ? pU[k] : src_u(s, p, pu[k]);
+            const double V = SRC == 0 ? (double)pv[k] : SRC == 1 ? pV[k] : src_v(s, p, pv[k]);
+            const bool mb = maybe_large(g, b);
+            for (int tx = tx0; tx <= tx1; ++tx)
+                for (int ty = ty0; ty <= ty1; ++ty) {
+                    const int t = tx * g.nty + ty;
+                    const unsigned bp = tile_box(b, tx, ty);
+                    const float4 q0 = make_float4((float)(U - corner_x(g, max(b.x0, tx * kTile))),
+                                                  (float)(V - corner_y(g, max(b.y0, ty * kTile))),
+                                                  ph[k], cf0);
+                    const float4 q1 = make_float4(cf1, __int_as_float(p), band, __uint_as_float(bp));
+                    if (mb && box_large(bp, g.gather_min)) {
+                        const int slot = atomicAdd(&cur1[t], 1);
+                        rec_store(&recs[2 * (long long)slot], q0);
+                        rec_store(&recs[2 * (long long)slot + 1], q1);
+                    } else {
+                        pair_insert(t, p, q0, q1);
                     }
                 }
-            }
-            if (!__syncthreads_or(cnt > 0)) break;
-            // ranks within the round, per tile
-#pragma unroll
-            for (int j = 0; j < kPairRU; ++j)
-                if (rt[j] >= 0) {
-                    const int sh = 16 * (rt[j] & 1);
-                    rq[j] = (int)((atomicAdd(&bc[rt[j] >> 1], 1u << sh) >> sh) & 0xffffu);
-                    if (rq[j] > 0) atomicMax(&shared_q[0], rq[j]);
-                }
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < kPairRU; ++j)
-                if (rt[j] >= 0) rslot[j] = cur[rt[j]] + rq[j];
-            const int mq = shared_q[0];
-            __syncthreads();  // every lane has its slot and the round's max rank
-#pragma unroll
-            for (int j = 0; j < kPairRU; ++j)
-                if (rq[j] == 0) {  // one lane per tile: advance the cursor, clear the counter
-                    const int sh = 16 * (rt[j] & 1);
-                    cur[rt[j]] += (int)((bc[rt[j] >> 1] >> sh) & 0xffffu);
-                    atomicAnd(&bc[rt[j] >> 1], ~(0xffffu << sh));
-                }
-            if (threadIdx.x == 0) shared_q[0] = 0;
-            for (int r = 0; r <= mq; ++r) {
-#pragma unroll
-                for (int j = 0; j < kPairRU; ++j)
-                    if (rq[j] == r && !(rslot[j] & 1)) {  // first of its pair: park it
-                        const int t = rt[j];
-                        pa[t] = r0[j];
-                        pc1[t] = r1[j].x;
-                        pp[t] = __float_as_int(r1[j].y);
-                        pbox[t] = __float_as_uint(r1[j].w);
-                    }
-                __syncthreads();
-#pragma unroll
-                for (int j = 0; j < kPairRU; ++j)
-                    if (rq[j] == r && (rslot[j] & 1)) {  // second: both records, 64 B
-                        const int t = rt[j];
-                        const float4 f0 = pa[t];
-                        const float4 f1 = make_float4(pc1[t], __int_as_float(pp[t]),
-                                                      rec_band(g.mgl, f0.z), __uint_as_float(pbox[t]));
-                        float4* d = recs + 2 * (long long)(rslot[j] - 1);
-                        rec_store(d, f0);
-                        rec_store(d + 1, f1);
-                        rec_store(d + 2, r0[j]);
-                        rec_store(d + 3, r1[j]);
-                    }
-                __syncthreads();
-            }
         }
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
@@ -675,31 +609,31 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter_pair(
             pV[k] = nV[k];
         }
     }
+    __syncthreads();
     // flush: a parked record gets a hole as its partner; the padding slots up to the run's
     // end (the next scatter workgroup's first count row, or the tile's end) become holes
     const float4 hole0 = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
     const float4 hole1 = make_float4(0.0f, __int_as_float(0), 0.0f, __uint_as_float(kHoleBox));
     const long long nrow = min((sb + 1) * grp, nblk);
     for (int t = threadIdx.x; t < nt; t += kScatterBlock) {
-        int cc = cur[t];
+        const unsigned long long x = wd[t];
+        int cc = (int)(unsigned)(x >> 32);
+        const unsigned st = (unsigned)x;
         const int end = (int)tile_start[t] + (nrow < nblk ? hist[nrow * 2 * nt + t] : tile_total[t]);
-        if (cc & 1) {
+        if (st != kParkEmpty) {  // (never busy here: every hand-off completed)
             const float4 f0 = pa[t];
-            const float4 f1 = make_float4(pc1[t], __int_as_float(pp[t]), rec_band(g.mgl, f0.z),
+            const float4 f1 = make_float4(pc1[t], __int_as_float((int)st), rec_band(g.mgl, f0.z),
                                           __uint_as_float(pbox[t]));
-            float4* d = recs + 2 * (long long)(cc - 1);
+            float4* d = recs + 2 * (long long)cc;
             rec_store(d, f0);
             rec_store(d + 1, f1);
             rec_store(d + 2, hole0);
             rec_store(d + 3, hole1);
-            ++cc;
+            cc += 2;
         }
-        for (; cc < end; cc += 2) {
-            float4* d = recs + 2 * (long long)cc;
-            rec_store(d, hole0);
-            rec_store(d + 1, hole1);
-            rec_store(d + 2, hole0);
-            rec_store(d + 3, hole1);
+        for (; cc < end; ++cc) {
+            rec_store(&recs[2 * (long long)cc], hole0);
+            rec_store(&recs[2 * (long long)cc + 1], hole1);
         }
     }
 }
@@ -1016,7 +950,11 @@ __device__ __forceinline__ bool small3_fast(const Prep& P, int bw, int bh, int X
         m = fminf(m, fminf(fminf(fabsf(e.x), fabsf(e.y)), fabsf(r2c[i] - P.thr)));
     }
     if (!(m > P.band)) return false;  // a pair in the band (or NaN): exact path
+#ifdef ASP_ABLATE_DEP_CONFLICTS  // timing ablation only (wrong maps): bank-conflict-free adds
+    const int base = (int)(threadIdx.x & 31);
+#else
     const int base = pix(P.b.x0 - X0, P.b.y0 - Y0);
+#endif
     const f2v hv = f2v{P.hinv, P.hinv};
     // column j = 2 of rows 0, 1 as one packed pair, row 2 with a dummy partner
     f2v wc01 = kernel_shape2<KID>(sqrt2(f2v{r2c[0], r2c[1]}) * hv);
@@ -1387,15 +1325,16 @@ constexpr size_t deposit_lds() {
 template <int KID, int NOUT, int ACC>
 __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_deposit(
     Grid g, Src64 s, const float4* __restrict__ recs, const Item* __restrict__ items,
-    const int2* __restrict__ tile_k, unsigned long long* __restrict__ slabs,
-    float* __restrict__ out0, float* __restrict__ out1, int flags) {
+    const int* __restrict__ order, const int2* __restrict__ tile_k,
+    unsigned long long* __restrict__ slabs, float* __restrict__ out0, float* __restrict__ out1,
+    int flags) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];
     unsigned long long* acc0 = acc;
     unsigned long long* acc1 = acc + kTileWords;
     float* xt = (float*)(acc + NOUT * kTileWords);
     float* yt = xt + kTile;
     __shared__ int defer_lds[kDepBlock / 64][kDeferCap];
-    const Item it = items[blockIdx.x];
+    const Item it = items[order[blockIdx.x]];  // largest items first (k_item_order)
     if (it.mode != 0) return;  // the large stream's (K4g)
     int tx = it.tile / g.nty, ty = it.tile - (it.tile / g.nty) * g.nty;
     int X0 = tx * kTile, Y0 = ty * kTile;
@@ -1506,10 +1445,11 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
 template <int KID, int NOUT, int ACC>
 __global__ __launch_bounds__(kGatherThreads) void k_gather(
     Grid g, Src64 s, const float4* __restrict__ recs, const Item* __restrict__ items,
-    const int2* __restrict__ tile_k, unsigned long long* __restrict__ slabs,
-    float* __restrict__ out0, float* __restrict__ out1, int flags) {
+    const int* __restrict__ order, const int2* __restrict__ tile_k,
+    unsigned long long* __restrict__ slabs, float* __restrict__ out0, float* __restrict__ out1,
+    int flags) {
     extern __shared__ __attribute__((aligned(16))) double tot[];
-    const Item it = items[blockIdx.x / kGatherRegions];
+    const Item it = items[order[blockIdx.x / kGatherRegions]];  // largest first
     if (it.mode != 1) return;
     const int tx = it.tile / g.nty, ty = it.tile - (it.tile / g.nty) * g.nty;
     const int X0 = tx * kTile, Y0 = ty * kTile;
@@ -2136,12 +2076,22 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
         ASP_LAUNCHED();
         m.done();
     }
+    {  // largest work items first
+        ASP_TRY(ensure(ws.iorder, (size_t)std::max(1, pl.n_items) * sizeof(int)));
+        static const int identity = [] {
+            const char* e = getenv("ASP_ITEM_ORDER");
+            return e && atoi(e) == 0 ? 1 : 0;
+        }();
+        hipLaunchKernelGGL(k_item_order, dim3(1), dim3(kScanThreads), 0, st,
+                           (const Item*)ws.items.p, pl.n_items, (int*)ws.iorder.p, identity);
+        ASP_LAUNCHED();
+    }
     {
         StageMark m(ws, kSDeposit, st);
         const size_t lds = deposit_lds<NOUT>();
         hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(pl.n_items), dim3(kDepBlock),
                            lds, st, g, s, (const float4*)ws.recs.p,
-                           (const Item*)ws.items.p, (const int2*)ws.tile_k.p,
+                           (const Item*)ws.items.p, (const int*)ws.iorder.p, (const int2*)ws.tile_k.p,
                            (unsigned long long*)ws.slabs.p, o0, o1, dflags);
         ASP_LAUNCHED();
         m.done();
@@ -2152,8 +2102,8 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
         hipLaunchKernelGGL((k_gather<KID, NOUT, ACC>), dim3(pl.n_items * kGatherRegions),
                            dim3(kGatherThreads), lds, st, g,
                            s, (const float4*)ws.recs.p, (const Item*)ws.items.p,
-                           (const int2*)ws.tile_k.p, (unsigned long long*)ws.slabs.p, o0, o1,
-                           dflags);
+                           (const int*)ws.iorder.p, (const int2*)ws.tile_k.p,
+                           (unsigned long long*)ws.slabs.p, o0, o1, dflags);
         ASP_LAUNCHED();
         m.done();
     }

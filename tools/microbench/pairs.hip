@@ -13,12 +13,18 @@
 
 #include <cstdio>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 constexpr int T = 512;           // threads per workgroup
 constexpr int U = 2;             // records per lane per batch
 constexpr int NT = 4096;         // tiles
 constexpr int B = 256;           // workgroups
+constexpr int TABN = 1 << 22;    // skewed mode: tile ids drawn from a Plummer-like table
+__device__ const int* g_tab = nullptr;
+__device__ __forceinline__ int tile_of(unsigned hsh) {
+    return g_tab ? g_tab[hsh & (TABN - 1)] : (int)(hsh & (NT - 1));
+}
 
 __device__ __host__ __forceinline__ unsigned hash32(unsigned x) {
     x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
@@ -36,7 +42,7 @@ __global__ __launch_bounds__(T) void kA(float4* __restrict__ out, long long per_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             long long j = j0 + threadIdx.x * U + u;
-            int t = (int)(hash32((unsigned)(b * per_wg + j)) & (NT - 1));
+            int t = tile_of(hash32((unsigned)(b * per_wg + j)));
             int slot = j < per_wg ? atomicAdd(&cur[t], 1) : -1;
             float4 v0 = make_float4((float)j, (float)t, 1.f, 2.f);
 #pragma unroll
@@ -73,7 +79,7 @@ __global__ __launch_bounds__(T) void kP(float4* __restrict__ out, long long per_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             long long j = j0 + threadIdx.x * U + u;
-            tt[u] = (int)(hash32((unsigned)(b * per_wg + j)) & (NT - 1));
+            tt[u] = tile_of(hash32((unsigned)(b * per_wg + j)));
             q[u] = -1;
             r0[u] = make_float4((float)j, (float)tt[u], 1.f, 2.f);
             r1[u] = make_float4(3.f, 0.f, 0.f, 0.f);
@@ -140,13 +146,112 @@ __global__ __launch_bounds__(T) void kP(float4* __restrict__ out, long long per_
     (void)lane;
 }
 
+// M: the lock-free mailbox handoff (k_scatter_pair's protocol): one 64-bit LDS word per
+// tile {run cursor, state}; state -1 empty, -2 busy, >= 0 parked (index into the park
+// slot).  One exchange decides: empty -> park, parked -> take and write the pair at the
+// cursor, busy -> retry.  No barriers.
+__global__ __launch_bounds__(T) void kM(float4* __restrict__ out, long long per_wg,
+                                        const long long* __restrict__ base,
+                                        const long long* __restrict__ endp) {
+    extern __shared__ __attribute__((aligned(16))) float4 pend[];  // 2 per tile (32 B)
+    unsigned long long* wd = (unsigned long long*)(pend + 2 * NT);  // {cursor << 32 | state}
+    const int b = blockIdx.x;
+    for (int t = threadIdx.x; t < NT; t += T)
+        wd[t] = ((unsigned long long)(unsigned)base[(long long)t * B + b] << 32) | 0xffffffffull;
+    __syncthreads();
+    constexpr unsigned long long kBusy = 0xfffffffeull;
+    for (long long j0 = 0; j0 < per_wg; j0 += T * U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            long long j = j0 + threadIdx.x * U + u;
+            const bool live = j < per_wg;
+            int t = tile_of(hash32((unsigned)(b * per_wg + j)));
+            float4 r0 = make_float4((float)j, (float)t, 1.f, 2.f), r1 = make_float4(3.f, 0.f, 0.f, 0.f);
+            bool done = !live;
+            do {
+                if (!done) {
+                    const unsigned long long x = atomicExch(&wd[t], kBusy);
+                    const unsigned st = (unsigned)x;
+                    const unsigned cur = (unsigned)(x >> 32);
+                    if (st == 0xffffffffu) {  // empty: park
+                        pend[2 * t] = r0;
+                        pend[2 * t + 1] = r1;
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __hip_atomic_store(&wd[t], ((unsigned long long)cur << 32) | 0u,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        done = true;
+                    } else if (st != 0xfffffffeu) {  // parked: take, write the pair
+                        const float4 f0 = pend[2 * t], f1 = pend[2 * t + 1];
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __hip_atomic_store(&wd[t], ((unsigned long long)(cur + 2) << 32) | 0xffffffffull,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        float4* d = out + 2 * (long long)cur;
+                        d[0] = f0;
+                        d[1] = f1;
+                        d[2] = r0;
+                        d[3] = r1;
+                        done = true;
+                    }  // busy: the exchange left it busy; retry
+                }
+            } while (__ballot(!done) != 0ull);
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < NT; t += T) {
+        const unsigned long long x = wd[t];
+        if ((unsigned)x == 0u) {
+            float4* d = out + 2 * (long long)(x >> 32);
+            d[0] = pend[2 * t];
+            d[1] = pend[2 * t + 1];
+            d[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+            d[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+}
+
+static int run(bool skew);
 int main() {
+    int rc = run(false);
+    if (rc) return rc;
+    return run(true);
+}
+
+static int run(bool skew) {
     const long long N = 100000000LL;
     const long long per_wg = N / B;
+    // skewed: 64 x 64 tiles over [-4, 4]^2, Plummer surface density (1 + R^2)^-2
+    std::vector<int> tab(TABN);
+    {
+        std::vector<double> w(NT), cdf(NT);
+        double sum = 0;
+        for (int t = 0; t < NT; ++t) {
+            double x = -4 + 8.0 * ((t / 64) + 0.5) / 64, y = -4 + 8.0 * ((t % 64) + 0.5) / 64;
+            double r2 = x * x + y * y;
+            w[t] = 1.0 / ((1 + r2) * (1 + r2));
+            sum += w[t];
+            cdf[t] = sum;
+        }
+        int t = 0;
+        for (int i = 0; i < TABN; ++i) {
+            double q = (i + 0.5) / TABN * sum;
+            while (cdf[t] < q) ++t;
+            tab[i] = t;
+        }
+        // shuffle so the low hash bits pick random table entries
+        for (int i = TABN - 1; i > 0; --i) std::swap(tab[i], tab[hash32((unsigned)i) % (unsigned)(i + 1)]);
+    }
+    int* dtab = nullptr;
+    if (skew) {
+        hipMalloc(&dtab, TABN * sizeof(int));
+        hipMemcpy(dtab, tab.data(), TABN * sizeof(int), hipMemcpyHostToDevice);
+    }
+    hipMemcpyToSymbol(HIP_SYMBOL(g_tab), &dtab, sizeof(dtab));
+    auto tile_h = [&](unsigned hsh) { return skew ? tab[hsh & (TABN - 1)] : (int)(hsh & (NT - 1)); };
+    printf("== %s tiles\n", skew ? "Plummer-skewed" : "uniform");
     std::vector<long long> cnt((size_t)NT * B, 0);
     for (int b = 0; b < B; ++b)
         for (long long j = 0; j < per_wg; ++j)
-            cnt[(size_t)(hash32((unsigned)(b * per_wg + j)) & (NT - 1)) * B + b]++;
+            cnt[(size_t)tile_h(hash32((unsigned)(b * per_wg + j))) * B + b]++;
     std::vector<long long> baseA(cnt.size()), baseP(cnt.size()), endP(cnt.size());
     long long sA = 0, sP = 0;
     for (size_t i = 0; i < cnt.size(); ++i) {
@@ -172,22 +277,29 @@ int main() {
         printf("cannot set LDS size %zu\n", ldsP);
         return 3;
     }
+    const size_t ldsM = (size_t)2 * NT * 16 + NT * 8;
+    if (ldsM > 163840 || hipFuncSetAttribute((const void*)kM, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)ldsM) != hipSuccess) {
+        printf("cannot set LDS size %zu\n", ldsM);
+        return 4;
+    }
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     printf("records %lld, padded %lld (holes %.2f %%)\n", sA, sP, 100.0 * (sP - sA) / sA);
     for (int rep = 0; rep < 3; ++rep) {
-        for (int mode = 0; mode < 2; ++mode) {
+        for (int mode = 0; mode < 3; ++mode) {
             hipEventRecord(e0);
             if (mode == 0) hipLaunchKernelGGL(kA, dim3(B), dim3(T), 0, 0, d, per_wg, dA);
-            else hipLaunchKernelGGL(kP<0>, dim3(B), dim3(T), ldsP, 0, d, per_wg, dP, dE);
+            else if (mode == 1) hipLaunchKernelGGL(kP<0>, dim3(B), dim3(T), ldsP, 0, d, per_wg, dP, dE);
+            else hipLaunchKernelGGL(kM, dim3(B), dim3(T), ldsM, 0, d, per_wg, dP, dE);
             hipEventRecord(e1);
             hipEventSynchronize(e1);
             float ms;
             hipEventElapsedTime(&ms, e0, e1);
             hipError_t err = hipGetLastError();
             printf("rep %d  %-28s %7.3f ms %s\n", rep,
-                   mode == 0 ? "A 32-B records (paired lanes)" : "P 64-B pairs, one lane",
+                   mode == 0 ? "A 32-B records (paired lanes)" : mode == 1 ? "P 64-B pairs, sub-rounds" : "M 64-B pairs, mailbox",
                    ms, err == hipSuccess ? "" : hipGetErrorString(err));
         }
     }
@@ -204,5 +316,23 @@ int main() {
         else if (h[2 * s].z == 0.f) ++holes;
     }
     printf("P layout: %lld unwritten slots, %lld holes\n", bad, holes);
+    hipMemset(d, 0xff, (size_t)sP * 32);
+    hipLaunchKernelGGL(kM, dim3(B), dim3(T), ldsM, 0, d, per_wg, dP, dE);
+    hipMemcpy(h.data(), d, (size_t)sP * 32, hipMemcpyDeviceToHost);
+    bad = 0;
+    long long recs = 0;
+    for (long long s2 = 0; s2 < sP; ++s2) {
+        unsigned bits;
+        std::memcpy(&bits, &h[2 * s2].w, 4);
+        if (bits == 0xffffffffu) ++bad;
+        else if (h[2 * s2].z != 0.f) ++recs;
+    }
+    printf("M layout: %lld unwritten (the runs' padding beyond the flush), %lld records (want %lld)\n",
+           bad, recs, sA);
+    hipFree(d);
+    hipFree(dA);
+    hipFree(dP);
+    hipFree(dE);
+    if (dtab) hipFree(dtab);
     return 0;
 }
