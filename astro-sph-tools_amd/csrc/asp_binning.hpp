@@ -159,7 +159,7 @@ constexpr int kScanPer = 16;  // max tiles per scan thread held in registers (<=
 template <int PER>  // tiles per thread held in registers: ntiles <= PER * kScanThreads
 static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     const int* __restrict__ tile_total, const int* __restrict__ morton, int ntiles, int nstream,
-    long long* __restrict__ tile_start, Item* __restrict__ items, Merge* __restrict__ merges,
+    int pad, long long* __restrict__ tile_start, Item* __restrict__ items, Merge* __restrict__ merges,
     int* __restrict__ ctr) {
     __shared__ long long s_rec[kScanThreads], s_item[kScanThreads], s_slab[kScanThreads],
         s_merge[kScanThreads];
@@ -177,10 +177,10 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
         cs_[q] = in ? tile_total[tt[q]] : 0;
         cl_[q] = in && nstream == 2 ? tile_total[tt[q] + ntiles] : 0;
     }
-    // nstream = 2: every tile's run starts on an even slot (a 64-B pair boundary, for
+    // pad: every tile's run starts on an even slot (a 64-B pair boundary, for
     // k_scatter_pair): a tile whose two streams hold an odd total is followed by a gap slot
     // that no item covers
-    auto span = [&](int cs, int cl) { return (long long)(cs + cl) + (nstream == 2 ? ((cs + cl) & 1) : 0); };
+    auto span = [&](int cs, int cl) { return (long long)(cs + cl) + (pad ? ((cs + cl) & 1) : 0); };
     long long loc = 0, wloc = 0;  // all records; stream-1 records
 #pragma unroll
     for (int q = 0; q < PER; ++q) {

@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
                                                        const float* __restrict__ h,
                                                        long long n, long long nblk, Grid g,
                                                        Src64 s, int* __restrict__ hist,
-                                                       int* __restrict__ ctr) {
+                                                       int* __restrict__ ctr, int pad) {
     extern __shared__ __attribute__((aligned(16))) int lh[];  // 2 * ntiles columns
     for (int t = threadIdx.x; t < 2 * g.ntiles; t += kCountBlock) lh[t] = 0;
     __syncthreads();
@@ -197,11 +197,11 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
     }
     if (nwide) atomicAdd(&ctr[cWideCount], nwide);
     __syncthreads();
-    // small / mid-size runs padded to even counts: every run starts and ends on a 64-B pair
-    // boundary (k_scatter_pair; the padding slots are written as holes)
+    // pad: small / mid-size runs padded to even counts, so that every run starts and ends
+    // on a 64-B pair boundary (k_scatter_pair; the padding slots are written as holes)
     int* row = hist + (long long)blockIdx.x * 2 * g.ntiles;
     for (int t = threadIdx.x; t < 2 * g.ntiles; t += kCountBlock)
-        row[t] = t < g.ntiles ? (lh[t] + 1) & ~1 : lh[t];
+        row[t] = pad && t < g.ntiles ? (lh[t] + 1) & ~1 : lh[t];
 }
 
 // A hole record (padding slot of a small / mid-size run): box x0 = 255 > x1 = 0, no pixel.
@@ -470,6 +470,16 @@ constexpr unsigned kParkEmpty = 0xffffffffu;  // park states; a parked record: i
 constexpr unsigned kParkBusy = 0xfffffffeu;
 static inline size_t scatter_pair_lds(const Grid& g) { return (size_t)g.ntiles * 36; }
 
+// The pair scatter is opt-in (ASP_SCATTER_PAIRS=1; fp64 accumulation, its LDS fits): on
+// the Plummer bench field it measured slower than single records.
+static bool scatter_pairs(const Grid& g, bool det) {
+    static const bool on = [] {
+        const char* e = getenv("ASP_SCATTER_PAIRS");
+        return e && atoi(e) != 0;
+    }();
+    return on && !det && scatter_pair_lds(g) <= 163840;
+}
+
 template <int KID, int NOUT, bool CULL, int SRC, int PROBE>
 __global__ __launch_bounds__(kScatterBlock) void k_scatter_pair(
     const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
@@ -492,47 +502,74 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter_pair(
         cur1[t] = (int)tile_start[t + nt] + row[t + nt];
     }
     __syncthreads();
-    // One small / mid-size record (tile t, particle p) into the pairs.  The retry loop
-    // exits only when EVERY participating lane of the wave is done (a wave-uniform exit):
-    // a lane that takes the word completes its hand-off inside the same iteration, so a
-    // lane of the same wave retrying on that tile's busy state never waits on code the
-    // compiler would otherwise sink behind a divergent loop exit (which hangs).  The retry
-    // count is bounded (a never-reached safety net: the record is dropped and counted).
-    auto pair_insert = [&](int t, int p, float4 q0, float4 q1) {
-        bool done = false;
+    // One attempt: EXCHANGE the tile's word with "busy"; empty -> park, parked -> take the
+    // partner and write the pair, busy (another lane mid-hand-off) -> false.  Never loops,
+    // so a lane never spins inside divergent control flow.
+    auto try_insert = [&](int t, int p, float4 q0, float4 q1) -> bool {
+        const unsigned long long x = atomicExch(&wd[t], (unsigned long long)kParkBusy);
+        const unsigned st = (unsigned)x;
+        const unsigned cc = (unsigned)(x >> 32);
+        if (st == kParkEmpty) {  // park
+            pa[t] = q0;
+            pc1[t] = q1.x;
+            pbox[t] = __float_as_uint(q1.w);
+            lds_order();  // the record before the state (LDS executes a wave's ops in order)
+            __hip_atomic_store(&wd[t], ((unsigned long long)cc << 32) | (unsigned)p,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return true;
+        }
+        if (st == kParkBusy) return false;
+        // take the parked partner (particle st)
+        const float4 f0 = pa[t];
+        const float4 f1 = make_float4(pc1[t], __int_as_float((int)st), rec_band(g.mgl, f0.z),
+                                      __uint_as_float(pbox[t]));
+        lds_order();  // the partner's reads before the slot is released
+        __hip_atomic_store(&wd[t], ((unsigned long long)(cc + 2) << 32) | kParkEmpty,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        float4* d = recs + 2 * (long long)cc;
+        rec_store(d, f0);
+        rec_store(d + 1, f1);
+        rec_store(d + 2, q0);
+        rec_store(d + 3, q1);
+        return true;
+    };
+    // A record that meets "busy" waits in the lane's one pending slot and is tried again
+    // at the lane's next record: a collision (two lanes of one wave on one hot tile is
+    // common on centrally concentrated fields) costs one more exchange, not a wave-wide
+    // retry round.  A lane whose pending record fails again retries both in a loop that
+    // exits only when EVERY lane of the wave is done (a wave-uniform exit: a lane holding
+    // "busy" completes its hand-off inside the same iteration, so no lane waits on code
+    // the compiler would sink behind a divergent loop exit).  The retries are bounded (a
+    // never-reached safety net: the record is dropped and counted).
+    bool pend = false;
+    int pt = 0, pp = 0;
+    float4 pq0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pq1 = pq0;
+    auto drain = [&](bool cur, int t, int p, float4 q0, float4 q1) {
         int tries = 0;
         do {
-            if (!done) {
-                const unsigned long long x = atomicExch(&wd[t], (unsigned long long)kParkBusy);
-                const unsigned st = (unsigned)x;
-                const unsigned cc = (unsigned)(x >> 32);
-                if (st == kParkEmpty) {  // park
-                    pa[t] = q0;
-                    pc1[t] = q1.x;
-                    pbox[t] = __float_as_uint(q1.w);
-                    lds_order();  // the record before the state (LDS executes a wave's ops in order)
-                    __hip_atomic_store(&wd[t], ((unsigned long long)cc << 32) | (unsigned)p,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    done = true;
-                } else if (st != kParkBusy) {  // take the parked partner (particle st)
-                    const float4 f0 = pa[t];
-                    const float4 f1 = make_float4(pc1[t], __int_as_float((int)st),
-                                                  rec_band(g.mgl, f0.z), __uint_as_float(pbox[t]));
-                    lds_order();  // the partner's reads before the slot is released
-                    __hip_atomic_store(&wd[t], ((unsigned long long)(cc + 2) << 32) | kParkEmpty,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    float4* d = recs + 2 * (long long)cc;
-                    rec_store(d, f0);
-                    rec_store(d + 1, f1);
-                    rec_store(d + 2, q0);
-                    rec_store(d + 3, q1);
-                    done = true;
-                } else if (++tries > (1 << 22)) {  // busy far too long: give up
-                    atomicAdd(&ctr[cPairFail], 1);
-                    done = true;
+            if (pend || cur) {
+                if (pend && try_insert(pt, pp, pq0, pq1)) pend = false;
+                if (cur && !pend && try_insert(t, p, q0, q1)) cur = false;
+                if ((pend || cur) && ++tries > (1 << 22)) {
+                    atomicAdd(&ctr[cPairFail], (int)pend + (int)cur);
+                    pend = cur = false;
                 }
             }
-        } while (__ballot(!done) != 0ull);
+        } while (__ballot(pend || cur) != 0ull);
+    };
+    auto pair_insert = [&](int t, int p, float4 q0, float4 q1) {
+        if (pend && try_insert(pt, pp, pq0, pq1)) pend = false;
+        if (!pend) {
+            if (!try_insert(t, p, q0, q1)) {
+                pend = true;
+                pt = t;
+                pp = p;
+                pq0 = q0;
+                pq1 = q1;
+            }
+        } else {
+            drain(true, t, p, q0, q1);
+        }
     };
     const long long gcnt = min((long long)grp, nblk - sb * grp);
     auto batch_base = [&](long long c) { return ((c / gcnt) * nblk + sb * grp + c % gcnt) * kBatch; };
@@ -609,6 +646,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter_pair(
             pV[k] = nV[k];
         }
     }
+    drain(false, 0, 0, pq0, pq1);  // the pending records
     __syncthreads();
     // flush: a parked record gets a hole as its partner; the padding slots up to the run's
     // end (the next scatter workgroup's first count row, or the tile's end) become holes
@@ -1353,68 +1391,69 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
     const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
     tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
     const int lane = threadIdx.x & 63;
-    {
-        int* dlist = defer_lds[threadIdx.x >> 6];
-        int ndef = 0;  // wave-uniform
-        // Software pipeline: batch i + 2 is issued before batch i deposits.  The loads are
-        // unconditional (index clamped to the item's last record; lanes past the end ignore
-        // theirs), so every iteration issues the same two loads and the compiler's wait
-        // before batch i leaves the batch just issued in flight (vmcnt(2); the register
-        // rotation makes it wait for batch i + 1 too).  Loads under a branch made it
-        // vmcnt(0), i.e. one full memory latency per batch: deposit 1.26 -> 1.22 ms (cfg 3).
-        const int last = it.count - 1;
-        float4 r0, r1, q0, q1;
-        load_rec(recs, it.start + min((int)threadIdx.x, last), r0, r1);
-        load_rec(recs, it.start + min((int)threadIdx.x + kDepBlock, last), q0, q1);
-        for (int base = 0; base < it.count; base += kDepBlock) {
-            int i = base + threadIdx.x;
-            float4 n0, n1;
-            load_rec(recs, it.start + min(i + 2 * kDepBlock, last), n0, n1);
-            Prep P;
-            P.b = Box{0, -1, 0, -1};
-            bool live = i < it.count;
-            if (live) rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
-            live = live && P.b.x0 <= P.b.x1;  // not a hole (padding slot)
-            r0 = q0;
-            r1 = q1;
-            q0 = n0;
-            q1 = n1;
-            const int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
-            const bool small = live && is_small(bw, bh);
-            bool amb = false;
-            if (small) {
-                // lane-per-record.  Boxes of <= 3 x 3 corners (pixel-scale h) take the
-                // packed body; 4-wide boxes and records with a pair in the error band are
-                // deferred to the exact body, a full wave of them at a time
-                if (bw <= 3 && bh <= 3)
-                    amb = !small3_fast<KID, NOUT, ACC>(P, bw, bh, X0, Y0, xt, yt, acc0, acc1);
-                else
-                    amb = true;
-            }
-            {
-                unsigned long long am = __ballot(amb);
-                if (am) {
-                    if (amb) dlist[ndef + __popcll(am & ((1ull << lane) - 1ull))] = i;
-                    ndef += __popcll(am);
-                    if (ndef >= 64) {  // a full wave of deferred records
-                        ndef -= 64;
-                        deferred<KID, NOUT, ACC>(g, s, recs, it.start, dlist, ndef, 64, X0, Y0,
-                                                 kk, xt, yt, acc0, acc1, lane);
-                    }
+    int* dlist = defer_lds[threadIdx.x >> 6];
+    int ndef = 0;  // wave-uniform
+    // One batch: record i (index within the item; r0, r1 its halves) of every thread.
+    auto batch = [&](int i, const float4& r0, const float4& r1) {
+        Prep P;
+        P.b = Box{0, -1, 0, -1};
+        bool live = i < it.count;
+        if (live) rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
+        live = live && P.b.x0 <= P.b.x1;  // not a hole (padding slot)
+        const int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
+        const bool small = live && is_small(bw, bh);
+        bool amb = false;
+        if (small) {
+            // lane-per-record.  Boxes of <= 3 x 3 corners (pixel-scale h) take the packed
+            // body; 4-wide boxes and records with a pair in the error band are deferred to
+            // the exact body, a full wave of them at a time
+            if (bw <= 3 && bh <= 3)
+                amb = !small3_fast<KID, NOUT, ACC>(P, bw, bh, X0, Y0, xt, yt, acc0, acc1);
+            else
+                amb = true;
+        }
+        {
+            unsigned long long am = __ballot(amb);
+            if (am) {
+                if (amb) dlist[ndef + __popcll(am & ((1ull << lane) - 1ull))] = i;
+                ndef += __popcll(am);
+                if (ndef >= 64) {  // a full wave of deferred records
+                    ndef -= 64;
+                    deferred<KID, NOUT, ACC>(g, s, recs, it.start, dlist, ndef, 64, X0, Y0, kk,
+                                             xt, yt, acc0, acc1, lane);
                 }
             }
-            unsigned long long mid = __ballot(live && !small);
-            while (mid) {
-                int l = __builtin_ctzll(mid);
-                mid &= mid - 1;
-                Prep Q = bcast_prep(P, l);
-                sweep<KID, NOUT, ACC>(g, s, Q, X0, Y0, xt, yt, acc0, acc1, lane);
-            }
         }
-        if (ndef > 0)
-            deferred<KID, NOUT, ACC>(g, s, recs, it.start, dlist, 0, ndef, X0, Y0, kk, xt, yt,
-                                     acc0, acc1, lane);
+        unsigned long long mid = __ballot(live && !small);
+        while (mid) {
+            int l = __builtin_ctzll(mid);
+            mid &= mid - 1;
+            Prep Q = bcast_prep(P, l);
+            sweep<KID, NOUT, ACC>(g, s, Q, X0, Y0, xt, yt, acc0, acc1, lane);
+        }
+    };
+    const int last = it.count - 1;
+    // Software pipeline: batch i + 2 is issued before batch i deposits.  The loads are
+    // unconditional (index clamped to the item's last record; lanes past the end ignore
+    // theirs), so every iteration issues the same two loads and the compiler's wait
+    // before batch i leaves the batch just issued in flight (vmcnt(2); the register
+    // rotation makes it wait for batch i + 1 too).  Loads under a branch made it
+    // vmcnt(0), i.e. one full memory latency per batch: deposit 1.26 -> 1.22 ms (cfg 3).
+    float4 r0, r1, q0, q1;
+    load_rec(recs, it.start + min((int)threadIdx.x, last), r0, r1);
+    load_rec(recs, it.start + min((int)threadIdx.x + kDepBlock, last), q0, q1);
+    for (int base = 0; base < it.count; base += kDepBlock) {
+        float4 n0, n1;
+        load_rec(recs, it.start + min(base + (int)threadIdx.x + 2 * kDepBlock, last), n0, n1);
+        batch(base + threadIdx.x, r0, r1);
+        r0 = q0;
+        r1 = q1;
+        q0 = n0;
+        q1 = n1;
     }
+    if (ndef > 0)
+        deferred<KID, NOUT, ACC>(g, s, recs, it.start, dlist, 0, ndef, X0, Y0, kk, xt, yt, acc0,
+                                 acc1, lane);
     __syncthreads();
     if (it.slab >= 0) {  // split tile: partial sums, merged by K5 (slab layout unpadded)
         unsigned long long* dst = slabs + (long long)it.slab * NOUT * kTilePix;
@@ -2005,19 +2044,14 @@ static int allow_lds(K kern, size_t bytes) {
 }
 
 // K3 on stream st.  rec_cap / wide_cap: the capacities the kernel checks against the
-// device counters (speculative launch; see project2d).  fp64 accumulation scatters the
-// small / mid-size stream as 64-B pairs (k_scatter_pair); fixed point keeps k_scatter,
-// whose per-tile maxima need the LDS the pairs take (ASP_SCATTER_PAIRS=0 forces it).
+// device counters (speculative launch; see project2d).  k_scatter, or with
+// scatter_pairs() the 64-B pair scatter k_scatter_pair.
 template <int KID, int NOUT, int ACC, bool CULL, int SRC, int PROBE>
 static int scatter_variant(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl,
                            const float* u, const float* v, const float* h, const float* a0,
                            const float* a1, long long rec_cap, int wide_cap, hipStream_t st) {
     int* dc = (int*)ws.counters.p;
-    static const bool pairs_off = [] {
-        const char* e = getenv("ASP_SCATTER_PAIRS");
-        return e && atoi(e) == 0;
-    }();
-    if (ACC == kAccF64 && !pairs_off && scatter_pair_lds(g) <= 163840) {
+    if (ACC == kAccF64 && scatter_pairs(g, false)) {
         auto kern = k_scatter_pair<KID, NOUT, CULL, SRC, PROBE>;
         ASP_TRY(allow_lds(kern, scatter_pair_lds(g)));
         hipLaunchKernelGGL(kern, dim3((unsigned)pl.nblk_s), dim3(kScatterBlock),
@@ -2089,8 +2123,7 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
     {
         StageMark m(ws, kSDeposit, st);
         const size_t lds = deposit_lds<NOUT>();
-        hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(pl.n_items), dim3(kDepBlock),
-                           lds, st, g, s, (const float4*)ws.recs.p,
+        hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(pl.n_items), dim3(kDepBlock), lds, st, g, s, (const float4*)ws.recs.p,
                            (const Item*)ws.items.p, (const int*)ws.iorder.p, (const int2*)ws.tile_k.p,
                            (unsigned long long*)ws.slabs.p, o0, o1, dflags);
         ASP_LAUNCHED();
@@ -2198,7 +2231,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
         hipLaunchKernelGGL(g.nonsquare || g.mixed ? k_count<true> : k_count<false>,
                            dim3((unsigned)pl.nblk), dim3(kCountBlock),
                            (size_t)2 * g.ntiles * sizeof(int), st, du, dv, dh, n, pl.nblk, g, s,
-                           (int*)ws.hist.p, dc);
+                           (int*)ws.hist.p, dc, (int)scatter_pairs(g, det));
         ASP_LAUNCHED();
         m.done();
     }
@@ -2214,7 +2247,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
         StageMark m(ws, kSTilescan, st);
         hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
                            (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles, 2,
-                           (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p, dc);
+                           (int)scatter_pairs(g, det), (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p, dc);
         ASP_LAUNCHED();
         m.done();
     }
