@@ -60,7 +60,8 @@ struct Grid {
     int nonsquare;    // nx != ny: the y chunk cull is not implied by the r2 test
     int mixed;        // the cull reads other position columns than the pixel test (Src64)
     int wide_tiles;   // particles over more tiles than this take the wide path (K6)
-    int gather_min;   // records with clipped boxes >= this on both axes are gathered (K4)
+    int gather_min;   // records with clipped boxes >= this on both axes are gathered (K4g)
+    int gather_area;  // ... and so are clipped boxes of at least this many pixels
 };
 
 // The caller's particle arrays, resident in HBM, read by particle index where the exact

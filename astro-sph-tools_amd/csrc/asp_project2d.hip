@@ -8,7 +8,7 @@
 //   K1 count     one streaming pass over (u, v, h): per-workgroup LDS histogram of
 //                (particle, GPU tile) insertions -> hist[block][tile], two streams per
 //                tile: records whose box clipped to the tile is small / mid-size, and
-//                LARGE ones (>= gather_min pixels on both axes)
+//                LARGE ones (>= gather_min pixels on both axes, or >= gather_area pixels)
 //   K2a colscan  per tile, exclusive prefix over blocks (in place) + tile totals
 //   K2b tilescan one workgroup: tile start offsets in Morton order of the tiles, the
 //                deposit work list (runs of <= CH records of one tile; empty tiles get
@@ -80,6 +80,11 @@ static_assert(kBatch == (long long)kScatterBlock * kUnroll, "count and scatter b
 // stream (K4g); the threshold is a Grid field so it can be tuned per call
 // (ASP_GATHER_MIN).
 constexpr int kGatherMinDefault = 5;
+// ... or at least this many pixels: the thin slivers of large discs clipped at tile edges,
+// which K4 sweeps a whole wave per record (ASP_GATHER_AREA): cfg 2 at
+// physical h 11.42-11.49 -> 11.10 ms (12-20 alike), the pixel-scale map unchanged at 20
+// (16 sends its 4 x 4 boxes to K4g: 3.25 -> 3.32 ms)
+constexpr int kGatherAreaDefault = 20;
 
 // Vector of U floats (one 4 U-byte load per lane).
 template <int U>
@@ -124,20 +129,21 @@ __device__ __forceinline__ unsigned tile_box(const Box& b, int tx, int ty) {
     return x0 | (x1 << 8) | (y0 << 16) | (y1 << 24);
 }
 
-__device__ __forceinline__ bool box_large(unsigned bp, int gmin) {
+__device__ __forceinline__ bool box_large(unsigned bp, const Grid& g) {
     int bw = (int)((bp >> 8) & 255u) - (int)(bp & 255u) + 1;
     int bh = (int)(bp >> 24) - (int)((bp >> 16) & 255u) + 1;
-    return bw >= gmin && bh >= gmin;
+    return (bw >= g.gather_min && bh >= g.gather_min) || bw * bh >= g.gather_area;
 }
 
 // Histogram column of a (particle, tile) insertion: t (small / mid-size stream) or
 // t + ntiles (large stream, gathered by K4g).  `maybe`: the unclipped box is large.
 __device__ __forceinline__ int column(const Grid& g, const Box& b, bool maybe, int tx, int ty) {
     const int t = tx * g.nty + ty;
-    return maybe && box_large(tile_box(b, tx, ty), g.gather_min) ? t + g.ntiles : t;
+    return maybe && box_large(tile_box(b, tx, ty), g) ? t + g.ntiles : t;
 }
 __device__ __forceinline__ bool maybe_large(const Grid& g, const Box& b) {
-    return b.x1 - b.x0 + 1 >= g.gather_min && b.y1 - b.y0 + 1 >= g.gather_min;
+    const int bw = b.x1 - b.x0 + 1, bh = b.y1 - b.y0 + 1;  // unclipped: an upper bound
+    return (bw >= g.gather_min && bh >= g.gather_min) || (long long)bw * bh >= g.gather_area;
 }
 
 // ----------------------------------------------------------------------------------
@@ -360,7 +366,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             auto insert = [&](int tx, int ty, bool first) {
                 const int t = tx * g.nty + ty;
                 const unsigned bp = tile_box(b, tx, ty);
-                const int col = mb && box_large(bp, g.gather_min) ? t + g.ntiles : t;
+                const int col = mb && box_large(bp, g) ? t + g.ntiles : t;
                 int slot = atomicAdd(&cur[col], 1);
                 if constexpr (ACC == kAccFix) {
                     atomicMax(&cm[t * NOUT], c0);
@@ -626,7 +632,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter_pair(
                                                   (float)(V - corner_y(g, max(b.y0, ty * kTile))),
                                                   ph[k], cf0);
                     const float4 q1 = make_float4(cf1, __int_as_float(p), band, __uint_as_float(bp));
-                    if (mb && box_large(bp, g.gather_min)) {
+                    if (mb && box_large(bp, g)) {
                         const int slot = atomicAdd(&cur1[t], 1);
                         rec_store(&recs[2 * (long long)slot], q0);
                         rec_store(&recs[2 * (long long)slot + 1], q1);
@@ -1476,7 +1482,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
 
 // ----------------------------------------------------------------------------------
 // K4g: deposit one work item of the LARGE stream (records whose clipped box is at least
-// gather_min pixels on both axes) in the gather form: every wave streams the item's
+// gather_min pixels on both axes, or gather_area pixels) in the gather form: every wave streams the item's
 // records 64 at a time (coalesced 32-B loads, the next 64 in flight) and walks those that
 // meet its region (gather_walk).  The tile (or its partial slab) is written straight
 // from the registers.
@@ -1989,6 +1995,7 @@ bool make_grid(double x_min, double x_max, double y_min, double y_max, int nx, i
     g.mixed = 0;
     g.wide_tiles = kWideTilesDefault;
     g.gather_min = kGatherMinDefault;
+    g.gather_area = kGatherAreaDefault;
     return true;
 }
 
@@ -2174,6 +2181,7 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
 static void grid_tunables(Grid& g) {
     if (const char* e = getenv("ASP_WIDE_TILES")) g.wide_tiles = std::max(1, atoi(e));
     if (const char* e = getenv("ASP_GATHER_MIN")) g.gather_min = std::max(2, atoi(e));
+    if (const char* e = getenv("ASP_GATHER_AREA")) g.gather_area = std::max(4, atoi(e));
 }
 
 // The projection on DEVICE arrays (fp32 working copies u, v, h, a0, a1; s: the caller's

@@ -401,16 +401,20 @@ def test_default_vs_deterministic_modes(gpu):
     assert_map_close(b, a, abs_tol=1e-6, rel_tol=1e-5)
 
 
-@pytest.mark.parametrize("gmin", ["5", "12", "65"])
-def test_large_stream_threshold(gpu, oracle, gmin, monkeypatch):
-    """Records whose box clipped to a tile spans >= gather_min pixels on both axes go to
-    the large stream and are GATHERED (K4g: LDS list, register sums); the rest are
-    swept or deposited lane-per-record (K4).  Any threshold must give the same neighbour
-    counts (bit-exact) and values within tolerance: 5 sends almost every non-small box
-    to K4g, 65 none.  Tiles holding both streams are split items merged by K5."""
+@pytest.mark.parametrize("gmin,area", [("5", "20"), ("12", "20"), ("65", "1073741824"),
+                                       ("65", "20"), ("65", "6")])
+def test_large_stream_threshold(gpu, oracle, gmin, area, monkeypatch):
+    """Records whose box clipped to a tile spans >= gather_min pixels on both axes, or at
+    least gather_area pixels, go to the large stream and are GATHERED (K4g: register
+    sums); the rest are swept or deposited lane-per-record (K4).  Any thresholds must give
+    the same neighbour counts (bit-exact) and values within tolerance: 5 sends almost
+    every non-small box to K4g, 65 with the area test off none, 65 with area 20 only the
+    thin slivers of large discs clipped at tile edges, area 6 also most small boxes.
+    Tiles holding both streams are split items merged by K5."""
     from asp_amd.device import stats
     from asp_amd.tools.projections import create_image, create_weighted_image, indicator_kernel
     monkeypatch.setenv("ASP_GATHER_MIN", gmin)
+    monkeypatch.setenv("ASP_GATHER_AREA", area)
     rng = np.random.default_rng(11)
     n = 6000
     pos = rng.normal(0, 0.4, (n, 3))
@@ -420,7 +424,7 @@ def test_large_stream_threshold(gpu, oracle, gmin, monkeypatch):
     G, ext = 512, (-1.0, 1.0, -1.0, 1.0)
     cnt = create_image(pos, h, np.ones(n), (G, G), 64, 2, *ext, kernel_func=indicator_kernel)
     large = stats(0)["large"]
-    assert (large == 0) == (gmin == "65")
+    assert (large == 0) == (gmin == "65" and int(area) > 1 << 20)
     want, _ = oracle.project_scatter(pos[:, 0], pos[:, 1], h, np.ones(n), None, (G, G), 64,
                                      *ext, kernel="indicator")
     assert np.array_equal(cnt, want)
