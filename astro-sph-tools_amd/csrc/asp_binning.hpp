@@ -146,6 +146,46 @@ static __device__ __forceinline__ void block_scan_ll(long long* s, int tid) {
     __syncthreads();
 }
 
+// Exclusive scan of M values per thread over the block in one pass (shared barriers): x[m]
+// becomes the sum over lower threads, tot[m] the block total.
+template <int M>
+static __device__ __forceinline__ void block_scan_multi(long long (&x)[M], long long (&tot)[M],
+                                                        int tid) {
+    __shared__ long long part[M][kScanThreads / 64];
+    const int lane = tid & 63, w = tid >> 6;
+    long long inc[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        inc[m] = x[m];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            long long y = __shfl_up(inc[m], o);
+            if (lane >= o) inc[m] += y;
+        }
+        if (lane == 63) part[m][w] = inc[m];
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            long long q = lane < kScanThreads / 64 ? part[m][lane] : 0;
+#pragma unroll
+            for (int o = 1; o < kScanThreads / 64; o <<= 1) {
+                long long y = __shfl_up(q, o);
+                if (lane >= o) q += y;
+            }
+            if (lane < kScanThreads / 64) part[m][lane] = q;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        tot[m] = part[m][kScanThreads / 64 - 1];
+        x[m] = (w > 0 ? part[m][w - 1] : 0) + inc[m] - x[m];
+    }
+    __syncthreads();  // part is rewritten by the next scan
+}
+
 // items of one tile: regular ones of ch records, large ones of chl records
 static __device__ __forceinline__ void tile_items(int cs, int cl, int ch, int chl, int& ks,
                                                   int& kl) {
@@ -156,14 +196,16 @@ static __device__ __forceinline__ void tile_items(int cs, int cl, int ch, int ch
 
 constexpr int kScanPer = 16;  // max tiles per scan thread held in registers (<= 16384 tiles)
 
+constexpr int kOrderBuckets = 33;  // log2 classes of counts < 2^31, plus empty items
+
 template <int PER>  // tiles per thread held in registers: ntiles <= PER * kScanThreads
 static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     const int* __restrict__ tile_total, const int* __restrict__ morton, int ntiles, int nstream,
     int pad, long long* __restrict__ tile_start, Item* __restrict__ items, Merge* __restrict__ merges,
-    int* __restrict__ ctr) {
-    __shared__ long long s_rec[kScanThreads], s_item[kScanThreads], s_slab[kScanThreads],
-        s_merge[kScanThreads];
+    int* __restrict__ ctr, int* __restrict__ order, int identity) {
+    __shared__ int ocnt[kOrderBuckets];
     int tid = threadIdx.x;
+    if (tid < kOrderBuckets) ocnt[tid] = 0;
     int per = (ntiles + kScanThreads - 1) / kScanThreads;  // <= kScanPer (host-checked)
     int r0 = min(ntiles, tid * per), r1 = min(ntiles, r0 + per);
     // this thread's tiles, their small- and large-record counts: all loads issued up front
@@ -181,26 +223,20 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     // k_scatter_pair): a tile whose two streams hold an odd total is followed by a gap slot
     // that no item covers
     auto span = [&](int cs, int cl) { return (long long)(cs + cl) + (pad ? ((cs + cl) & 1) : 0); };
-    long long loc = 0, wloc = 0;  // all records; stream-1 records
+    long long sa[2] = {0, 0}, ta[2];  // all records; stream-1 records
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-        loc += span(cs_[q], cl_[q]);
-        wloc += cl_[q];
+        sa[0] += span(cs_[q], cl_[q]);
+        sa[1] += cl_[q];
     }
-    s_rec[tid] = loc;
-    s_item[tid] = wloc;
-    __syncthreads();
-    block_scan_ll(s_rec, tid);
-    block_scan_ll(s_item, tid);
-    long long total = s_rec[kScanThreads - 1];
-    long long total1 = s_item[kScanThreads - 1];
-    const long long base0 = s_rec[tid] - loc;
-    long long base = base0;
+    block_scan_multi<2>(sa, ta, tid);
+    const long long total = ta[0], total1 = ta[1];
+    const long long base0 = sa[0];
     int ch = (int)max((long long)kMinItemRecords,
                       (total - total1 + kTargetItems - 1) / kTargetItems);
     int chl = (int)max((long long)kMinItemRecords1, (total1 + kTargetItems1 - 1) / kTargetItems1);
-    __syncthreads();
-    long long nit = 0, nsl = 0, nmg = 0;
+    long long sb3[3] = {0, 0, 0}, tb[3];  // items, slabs, merges of this thread's tiles
+    long long base = base0;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         if (r0 + q >= r1) continue;
@@ -210,92 +246,96 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
         base += span(cs, cl);
         int ks, kl;
         tile_items(cs, cl, ch, chl, ks, kl);
-        nit += ks + kl;
+        sb3[0] += ks + kl;
         if (ks + kl > 1) {
-            nsl += ks + kl;
-            nmg += 1;
+            sb3[1] += ks + kl;
+            sb3[2] += 1;
         }
     }
-    s_item[tid] = nit;
-    s_slab[tid] = nsl;
-    s_merge[tid] = nmg;
-    __syncthreads();
-    block_scan_ll(s_item, tid);
-    block_scan_ll(s_slab, tid);
-    block_scan_ll(s_merge, tid);
-    long long ib = s_item[tid] - nit, sb = s_slab[tid] - nsl, mb = s_merge[tid] - nmg;
-    base = base0;
+    block_scan_multi<3>(sb3, tb, tid);
+    // this thread's items in order: f(item index, item)
+    auto for_items = [&](auto&& f) {
+        long long ib = sb3[0], sb = sb3[1];
+        long long b = base0;
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        if (r0 + q >= r1) continue;
-        int t = tt[q], cs = cs_[q], cl = cl_[q];
-        int ks, kl;
-        tile_items(cs, cl, ch, chl, ks, kl);
-        int k = ks + kl;
-        long long s0 = base;
-        base += span(cs, cl);
-        for (int j = 0; j < k; ++j) {
-            Item it;
-            bool lg = j >= ks;
-            int jj = lg ? j - ks : j;
-            int c = lg ? cl : cs, chunk = lg ? chl : ch;
-            it.start = (lg ? s0 + cs : s0) + (long long)jj * chunk;
-            it.tile = t;
-            it.count = c > 0 ? min(chunk, c - jj * chunk) : 0;
-            it.slab = k > 1 ? (int)(sb + j) : -1;
-            it.mode = lg ? 1 : 0;
-            items[ib + j] = it;
+        for (int q = 0; q < PER; ++q) {
+            if (r0 + q >= r1) continue;
+            int t = tt[q], cs = cs_[q], cl = cl_[q];
+            int ks, kl;
+            tile_items(cs, cl, ch, chl, ks, kl);
+            int k = ks + kl;
+            long long s0 = b;
+            b += span(cs, cl);
+            for (int j = 0; j < k; ++j) {
+                Item it;
+                bool lg = j >= ks;
+                int jj = lg ? j - ks : j;
+                int c = lg ? cl : cs, chunk = lg ? chl : ch;
+                it.start = (lg ? s0 + cs : s0) + (long long)jj * chunk;
+                it.tile = t;
+                it.count = c > 0 ? min(chunk, c - jj * chunk) : 0;
+                it.slab = k > 1 ? (int)(sb + j) : -1;
+                it.mode = lg ? 1 : 0;
+                f(ib + j, it);
+            }
+            ib += k;
+            if (k > 1) sb += k;
         }
-        ib += k;
-        if (k > 1) {
-            Merge m;
-            m.tile = t;
-            m.slab0 = (int)sb;
-            m.nslab = k;
-            m.pad = 0;
-            merges[mb++] = m;
-            sb += k;
+    };
+    for_items([&](long long i, const Item& it) { items[i] = it; });
+    {  // the merge list
+        long long mb = sb3[2], sb = sb3[1];
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            if (r0 + q >= r1) continue;
+            int ks, kl;
+            tile_items(cs_[q], cl_[q], ch, chl, ks, kl);
+            int k = ks + kl;
+            if (k > 1) {
+                Merge m;
+                m.tile = tt[q];
+                m.slab0 = (int)sb;
+                m.nslab = k;
+                m.pad = 0;
+                merges[mb++] = m;
+                sb += k;
+            }
+        }
+    }
+    // K2c, dispatch order of the deposit work items -- largest first (longest-processing-
+    // time scheduling: the items of the dense central tiles used to start late in Morton
+    // order and finish last): items bucketed by floor(log2(count)), buckets in decreasing
+    // size, order within a bucket unspecified.  order[b] = the item workgroup b takes.
+    // (Was a kernel of its own on the critical path before the deposit.)
+    if (order) {
+        auto bucket = [](int c) { return c <= 0 ? kOrderBuckets - 1 : __builtin_clz((unsigned)c) - 1; };
+        if (identity) {  // A/B switch (ASP_ITEM_ORDER=0): Morton order as produced
+            for_items([&](long long i, const Item&) { order[i] = (int)i; });
+        } else {
+            for_items([&](long long, const Item& it) { atomicAdd(&ocnt[bucket(it.count)], 1); });
+            __syncthreads();
+            if (tid == 0) {
+                int s = 0;
+                for (int b = 0; b < kOrderBuckets; ++b) {
+                    const int c = ocnt[b];
+                    ocnt[b] = s;
+                    s += c;
+                }
+            }
+            __syncthreads();
+            for_items([&](long long i, const Item& it) {
+                order[atomicAdd(&ocnt[bucket(it.count)], 1)] = (int)i;
+            });
         }
     }
     if (tid == kScanThreads - 1) {
-        ctr[cItems] = (int)s_item[kScanThreads - 1];
+        ctr[cItems] = (int)tb[0];
         ctr[cRecs] = (int)min(total, (long long)0x7fffffff);
         ctr[cChunk] = ch;
-        ctr[cSlabs] = (int)s_slab[kScanThreads - 1];
-        ctr[cMerges] = (int)s_merge[kScanThreads - 1];
+        ctr[cSlabs] = (int)tb[1];
+        ctr[cMerges] = (int)tb[2];
         ctr[cLarge] = (int)min(total1, (long long)0x7fffffff);
     }
-}
-
-// ----------------------------------------------------------------------------------
-// K2c: dispatch order of the deposit work items -- largest first (longest-processing-time
-// scheduling: the items of the dense central tiles used to start late in Morton order and
-// finish last).  One workgroup; items bucketed by floor(log2(count)), buckets in
-// decreasing size, order within a bucket unspecified.  order[b] = the item workgroup b
-// takes.
-// ----------------------------------------------------------------------------------
-constexpr int kOrderBuckets = 33;  // log2 classes of counts < 2^31, plus empty items
-[[maybe_unused]] static __global__ __launch_bounds__(kScanThreads) void k_item_order(
-    const Item* __restrict__ items, int n, int* __restrict__ order, int identity) {
-    __shared__ int cnt[kOrderBuckets], start[kOrderBuckets];
-    if (identity) {  // A/B switch (ASP_ITEM_ORDER=0): Morton order as produced
-        for (int i = threadIdx.x; i < n; i += kScanThreads) order[i] = i;
-        return;
-    }
-    if (threadIdx.x < kOrderBuckets) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    auto bucket = [](int c) { return c <= 0 ? kOrderBuckets - 1 : __builtin_clz((unsigned)c) - 1; };
-    for (int i = threadIdx.x; i < n; i += kScanThreads) atomicAdd(&cnt[bucket(items[i].count)], 1);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int s = 0;
-        for (int b = 0; b < kOrderBuckets; ++b) {
-            start[b] = s;
-            s += cnt[b];
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += kScanThreads) order[atomicAdd(&start[bucket(items[i].count)], 1)] = i;
 }
 
 }  // namespace asp

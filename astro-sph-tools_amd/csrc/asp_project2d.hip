@@ -1378,7 +1378,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
     float* xt = (float*)(acc + NOUT * kTileWords);
     float* yt = xt + kTile;
     __shared__ int defer_lds[kDepBlock / 64][kDeferCap];
-    const Item it = items[order[blockIdx.x]];  // largest items first (k_item_order)
+    const Item it = items[order[blockIdx.x]];  // largest items first (k_tilescan)
     if (it.mode != 0) return;  // the large stream's (K4g)
     int tx = it.tile / g.nty, ty = it.tile - (it.tile / g.nty) * g.nty;
     int X0 = tx * kTile, Y0 = ty * kTile;
@@ -2030,6 +2030,14 @@ struct Plan {
 };
 
 // items / merges in the work-list buffers
+// Deposit items in tilescan order (ASP_ITEM_ORDER=0, an A/B switch) instead of largest first.
+static int item_order_identity() {
+    static const int identity = [] {
+        const char* e = getenv("ASP_ITEM_ORDER");
+        return e && atoi(e) == 0 ? 1 : 0;
+    }();
+    return identity;
+}
 static inline size_t item_cap(const Grid& g) { return (size_t)2 * g.ntiles + kTargetItems + kTargetItems1 + 16; }
 static inline size_t merge_cap(const Grid& g) { return (size_t)g.ntiles + 16; }
 
@@ -2116,16 +2124,6 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
                            (const int*)ws.tile_total.p, (int2*)ws.tile_k.p);
         ASP_LAUNCHED();
         m.done();
-    }
-    {  // largest work items first
-        ASP_TRY(ensure(ws.iorder, (size_t)std::max(1, pl.n_items) * sizeof(int)));
-        static const int identity = [] {
-            const char* e = getenv("ASP_ITEM_ORDER");
-            return e && atoi(e) == 0 ? 1 : 0;
-        }();
-        hipLaunchKernelGGL(k_item_order, dim3(1), dim3(kScanThreads), 0, st,
-                           (const Item*)ws.items.p, pl.n_items, (int*)ws.iorder.p, identity);
-        ASP_LAUNCHED();
     }
     {
         StageMark m(ws, kSDeposit, st);
@@ -2229,6 +2227,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     ASP_TRY(ensure(ws.tile_start, (size_t)2 * g.ntiles * sizeof(long long)));
     ASP_TRY(ensure(ws.tile_k, (size_t)g.ntiles * sizeof(int2)));
     ASP_TRY(ensure(ws.items, item_cap(g) * sizeof(Item)));
+    ASP_TRY(ensure(ws.iorder, item_cap(g) * sizeof(int)));  // deposit order (k_tilescan)
     ASP_TRY(ensure(ws.merges, merge_cap(g) * sizeof(Merge)));
     ASP_TRY(ensure(ws.counters, (size_t)cNum * sizeof(int)));
     if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, kMarks * cNum * sizeof(int)));
@@ -2255,7 +2254,8 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
         StageMark m(ws, kSTilescan, st);
         hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
                            (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles, 2,
-                           (int)scatter_pairs(g, det), (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p, dc);
+                           (int)scatter_pairs(g, det), (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p, dc,
+                           (int*)ws.iorder.p, item_order_identity());
         ASP_LAUNCHED();
         m.done();
     }

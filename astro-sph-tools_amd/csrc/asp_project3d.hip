@@ -647,12 +647,12 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
             hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
                            (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1, 0,
                            (long long*)ws.tile_start.p, (Item*)ws.items.p,
-                           (Merge*)ws.merges.p, dc);
+                           (Merge*)ws.merges.p, dc, (int*)nullptr, 0);
         else
             hipLaunchKernelGGL(k_tilescan<kScanPer>, dim3(1), dim3(kScanThreads), 0, st,
                            (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1, 0,
                            (long long*)ws.tile_start.p, (Item*)ws.items.p,
-                           (Merge*)ws.merges.p, dc);
+                           (Merge*)ws.merges.p, dc, (int*)nullptr, 0);
         ASP_LAUNCHED();
         m.done();
     }
