@@ -5,7 +5,7 @@
 # on) and the rocprof kernel stats of the same bench command (tools/gpu/bench_final.sh).
 cd "$GRAFT_REPO_ROOT" || exit 9
 export TMPDIR=/tmp
-cp profiles/pmc_latest.json gpurun_out/pmc_latest.json
+mkdir -p gpurun_out/final && cp profiles/pmc_latest.json gpurun_out/pmc_latest.json
 bash tools/gpu/prof_full.sh r03cfg3 || exit 1
 python3 tools/pmc_summary.py gpurun_out/prof_r03cfg3 --json gpurun_out/pmc_latest.json \
   --key n100000000_g4096_wendland_c2_pixel_weighted \
@@ -16,6 +16,7 @@ python3 tools/pmc_summary.py gpurun_out/prof_r03cfg2p --json gpurun_out/pmc_late
   --source "rocprofv3 PMC passes, tools/gpu/r03/evidence.sh (prof_full.sh r03cfg2p), round 3" > /dev/null || exit 4
 cp gpurun_out/pmc_latest.json profiles/pmc_latest.json
 bash tools/gpu/bench_final.sh || exit 5
+mkdir -p gpurun_out/final
 timeout -k 10 300 python bench.py --cpu-baseline off --n 10000000 --grid 2048 --kernel cubic --map surface --h-law physical > gpurun_out/final/bench_cfg2_physical.json 2> gpurun_out/final/bench_cfg2_physical.err || exit 6
 timeout -k 10 300 python bench.py --cpu-baseline off --n 10000000 --grid 2048 --kernel cubic --map surface > gpurun_out/final/bench_cfg2_pixel.json 2> gpurun_out/final/bench_cfg2_pixel.err || exit 7
 timeout -k 10 300 python bench.py --workload cube > gpurun_out/final/bench_cube.json 2> gpurun_out/final/bench_cube.err || exit 8
