@@ -23,7 +23,7 @@ enum Ctr {
     cWideMax0 = 7,  // max |c0| over wide particles, fp32 bits (K3)
     cWideMax1 = 8,  // max |c1| over wide particles, fp32 bits (K3)
     cLarge = 9,     // records in the large stream (K2b)
-    cPairFail = 10, // k_scatter_pair records dropped by its retry bound (never expected)
+    cPairFail = 10, // (unused since the pair scatter was removed, round 3)
     cNum = 16
 };
 
@@ -219,9 +219,8 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
         cs_[q] = in ? tile_total[tt[q]] : 0;
         cl_[q] = in && nstream == 2 ? tile_total[tt[q] + ntiles] : 0;
     }
-    // pad: every tile's run starts on an even slot (a 64-B pair boundary, for
-    // k_scatter_pair): a tile whose two streams hold an odd total is followed by a gap slot
-    // that no item covers
+    // pad: every tile's run starts on an even slot (a tile whose two streams hold an odd
+    // total is followed by a gap slot that no item covers); unused (0) since round 3
     auto span = [&](int cs, int cl) { return (long long)(cs + cl) + (pad ? ((cs + cl) & 1) : 0); };
     long long sa[2] = {0, 0}, ta[2];  // all records; stream-1 records
 #pragma unroll

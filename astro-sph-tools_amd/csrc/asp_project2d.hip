@@ -155,7 +155,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
                                                        const float* __restrict__ h,
                                                        long long n, long long nblk, Grid g,
                                                        Src64 s, int* __restrict__ hist,
-                                                       int* __restrict__ ctr, int pad) {
+                                                       int* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) int lh[];  // 2 * ntiles columns
     for (int t = threadIdx.x; t < 2 * g.ntiles; t += kCountBlock) lh[t] = 0;
     __syncthreads();
@@ -203,15 +203,9 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
     }
     if (nwide) atomicAdd(&ctr[cWideCount], nwide);
     __syncthreads();
-    // pad: small / mid-size runs padded to even counts, so that every run starts and ends
-    // on a 64-B pair boundary (k_scatter_pair; the padding slots are written as holes)
     int* row = hist + (long long)blockIdx.x * 2 * g.ntiles;
-    for (int t = threadIdx.x; t < 2 * g.ntiles; t += kCountBlock)
-        row[t] = pad && t < g.ntiles ? (lh[t] + 1) & ~1 : lh[t];
+    for (int t = threadIdx.x; t < 2 * g.ntiles; t += kCountBlock) row[t] = lh[t];
 }
-
-// A hole record (padding slot of a small / mid-size run): box x0 = 255 > x1 = 0, no pixel.
-constexpr unsigned kHoleBox = 0x00ff00ffu;
 
 // Record stores of the scatter: plain stores (non-temporal ones measured 2x slower, the
 // L2 merges the 32-B halves of a line).
@@ -435,250 +429,6 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     if constexpr (ACC == kAccFix) {
         unsigned* out = cmx + (long long)blockIdx.x * g.ntiles * NOUT;  // per scatter block
         for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kScatterBlock) out[t] = cm[t];
-    }
-    // the small / mid-size runs' padding slots (k_count) become holes (an empty box)
-    const long long nrow = min((sb + 1) * grp, nblk);
-    for (int t = threadIdx.x; t < g.ntiles; t += kScatterBlock) {
-        const int end = (int)tile_start[t] + (nrow < nblk ? hist[nrow * 2 * g.ntiles + t] : tile_total[t]);
-        for (int cc = cur[t]; cc < end; ++cc) {
-            rec_store(&recs[2 * (long long)cc], make_float4(0.0f, 0.0f, 1.0f, 0.0f));
-            rec_store(&recs[2 * (long long)cc + 1],
-                      make_float4(0.0f, __int_as_float(0), 0.0f, __uint_as_float(kHoleBox)));
-        }
-    }
-}
-
-// ----------------------------------------------------------------------------------
-// K3p: the scatter writing the small / mid-size stream as 64-B PAIRS (fp64 accumulation).
-// The scatter's cost is the number of scattered write locations: the same
-// records written as 64-B-aligned pairs of a (workgroup, tile) run take half the
-// locations.  Each tile has one LDS park slot and one 64-bit word {run cursor, state}
-// (state: empty, busy, or the parked record's particle index).  A record EXCHANGES the
-// word with "busy" -- one LDS atomic decides everything: empty -> it parks its record and
-// stores {cursor, its index}; parked -> it takes the partner, stores {cursor + 2, empty}
-// and writes both records to slots cursor, cursor + 1; busy (another lane mid-handoff) ->
-// retry.  No barriers (tools/microbench/pairs.hip: 10^8 records 1.11 ms, vs 2.40 for
-// single 32-B records and 1.83 for barrier-synchronised rank rounds).  Runs of the small /
-// mid-size stream are even (k_count pads every count workgroup's count, k_tilescan aligns
-// every tile's start); a record still parked at the end is written with a hole (an empty
-// box) as its partner, and the run's remaining padding slots become holes.  Large-stream
-// records are written directly.  LDS per tile: the parked record (24 B: p lives in the
-// state, band is recomputed from h), the word, the large stream's cursor -- 36 B, 144 KiB
-// at 4096 tiles; one workgroup per CU as before.
-// ----------------------------------------------------------------------------------
-// Compiler ordering of LDS accesses only.  A wave's LDS operations execute in issue
-// order, so a park slot's record stores precede its state store (and a taker's reads
-// precede its release) without a fence -- a release fence would also wait for every
-// global load in flight (s_waitcnt vmcnt(0)): the next batch's prefetch, every record.
-__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
-
-constexpr unsigned kParkEmpty = 0xffffffffu;  // park states; a parked record: its index
-constexpr unsigned kParkBusy = 0xfffffffeu;
-static inline size_t scatter_pair_lds(const Grid& g) { return (size_t)g.ntiles * 36; }
-
-// The pair scatter is opt-in (ASP_SCATTER_PAIRS=1; fp64 accumulation, its LDS fits): on
-// the Plummer bench field it measured slower than single records.
-static bool scatter_pairs(const Grid& g, bool det) {
-    static const bool on = [] {
-        const char* e = getenv("ASP_SCATTER_PAIRS");
-        return e && atoi(e) != 0;
-    }();
-    return on && !det && scatter_pair_lds(g) <= 163840;
-}
-
-template <int KID, int NOUT, bool CULL, int SRC, int PROBE>
-__global__ __launch_bounds__(kScatterBlock) void k_scatter_pair(
-    const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
-    const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long nblk,
-    Grid g, Src64 s, const int* __restrict__ hist, const long long* __restrict__ tile_start,
-    const int* __restrict__ tile_total, float4* __restrict__ recs, int* __restrict__ wide_list,
-    int* __restrict__ ctr, int grp, long long rec_cap, int wide_cap) {
-    // speculative launch: see k_scatter
-    if (ctr[cRecs] > rec_cap || ctr[cWideCount] > wide_cap) return;
-    extern __shared__ __attribute__((aligned(16))) float4 pa[];  // parked {lu, lv, h, c0}
-    const int nt = g.ntiles;
-    unsigned long long* wd = (unsigned long long*)(pa + nt);  // {small / mid cursor, state}
-    float* pc1 = (float*)(wd + nt);                           // parked c1
-    unsigned* pbox = (unsigned*)(pc1 + nt);                   // parked box
-    int* cur1 = (int*)(pbox + nt);                            // large-stream cursors
-    const long long sb = blockIdx.x;
-    const int* row = hist + sb * grp * 2 * nt;
-    for (int t = threadIdx.x; t < nt; t += kScatterBlock) {
-        wd[t] = ((unsigned long long)(unsigned)((int)tile_start[t] + row[t]) << 32) | kParkEmpty;
-        cur1[t] = (int)tile_start[t + nt] + row[t + nt];
-    }
-    __syncthreads();
-    // One attempt: EXCHANGE the tile's word with "busy"; empty -> park, parked -> take the
-    // partner and write the pair, busy (another lane mid-hand-off) -> false.  Never loops,
-    // so a lane never spins inside divergent control flow.
-    auto try_insert = [&](int t, int p, float4 q0, float4 q1) -> bool {
-        const unsigned long long x = atomicExch(&wd[t], (unsigned long long)kParkBusy);
-        const unsigned st = (unsigned)x;
-        const unsigned cc = (unsigned)(x >> 32);
-        if (st == kParkEmpty) {  // park
-            pa[t] = q0;
-            pc1[t] = q1.x;
-            pbox[t] = __float_as_uint(q1.w);
-            lds_order();  // the record before the state (LDS executes a wave's ops in order)
-            __hip_atomic_store(&wd[t], ((unsigned long long)cc << 32) | (unsigned)p,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            return true;
-        }
-        if (st == kParkBusy) return false;
-        // take the parked partner (particle st)
-        const float4 f0 = pa[t];
-        const float4 f1 = make_float4(pc1[t], __int_as_float((int)st), rec_band(g.mgl, f0.z),
-                                      __uint_as_float(pbox[t]));
-        lds_order();  // the partner's reads before the slot is released
-        __hip_atomic_store(&wd[t], ((unsigned long long)(cc + 2) << 32) | kParkEmpty,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        float4* d = recs + 2 * (long long)cc;
-        rec_store(d, f0);
-        rec_store(d + 1, f1);
-        rec_store(d + 2, q0);
-        rec_store(d + 3, q1);
-        return true;
-    };
-    // A record that meets "busy" waits in the lane's one pending slot and is tried again
-    // at the lane's next record: a collision (two lanes of one wave on one hot tile is
-    // common on centrally concentrated fields) costs one more exchange, not a wave-wide
-    // retry round.  A lane whose pending record fails again retries both in a loop that
-    // exits only when EVERY lane of the wave is done (a wave-uniform exit: a lane holding
-    // "busy" completes its hand-off inside the same iteration, so no lane waits on code
-    // the compiler would sink behind a divergent loop exit).  The retries are bounded (a
-    // never-reached safety net: the record is dropped and counted).
-    bool pend = false;
-    int pt = 0, pp = 0;
-    float4 pq0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pq1 = pq0;
-    auto drain = [&](bool cur, int t, int p, float4 q0, float4 q1) {
-        int tries = 0;
-        do {
-            if (pend || cur) {
-                if (pend && try_insert(pt, pp, pq0, pq1)) pend = false;
-                if (cur && !pend && try_insert(t, p, q0, q1)) cur = false;
-                if ((pend || cur) && ++tries > (1 << 22)) {
-                    atomicAdd(&ctr[cPairFail], (int)pend + (int)cur);
-                    pend = cur = false;
-                }
-            }
-        } while (__ballot(pend || cur) != 0ull);
-    };
-    auto pair_insert = [&](int t, int p, float4 q0, float4 q1) {
-        if (pend && try_insert(pt, pp, pq0, pq1)) pend = false;
-        if (!pend) {
-            if (!try_insert(t, p, q0, q1)) {
-                pend = true;
-                pt = t;
-                pp = p;
-                pq0 = q0;
-                pq1 = q1;
-            }
-        } else {
-            drain(true, t, p, q0, q1);
-        }
-    };
-    const long long gcnt = min((long long)grp, nblk - sb * grp);
-    auto batch_base = [&](long long c) { return ((c / gcnt) * nblk + sb * grp + c % gcnt) * kBatch; };
-    auto load_src = [&](long long b, double* dU, double* dV) {
-        if constexpr (SRC == 1) {
-#pragma unroll
-            for (int k = 0; k < kUnroll; ++k) {
-                const long long q = min(b + (long long)threadIdx.x * kUnroll + k, n - 1) * s.stride;
-                dU[k] = s.u64[q];
-                dV[k] = s.v64[q];
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < kUnroll; ++k) dU[k] = dV[k] = 0.0;
-        }
-    };
-    const bool al = aligned_vec<kUnroll>(u, v, h) && aligned_vec<kUnroll>(a0, NOUT == 2 ? a1 : a0, a0);
-    float pu[kUnroll], pv[kUnroll], ph[kUnroll], pa0[kUnroll], pa1[kUnroll];
-    double pU[kUnroll], pV[kUnroll];
-    long long c = 0;
-    const long long p0 = batch_base(0);
-    load_batch<kUnroll>(u, v, h, p0, n, al, pu, pv, ph);
-    load_props<NOUT>(a0, a1, p0, n, al, pa0, pa1);
-    load_src(p0, pU, pV);
-    for (long long base = p0, next; base < n; base = next) {
-        next = batch_base(++c);
-        float nu[kUnroll], nv[kUnroll], nh[kUnroll], na0[kUnroll], na1[kUnroll];
-        load_batch<kUnroll>(u, v, h, next, n, al, nu, nv, nh);
-        load_props<NOUT>(a0, a1, next, n, al, na0, na1);
-        double nU[kUnroll], nV[kUnroll];
-        load_src(next, nU, nV);
-#pragma unroll
-        for (int k = 0; k < kUnroll; ++k) {
-            const int p = (int)(base + (long long)threadIdx.x * kUnroll + k);
-            Box b;
-            if (!footprint<CULL>(g, s, p, pu[k], pv[k], ph[k], b)) continue;
-            const int tx0 = b.x0 >> kTileShift, tx1 = b.x1 >> kTileShift;
-            const int ty0 = b.y0 >> kTileShift, ty1 = b.y1 >> kTileShift;
-            if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > g.wide_tiles) {
-                wide_list[atomicAdd(&ctr[cWideCursor], 1)] = p;
-                continue;
-            }
-            const float cf0 = (float)term_coef<KID>(pa0[k], ph[k]);
-            const float cf1 = NOUT == 2 ? (float)term_coef<KID>(pa1[k], ph[k]) : 0.0f;
-            const float band = rec_band(g.mgl, ph[k]);
-            const double U = SRC == 0 ? (double)pu[k] : SRC == 1 ? pU[k] : src_u(s, p, pu[k]);
-            const double V = SRC == 0 ? (double)pv[k] : SRC == 1 ? pV[k] : src_v(s, p, pv[k]);
-            const bool mb = maybe_large(g, b);
-            for (int tx = tx0; tx <= tx1; ++tx)
-                for (int ty = ty0; ty <= ty1; ++ty) {
-                    const int t = tx * g.nty + ty;
-                    const unsigned bp = tile_box(b, tx, ty);
-                    const float4 q0 = make_float4((float)(U - corner_x(g, max(b.x0, tx * kTile))),
-                                                  (float)(V - corner_y(g, max(b.y0, ty * kTile))),
-                                                  ph[k], cf0);
-                    const float4 q1 = make_float4(cf1, __int_as_float(p), band, __uint_as_float(bp));
-                    if (mb && box_large(bp, g)) {
-                        const int slot = atomicAdd(&cur1[t], 1);
-                        rec_store(&recs[2 * (long long)slot], q0);
-                        rec_store(&recs[2 * (long long)slot + 1], q1);
-                    } else {
-                        pair_insert(t, p, q0, q1);
-                    }
-                }
-        }
-#pragma unroll
-        for (int k = 0; k < kUnroll; ++k) {
-            pu[k] = nu[k];
-            pv[k] = nv[k];
-            ph[k] = nh[k];
-            pa0[k] = na0[k];
-            pa1[k] = na1[k];
-            pU[k] = nU[k];
-            pV[k] = nV[k];
-        }
-    }
-    drain(false, 0, 0, pq0, pq1);  // the pending records
-    __syncthreads();
-    // flush: a parked record gets a hole as its partner; the padding slots up to the run's
-    // end (the next scatter workgroup's first count row, or the tile's end) become holes
-    const float4 hole0 = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
-    const float4 hole1 = make_float4(0.0f, __int_as_float(0), 0.0f, __uint_as_float(kHoleBox));
-    const long long nrow = min((sb + 1) * grp, nblk);
-    for (int t = threadIdx.x; t < nt; t += kScatterBlock) {
-        const unsigned long long x = wd[t];
-        int cc = (int)(unsigned)(x >> 32);
-        const unsigned st = (unsigned)x;
-        const int end = (int)tile_start[t] + (nrow < nblk ? hist[nrow * 2 * nt + t] : tile_total[t]);
-        if (st != kParkEmpty) {  // (never busy here: every hand-off completed)
-            const float4 f0 = pa[t];
-            const float4 f1 = make_float4(pc1[t], __int_as_float((int)st), rec_band(g.mgl, f0.z),
-                                          __uint_as_float(pbox[t]));
-            float4* d = recs + 2 * (long long)cc;
-            rec_store(d, f0);
-            rec_store(d + 1, f1);
-            rec_store(d + 2, hole0);
-            rec_store(d + 3, hole1);
-            cc += 2;
-        }
-        for (; cc < end; ++cc) {
-            rec_store(&recs[2 * (long long)cc], hole0);
-            rec_store(&recs[2 * (long long)cc + 1], hole1);
-        }
     }
 }
 
@@ -1405,7 +1155,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
         P.b = Box{0, -1, 0, -1};
         bool live = i < it.count;
         if (live) rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
-        live = live && P.b.x0 <= P.b.x1;  // not a hole (padding slot)
+        live = live && P.b.x0 <= P.b.x1;  // (an empty box deposits nothing)
         const int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
         const bool small = live && is_small(bw, bh);
         bool amb = false;
@@ -1673,7 +1423,7 @@ __global__ __launch_bounds__(kBlock) void k_evals(Grid g, int kid, Src64 s,
             Prep P;
             rec_prep<kAccF64>(r0, r1, X0, Y0, make_int2(0, 0), P);
             const int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
-            if (bw <= 0) continue;  // a hole (padding slot)
+            if (bw <= 0) continue;  // an empty box
             if (it.mode == 1) {
                 c1 += gather_slots(g, kid, __float_as_uint(r1.w));
             } else if (bw <= 3 && bh <= 3) {
@@ -2059,29 +1809,18 @@ static int allow_lds(K kern, size_t bytes) {
 }
 
 // K3 on stream st.  rec_cap / wide_cap: the capacities the kernel checks against the
-// device counters (speculative launch; see project2d).  k_scatter, or with
-// scatter_pairs() the 64-B pair scatter k_scatter_pair.
+// device counters (speculative launch; see project2d).
 template <int KID, int NOUT, int ACC, bool CULL, int SRC, int PROBE>
 static int scatter_variant(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl,
                            const float* u, const float* v, const float* h, const float* a0,
                            const float* a1, long long rec_cap, int wide_cap, hipStream_t st) {
     int* dc = (int*)ws.counters.p;
-    if (ACC == kAccF64 && scatter_pairs(g, false)) {
-        auto kern = k_scatter_pair<KID, NOUT, CULL, SRC, PROBE>;
-        ASP_TRY(allow_lds(kern, scatter_pair_lds(g)));
-        hipLaunchKernelGGL(kern, dim3((unsigned)pl.nblk_s), dim3(kScatterBlock),
-                           scatter_pair_lds(g), st, u, v, h, a0, a1, pl.n, pl.nblk, g, s,
-                           (const int*)ws.hist.p, (const long long*)ws.tile_start.p,
-                           (const int*)ws.tile_total.p, (float4*)ws.recs.p, (int*)ws.wide.p, dc,
-                           pl.grp, rec_cap, wide_cap);
-    } else {
-        hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC, CULL, SRC, PROBE>), dim3((unsigned)pl.nblk_s),
-                           dim3(kScatterBlock), scatter_lds(g, NOUT, ACC == kAccFix), st, u, v, h,
-                           a0, a1, pl.n, pl.nblk, g, s, (const int*)ws.hist.p,
-                           (const long long*)ws.tile_start.p, (const int*)ws.tile_total.p,
-                           (float4*)ws.recs.p, (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc, pl.grp,
-                           rec_cap, wide_cap);
-    }
+    hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC, CULL, SRC, PROBE>), dim3((unsigned)pl.nblk_s),
+                       dim3(kScatterBlock), scatter_lds(g, NOUT, ACC == kAccFix), st, u, v, h, a0,
+                       a1, pl.n, pl.nblk, g, s, (const int*)ws.hist.p,
+                       (const long long*)ws.tile_start.p, (const int*)ws.tile_total.p,
+                       (float4*)ws.recs.p, (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc, pl.grp,
+                       rec_cap, wide_cap);
     ASP_LAUNCHED();
     return ASP_OK;
 }
@@ -2238,7 +1977,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
         hipLaunchKernelGGL(g.nonsquare || g.mixed ? k_count<true> : k_count<false>,
                            dim3((unsigned)pl.nblk), dim3(kCountBlock),
                            (size_t)2 * g.ntiles * sizeof(int), st, du, dv, dh, n, pl.nblk, g, s,
-                           (int*)ws.hist.p, dc, (int)scatter_pairs(g, det));
+                           (int*)ws.hist.p, dc);
         ASP_LAUNCHED();
         m.done();
     }
@@ -2254,7 +1993,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
         StageMark m(ws, kSTilescan, st);
         hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
                            (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles, 2,
-                           (int)scatter_pairs(g, det), (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p, dc,
+                           0, (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p, dc,
                            (int*)ws.iorder.p, item_order_identity());
         ASP_LAUNCHED();
         m.done();
