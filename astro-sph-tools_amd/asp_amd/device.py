@@ -35,11 +35,13 @@ def _check(t, name, n=None, device=None):
 
 def project2d(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
               kernel="cubic", ratio: bool = False, accumulate: bool = False, out0=None,
-              out1=None, stream=None, deterministic: bool = False):
+              out1=None, stream=None, deterministic: bool = False, rows=None):
     """Project device-resident particles; returns ``(out0, out1)`` (out1 None for one map).
 
     ``extent = (u_min, u_max, v_min, v_max)``; images are (nx, ny) float32 tensors on the
     particles' device.  ``ratio`` turns (sum a0 W, sum a1 W) into their ratio in out0.
+    ``rows = (row_lo, row_hi)``: only those image rows (asp_project2d_rows, the row-slab
+    decomposition): outputs are (row_hi - row_lo, ny), each pixel the whole image's.
     """
     import torch
     dev = u.device
@@ -49,14 +51,16 @@ def project2d(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
     if a1 is not None:
         _check(a1, "a1", n, dev)
     nx, ny = int(image_size[0]), int(image_size[1])
+    r0, r1 = (0, nx) if rows is None else (int(rows[0]), int(rows[1]))
+    mx = r1 - r0  # rows written
     if out0 is None:
-        out0 = torch.empty((nx, ny), dtype=torch.float32, device=dev)
+        out0 = torch.empty((mx, ny), dtype=torch.float32, device=dev)
     if a1 is not None and out1 is None:
-        out1 = torch.empty((nx, ny), dtype=torch.float32, device=dev)
+        out1 = torch.empty((mx, ny), dtype=torch.float32, device=dev)
     for t in (out0, out1):
         if t is not None and (t.dtype != torch.float32 or t.device != dev or not t.is_contiguous()
-                              or t.numel() != nx * ny):
-            raise ValueError("outputs must be contiguous float32 (nx, ny) tensors on the device")
+                              or t.numel() != mx * ny):
+            raise ValueError("outputs must be contiguous float32 (rows, ny) tensors on the device")
     flags = _lib.ASP_F_DEVICE_PTRS
     if ratio:
         flags |= _lib.ASP_F_RATIO
@@ -68,9 +72,15 @@ def project2d(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
         stream = torch.cuda.current_stream(dev).cuda_stream
     P = _lib.ptr
     x_min, x_max, y_min, y_max = (float(e) for e in extent)
-    _lib.check(_lib.lib().asp_project2d(
-        P(u), P(v), P(h), P(a0), P(a1), n, x_min, x_max, y_min, y_max, nx, ny, int(chunk_size),
-        kernel_id(kernel), flags, P(out0), P(out1), dev.index or 0, stream))
+    if rows is None:
+        _lib.check(_lib.lib().asp_project2d(
+            P(u), P(v), P(h), P(a0), P(a1), n, x_min, x_max, y_min, y_max, nx, ny,
+            int(chunk_size), kernel_id(kernel), flags, P(out0), P(out1), dev.index or 0, stream))
+    else:
+        _lib.check(_lib.lib().asp_project2d_rows(
+            P(u), P(v), P(h), P(a0), P(a1), n, x_min, x_max, y_min, y_max, nx, ny,
+            int(chunk_size), r0, r1, kernel_id(kernel), flags, P(out0), P(out1), dev.index or 0,
+            stream))
     return out0, (out1 if a1 is not None else None)
 
 

@@ -327,3 +327,156 @@ def project3d_sharded(x, y, z, h, a, *, cube_size, extent, kernel="cubic",
     bufs = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(bufs, pad, group=group)
     return torch.cat([bufs[r][:, :, :K[r + 1] - K[r]] for r in range(world)], dim=2)
+
+
+# ---------------------------------------------------------------------------------------
+# 2-D map, image-plane alternative: row-slab ownership with footprint-halo duplication
+# (SURVEY.md §8(e) / H2 "measure both"; the reference's own image chunks,
+# _projector.py:89-111, distributed).  Rank r owns image rows [R[r], R[r+1]); every
+# particle goes to each rank whose rows its 2h footprint reaches; each rank projects only
+# its rows (asp_project2d_rows: fewer tiles binned per rank, no grid reduction at all).
+# ---------------------------------------------------------------------------------------
+TILE = 64
+
+
+def row_slabs(nx: int, world_size: int, u=None, u_extent=None, weights=None,
+              sample: int = 1 << 20, seed: int = 0):
+    """Row bounds R (world_size + 1 ints, R[0] = 0, R[-1] = nx), every inner bound a
+    multiple of 64 (whole GPU tile rows, as asp_project2d_rows requires).  Without ``u``
+    the tile rows are split evenly; with the particles' ``u`` (device or host tensor) and
+    ``u_extent`` = (u_min, u_max) the split equalises the particle count -- or the summed
+    ``weights`` -- per slab (a random subsample of 2^20 decides)."""
+    import torch
+    T = -(-nx // TILE)
+    W = int(world_size)
+    if W <= 1:
+        return [0, nx]
+    if T < W:
+        raise ValueError(f"{nx} rows are {T} tile rows of 64: fewer than {W} row slabs")
+    if u is None or u.shape[0] == 0:
+        inner = [TILE * ((T * r) // W) for r in range(1, W)]
+    else:
+        lo, hi = (float(e) for e in u_extent)
+        g = torch.Generator(device=u.device)
+        g.manual_seed(seed)
+        k = min(u.shape[0], sample)
+        idx = torch.randint(0, u.shape[0], (k,), generator=g, device=u.device)
+        t = ((u[idx].double() - lo) / ((hi - lo) / nx) / TILE).floor().clamp(0, T - 1).long()
+        w = torch.ones(k, dtype=torch.float64, device=u.device) if weights is None \
+            else weights[idx].double()
+        per = torch.zeros(T, dtype=torch.float64, device=u.device).index_add_(0, t, w)
+        c = torch.cumsum(per, 0)
+        tot = float(c[-1])
+        inner = []
+        for r in range(1, W):
+            # the first tile row at which the cumulative weight reaches r / W of the total
+            j = int(torch.searchsorted(c, torch.tensor([tot * r / W], dtype=torch.float64,
+                                                       device=c.device)).item()) + 1
+            inner.append(TILE * j)
+    # at least one tile row per slab: bound i in [64 i, 64 (T - W + i)], increasing
+    R = [0]
+    for i, b in enumerate(inner, start=1):
+        R.append(min(max(b, R[-1] + TILE), TILE * (T - W + i)))
+    R.append(nx)
+    return R
+
+
+def route_rows(u, h, u_extent, nx: int, bounds):
+    """Owner-rank range [r0, r1] of every particle's row footprint (r0 > r1: none): the
+    rows whose corners can lie within 2|h| of u, with one row of slack each side (the
+    device decides every pixel exactly, so duplicates only cost bandwidth)."""
+    import torch
+    u_min, u_max = (float(e) for e in u_extent)
+    ps = (u_max - u_min) / nx
+    ud, rad = u.double(), (2.0 * h.double()).abs()
+    x0 = torch.floor((ud - rad - u_min) / ps) - 1
+    x1 = torch.ceil((ud + rad - u_min) / ps) + 1
+    ok = (rad > 0) & torch.isfinite(ud) & torch.isfinite(rad) & (x1 >= 0) & (x0 <= nx - 1)
+    x0 = x0.clamp(0, nx - 1).long()
+    x1 = x1.clamp(0, nx - 1).long()
+    W = len(bounds) - 1
+    K = torch.tensor(list(bounds[1:-1]), device=u.device, dtype=torch.long)
+    r0 = torch.searchsorted(K, x0, right=True)
+    r1 = torch.searchsorted(K, x1, right=True)
+    r0 = torch.where(ok, r0, torch.full_like(r0, W))
+    r1 = torch.where(ok, r1, torch.full_like(r1, -1))
+    return r0, r1
+
+
+def exchange_rows(cols, u, h, *, u_extent, nx: int, bounds, group=None):
+    """All-to-all: every rank receives every particle (from any rank) whose footprint
+    reaches its rows.  ``cols``: the per-particle float32 columns to move (u, v, h, a0[, a1])."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    r0, r1 = route_rows(u, h, u_extent, nx, bounds)
+    k = len(cols)
+    packed = torch.stack(list(cols), dim=1)
+    parts, counts = [], []
+    for d in range(world):
+        sel = packed[(r0 <= d) & (r1 >= d)]
+        parts.append(sel)
+        counts.append(sel.shape[0])
+    send = torch.cat(parts, dim=0).contiguous()
+    scount = torch.tensor(counts, dtype=torch.int64, device=u.device)
+    rcount = torch.empty_like(scount)
+    dist.all_to_all_single(rcount, scount, group=group)
+    rc = rcount.tolist()
+    recv = torch.empty((sum(rc), k), dtype=send.dtype, device=send.device)
+    dist.all_to_all_single(recv.view(-1), send.view(-1), [c * k for c in rc],
+                           [c * k for c in counts], group=group)
+    return tuple(recv[:, c].contiguous() for c in range(k))
+
+
+def project2d_rowslab(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
+                      kernel="cubic", ratio: bool = False, bounds=None, group=None,
+                      gather: str = "none", exchange: bool = True, out0=None, out1=None,
+                      projector=None, deterministic: bool = False):
+    """The map on W ranks by image rows: rank r owns rows [R[r], R[r+1]) of ``bounds``
+    (default :func:`row_slabs` balanced on the particles' u).  With ``exchange`` every
+    rank passes ITS particles (any split) and one all-to-all routes them to the owners of
+    the rows their footprints reach; ``exchange=False`` when the caller already holds
+    every particle reaching its rows.  Each rank projects its rows only
+    (asp_project2d_rows) with the ratio formed locally -- its rows' sums are complete, so
+    no grid collective runs.  ``gather="none"`` returns this rank's (rows, ny) slab(s);
+    ``"all"`` all-gathers map 0 (the ratio map with ``ratio``) into the full (nx, ny) map
+    on every rank and returns ``(full, None)``.  ``projector`` replaces the local
+    projection (CPU tests); default the HIP path."""
+    import torch
+    import torch.distributed as dist
+    if ratio and a1 is None:
+        raise ValueError("ratio needs a1")
+    if gather not in ("none", "all"):
+        raise ValueError(f"unknown gather {gather!r}")
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    nx, ny = int(image_size[0]), int(image_size[1])
+    if bounds is None:
+        if world > 1:  # every rank must agree: balance on rank 0's sample, broadcast
+            R = torch.tensor(row_slabs(nx, world, u, extent[:2]), dtype=torch.int64,
+                             device=u.device)
+            dist.broadcast(R, src=0, group=group)
+            bounds = R.tolist()
+        else:
+            bounds = [0, nx]
+    if len(bounds) != world + 1 or bounds[0] != 0 or bounds[-1] != nx:
+        raise ValueError(f"bounds must be {world + 1} row edges from 0 to nx, got {bounds}")
+    if world > 1 and exchange:
+        cols = (u, v, h, a0) if a1 is None else (u, v, h, a0, a1)
+        got = exchange_rows(cols, u, h, u_extent=extent[:2], nx=nx, bounds=bounds, group=group)
+        u, v, h, a0 = got[:4]
+        a1 = got[4] if a1 is not None else None
+    proj = project2d if projector is None else projector
+    kw = {"deterministic": True} if deterministic else {}
+    r0, r1 = bounds[rank], bounds[rank + 1]
+    o0, o1 = proj(u, v, h, a0, a1, image_size=image_size, extent=extent, chunk_size=chunk_size,
+                  kernel=kernel, ratio=ratio, out0=out0, out1=out1, rows=(r0, r1), **kw)
+    if gather == "none" or world == 1:
+        return o0, o1
+    rmax = max(bounds[r + 1] - bounds[r] for r in range(world))
+    pad = torch.zeros((rmax, ny), dtype=o0.dtype, device=o0.device)
+    pad[:r1 - r0] = o0
+    full = torch.empty((world * rmax, ny), dtype=o0.dtype, device=o0.device)
+    dist.all_gather_into_tensor(full, pad, group=group)
+    return torch.cat([full[r * rmax:r * rmax + bounds[r + 1] - bounds[r]]
+                      for r in range(world)], dim=0), None

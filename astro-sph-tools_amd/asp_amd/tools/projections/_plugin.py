@@ -101,6 +101,14 @@ def project_callable(positions, smoothing_lengths, props, axes, image_size, chun
     pos = np.ascontiguousarray(np.asarray(positions, dtype=np.float64))
     h = np.ascontiguousarray(np.asarray(smoothing_lengths, dtype=np.float64).reshape(-1))
     props = [np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(-1)) for a in props]
+    # the session reads h.size rows of positions: every array must describe the same particles
+    # (the native path's checks, device._f64_arg)
+    if pos.ndim != 2 or pos.shape != (h.size, 3):
+        raise ValueError(f"positions must be (N, 3) with N = len(smoothing_lengths) = {h.size}, "
+                         f"got {pos.shape}")
+    for a in props:
+        if a.size != h.size:
+            raise ValueError(f"property of {a.size} values for {h.size} particles")
     ext = tuple(float(np.asarray(e)) for e in extent)
     with _Session(pos, h, axes, ext, (nx, ny), chunk_size, device) as S:
         if mode == "per_pixel":

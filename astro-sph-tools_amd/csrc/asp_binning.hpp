@@ -23,7 +23,6 @@ enum Ctr {
     cWideMax0 = 7,  // max |c0| over wide particles, fp32 bits (K3)
     cWideMax1 = 8,  // max |c1| over wide particles, fp32 bits (K3)
     cLarge = 9,     // records in the large stream (K2b)
-    cPairFail = 10, // (unused since the pair scatter was removed, round 3)
     cNum = 16
 };
 
@@ -110,10 +109,16 @@ static __global__ __launch_bounds__(kColscanBlock) void k_colscan(int* __restric
 // chunked independently: each stream aims at its own item count.
 // ----------------------------------------------------------------------------------
 constexpr int kScanThreads = 1024;
+// Regular items per call (split granularity of the small/mid stream): the cube's bricks
+// (kTargetItems) and the 2-D map's tiles (kTargetItems2d).  2-D, same-box A/B
+// (profiles/r03/items/): 1024 / 2048 / 4096 items give the 10^8 map 3.229-3.234 /
+// 3.234-3.236 / 3.269-3.276 ms and the 1.25e7 shard (the N = 8 rank) 0.517 / 0.537 /
+// 0.601 ms -- fewer, longer items cost the shard less merge and tilescan work.
+constexpr int kTargetItems = 2048;
 #ifndef ASP_TARGET_ITEMS
-#define ASP_TARGET_ITEMS 2048
+#define ASP_TARGET_ITEMS 1024
 #endif
-constexpr int kTargetItems = ASP_TARGET_ITEMS;  // regular items per map (split granularity)
+constexpr int kTargetItems2d = ASP_TARGET_ITEMS;
 constexpr int kMinItemRecords = 2048;
 constexpr int kTargetItems1 = 4096;    // mode-1 items (a record there costs ~10-1000x)
 constexpr int kMinItemRecords1 = 256;
@@ -201,8 +206,8 @@ constexpr int kOrderBuckets = 33;  // log2 classes of counts < 2^31, plus empty 
 template <int PER>  // tiles per thread held in registers: ntiles <= PER * kScanThreads
 static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     const int* __restrict__ tile_total, const int* __restrict__ morton, int ntiles, int nstream,
-    int pad, long long* __restrict__ tile_start, Item* __restrict__ items, Merge* __restrict__ merges,
-    int* __restrict__ ctr, int* __restrict__ order, int identity) {
+    long long* __restrict__ tile_start, Item* __restrict__ items, Merge* __restrict__ merges,
+    int* __restrict__ ctr, int* __restrict__ order, int identity, int target) {
     __shared__ int ocnt[kOrderBuckets];
     int tid = threadIdx.x;
     if (tid < kOrderBuckets) ocnt[tid] = 0;
@@ -219,9 +224,7 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
         cs_[q] = in ? tile_total[tt[q]] : 0;
         cl_[q] = in && nstream == 2 ? tile_total[tt[q] + ntiles] : 0;
     }
-    // pad: every tile's run starts on an even slot (a tile whose two streams hold an odd
-    // total is followed by a gap slot that no item covers); unused (0) since round 3
-    auto span = [&](int cs, int cl) { return (long long)(cs + cl) + (pad ? ((cs + cl) & 1) : 0); };
+    auto span = [](int cs, int cl) { return (long long)(cs + cl); };  // a tile's run
     long long sa[2] = {0, 0}, ta[2];  // all records; stream-1 records
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -232,7 +235,7 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     const long long total = ta[0], total1 = ta[1];
     const long long base0 = sa[0];
     int ch = (int)max((long long)kMinItemRecords,
-                      (total - total1 + kTargetItems - 1) / kTargetItems);
+                      (total - total1 + target - 1) / target);
     int chl = (int)max((long long)kMinItemRecords1, (total1 + kTargetItems1 - 1) / kTargetItems1);
     long long sb3[3] = {0, 0, 0}, tb[3];  // items, slabs, merges of this thread's tiles
     long long base = base0;

@@ -109,6 +109,38 @@ inline int ensure_side(Workspace& ws) {
     return ASP_OK;
 }
 
+// Everything a private workspace (a plug-in session's) owns: device buffers, the pinned
+// counters and bounce buffers, the side stream and its events.  The shared per-device
+// workspaces (g_ws) live for the process; asp_release frees only their buffers.
+void release_pinned(Workspace& ws);
+inline void ws_teardown(Workspace& ws) {
+    for (Buf* b : ws.all_bufs()) {
+        if (b->p) (void)hipFree(b->p);
+        b->p = nullptr;
+        b->cap = 0;
+    }
+    if (ws.h_counters) (void)hipHostFree(ws.h_counters);
+    ws.h_counters = nullptr;
+    release_pinned(ws);
+    for (hipEvent_t& e : ws.chunk_ev) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+    }
+    for (hipEvent_t* e : {&ws.done_ev, &ws.scan_ev, &ws.cnt_ev, &ws.last_ev}) {
+        if (*e) (void)hipEventDestroy(*e);
+        *e = nullptr;
+    }
+    if (ws.side) (void)hipStreamDestroy(ws.side);
+    ws.side = nullptr;
+    for (auto& q : ws.ev)
+        for (auto& k : q)
+            for (auto& j : k)
+                for (hipEvent_t& e : j) {
+                    if (e) (void)hipEventDestroy(e);
+                    e = nullptr;
+                }
+}
+
 inline Workspace g_ws[64];
 
 inline int set_device(int device) {

@@ -744,11 +744,7 @@ __device__ __forceinline__ bool small3_fast(const Prep& P, int bw, int bh, int X
         m = fminf(m, fminf(fminf(fabsf(e.x), fabsf(e.y)), fabsf(r2c[i] - P.thr)));
     }
     if (!(m > P.band)) return false;  // a pair in the band (or NaN): exact path
-#ifdef ASP_ABLATE_DEP_CONFLICTS  // timing ablation only (wrong maps): bank-conflict-free adds
-    const int base = (int)(threadIdx.x & 31);
-#else
     const int base = pix(P.b.x0 - X0, P.b.y0 - Y0);
-#endif
     const f2v hv = f2v{P.hinv, P.hinv};
     // column j = 2 of rows 0, 1 as one packed pair, row 2 with a dummy partner
     f2v wc01 = kernel_shape2<KID>(sqrt2(f2v{r2c[0], r2c[1]}) * hv);
@@ -1788,7 +1784,7 @@ static int item_order_identity() {
     }();
     return identity;
 }
-static inline size_t item_cap(const Grid& g) { return (size_t)2 * g.ntiles + kTargetItems + kTargetItems1 + 16; }
+static inline size_t item_cap(const Grid& g) { return (size_t)2 * g.ntiles + kTargetItems2d + kTargetItems1 + 16; }
 static inline size_t merge_cap(const Grid& g) { return (size_t)g.ntiles + 16; }
 
 static inline size_t scatter_lds(const Grid& g, int nout, bool det) {
@@ -1993,8 +1989,8 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
         StageMark m(ws, kSTilescan, st);
         hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
                            (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles, 2,
-                           0, (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p, dc,
-                           (int*)ws.iorder.p, item_order_identity());
+                           (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p, dc,
+                           (int*)ws.iorder.p, item_order_identity(), kTargetItems2d);
         ASP_LAUNCHED();
         m.done();
     }
@@ -2077,7 +2073,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
 #undef ASP_TAIL2
 #undef ASP_TAIL
     if (rc != ASP_OK) return rc;
-    ws.stats[9] = 0;
+    for (int k = 9; k <= 12; ++k) ws.stats[k] = 0;  // the evals diagnostic of THIS pass only
     if (getenv("ASP_COUNT_EVALS")) {  // diagnostic: the deposit kernels' lane-slots
         ASP_TRY(ensure(ws.aux[5], 3 * sizeof(unsigned long long)));
         ASP_HIP(hipMemsetAsync(ws.aux[5].p, 0, 3 * sizeof(unsigned long long), st));
@@ -2132,15 +2128,19 @@ static Src64 src_from(const Src64& s, long long b) {  // particles b.. of s
 // The whole call: every window of the image (window_grid) and, inside it, particle
 // batches of < 2^31 particles, each batch split in two while its records reach 2^31.
 // Batches after the first accumulate; the ratio of a batched map is formed at the end.
+// rows [row0, ...) of the image only (row0 = tile_lo * 64; asp_project2d_rows): tile rows
+// [tile_lo, tile_hi), d0 / d1 pointing at row row0 of the image.
 int project2d_full(Workspace& ws, const Grid& full, const Src64& s, const float* du,
                    const float* dv, const float* dh, const float* da0, const float* da1,
-                   long long n, int kid, int flags, float* d0, float* d1, hipStream_t st) {
+                   long long n, int kid, int flags, float* d0, float* d1, hipStream_t st,
+                   int tile_lo = 0, int tile_hi = -1) {
     const int wr = window_rows(full);
     const long long B = max_batch();
     long long agg[kNStats] = {0};
-    for (int tx0 = 0; tx0 < full.ntx; tx0 += wr) {
-        const Grid g = window_grid(full, tx0, std::min(tx0 + wr, full.ntx));
-        const long long off = (long long)g.ox * full.ny;
+    if (tile_hi < 0) tile_hi = full.ntx;
+    for (int tx0 = tile_lo; tx0 < tile_hi; tx0 += wr) {
+        const Grid g = window_grid(full, tx0, std::min(tx0 + wr, tile_hi));
+        const long long off = (long long)(g.ox - tile_lo * kTile) * full.ny;
         float* w0 = d0 + off;
         float* w1 = d1 ? d1 + off : nullptr;
         std::vector<std::pair<long long, long long>> todo;  // batches, last first
@@ -2182,7 +2182,7 @@ int project2d_full(Workspace& ws, const Grid& full, const Src64& s, const float*
         }
     }
     for (int k : {0, 1, 2, 6, 7, 8, 9, 10, 11, 12}) ws.stats[k] = agg[k];
-    ws.stats[4] = full.ntiles;
+    ws.stats[4] = (tile_hi - tile_lo) * full.nty;
     return ASP_OK;
 }
 
@@ -2236,11 +2236,17 @@ static int host_results(float* out0, float* out1, const float* d0, const float* 
 static int project2d(const float* u, const float* v, const float* h, const float* a0,
                      const float* a1, long long n, double x_min, double x_max, double y_min,
                      double y_max, int nx, int ny, int cs, int kid, int flags, float* out0,
-                     float* out1, int device, void* stream) {
+                     float* out1, int device, void* stream, int row_lo = 0, int row_hi = -1) {
     ASP_TRY(check_args(a1, out0, out1, n, kid, flags));
     if (n > 0 && (!u || !v || !h || !a0)) return fail(ASP_ERR_INVALID, "NULL particle array");
     Grid g;
     ASP_TRY(setup_grid(x_min, x_max, y_min, y_max, nx, ny, cs, g));
+    if (row_hi < 0) row_hi = nx;
+    if (row_lo < 0 || row_lo >= row_hi || row_hi > nx || row_lo % kTile != 0 ||
+        (row_hi % kTile != 0 && row_hi != nx))
+        return fail(ASP_ERR_INVALID, "rows: need 0 <= row_lo < row_hi <= nx, row_lo a multiple "
+                                     "of 64, row_hi a multiple of 64 or nx");
+    nx = row_hi - row_lo;  // the rows this call writes (the grid keeps the whole image's)
     ASP_TRY(set_device(device));
     Workspace& ws = g_ws[device];
     std::lock_guard<std::mutex> lock(ws.mu);
@@ -2266,7 +2272,8 @@ static int project2d(const float* u, const float* v, const float* h, const float
         ASP_TRY(host_outputs(ws, out0, out1, npix, flags, st, d0, d1));
     }
     const Src64 s{nullptr, nullptr, nullptr, nullptr, nullptr, 0, du, dv, dh};
-    ASP_TRY(project2d_full(ws, g, s, du, dv, dh, da0, da1, n, kid, flags, d0, d1, st));
+    ASP_TRY(project2d_full(ws, g, s, du, dv, dh, da0, da1, n, kid, flags, d0, d1, st,
+                           row_lo / kTile, (row_hi + kTile - 1) / kTile));
     if (!dev) ASP_TRY(host_results(out0, out1, d0, d1, npix, st));
     return ws_end_.finish();
 }
@@ -2360,7 +2367,8 @@ static int pairs_bin(PairsSession& S, int tx0) {
     S.wtx0 = -1;
     ASP_TRY(ensure(ws.pairs[0], (size_t)g.ntiles * kTilePix * sizeof(int)));  // pixcnt
     ASP_TRY(ensure(ws.pairs[3], (size_t)g.ntiles * sizeof(long long)));       // tile totals
-    if (S.n == 0) {
+    if (S.n == 0) {  // nothing binned: zero pixel counts and tile totals
+        ASP_HIP(hipMemsetAsync(ws.pairs[0].p, 0, (size_t)g.ntiles * kTilePix * sizeof(int), S.st));
         ASP_HIP(hipMemsetAsync(ws.pairs[3].p, 0, (size_t)g.ntiles * sizeof(long long), S.st));
         S.n_wide = 0;
     } else {
@@ -2412,9 +2420,7 @@ static int pairs_begin(const double* pos, const double* h, long long n, int axis
     Workspace& ws = S->ws;
     auto bail = [&](int rc) {
         (void)hipStreamSynchronize(S->st);
-        for (Buf* b : ws.all_bufs())
-            if (b->p) (void)hipFree(b->p);
-        release_pinned(ws);
+        ws_teardown(ws);
         delete S;
         return rc;
     };
@@ -2490,9 +2496,13 @@ static int pairs_emit(PairsSession& S, int t0, int t1, long long* offsets, int* 
     ASP_TRY(ensure(ws.aux[4], sizeof(int)));
     int* dovf = (int*)ws.aux[4].p;
     ASP_HIP(hipMemsetAsync(dovf, 0, sizeof(int), S.st));
-    if (npx == 0) {
-        if (!dev) offsets[0] = 0;
-        else ASP_HIP(hipMemsetAsync(offsets, 0, sizeof(long long), S.st));
+    if (npx == 0 || S.n == 0) {
+        // no tiles, or no particles (nothing was binned: no records for k_pairs to read):
+        // every pixel's range is empty
+        if (!dev) std::fill(offsets, offsets + npx + 1, 0LL);
+        else ASP_HIP(hipMemsetAsync(offsets, 0, (size_t)(npx + 1) * sizeof(long long), S.st));
+        ASP_HIP(hipStreamSynchronize(S.st));
+        return ASP_OK;
     }
     // window by window (the session re-bins only when the range moves to another window)
     long long done = 0;
@@ -2541,10 +2551,7 @@ static int pairs_end(PairsSession* S) {
     if (!S) return ASP_OK;
     (void)hipSetDevice(S->device);
     (void)hipStreamSynchronize(S->st);
-    for (Buf* b : S->ws.all_bufs())
-        if (b->p) (void)hipFree(b->p);
-    if (S->ws.h_counters) (void)hipHostFree(S->ws.h_counters);
-    release_pinned(S->ws);
+    ws_teardown(S->ws);  // buffers, pinned memory, the side stream and its events
     delete S;
     return ASP_OK;
 }
@@ -2575,6 +2582,16 @@ int asp_project2d(const float* u, const float* v, const float* h, const float* a
     t_err.clear();
     return project2d(u, v, h, a0, a1, n, u_min, u_max, v_min, v_max, nx, ny, chunk_size,
                      kernel_id, flags, out0, out1, device, stream);
+}
+
+int asp_project2d_rows(const float* u, const float* v, const float* h, const float* a0,
+                       const float* a1, int64_t n, double u_min, double u_max, double v_min,
+                       double v_max, int32_t nx, int32_t ny, int32_t chunk_size, int32_t row_lo,
+                       int32_t row_hi, int32_t kernel_id, int32_t flags, float* out0,
+                       float* out1, int32_t device, void* stream) {
+    t_err.clear();
+    return project2d(u, v, h, a0, a1, n, u_min, u_max, v_min, v_max, nx, ny, chunk_size,
+                     kernel_id, flags, out0, out1, device, stream, row_lo, row_hi);
 }
 
 int asp_project2d_f64(const double* positions, const double* h, const double* a0,

@@ -645,14 +645,14 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
         StageMark m(ws, kS3Tilescan, st);
         if (g.nb <= 4 * kScanThreads)
             hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
-                           (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1, 0,
+                           (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1,
                            (long long*)ws.tile_start.p, (Item*)ws.items.p,
-                           (Merge*)ws.merges.p, dc, (int*)nullptr, 0);
+                           (Merge*)ws.merges.p, dc, (int*)nullptr, 0, kTargetItems);
         else
             hipLaunchKernelGGL(k_tilescan<kScanPer>, dim3(1), dim3(kScanThreads), 0, st,
-                           (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1, 0,
+                           (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1,
                            (long long*)ws.tile_start.p, (Item*)ws.items.p,
-                           (Merge*)ws.merges.p, dc, (int*)nullptr, 0);
+                           (Merge*)ws.merges.p, dc, (int*)nullptr, 0, kTargetItems);
         ASP_LAUNCHED();
         m.done();
     }

@@ -71,8 +71,6 @@ def parse():
     ap.add_argument("--cube", type=int, default=512, help="cube edge (voxels), --workload cube")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="N > 1: wait for each map's collective before the next map")
-    ap.add_argument("--profile-steps", type=int, default=3,
-                    help="untimed steps with events around every stage (the breakdown)")
     ap.add_argument("--no-stage-events", dest="stage_events", action="store_false",
                     help="diagnostic: no per-stage HIP events in the timed region (no roofline)")
     ap.add_argument("--quiet", action="store_true")
@@ -228,6 +226,11 @@ def run_cube(args, world, rank, local, dev):
                            "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                            "frac": round(tf / VALU_PEAK_TFLOPS, 4), "included_pairs": int(pairs),
                            "flops_per_pair": F, "pairs_per_s": pairs / (dom_ms * 1e-3)}
+    for key in ("roofline", "roofline_hbm"):
+        fr = res.get(key, {}).get("frac")
+        if fr is not None and fr > 1.0:
+            log(f"bench: {key}.frac = {fr} > 1 -- not a valid measurement; no line printed")
+            sys.exit(4)
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -503,8 +506,10 @@ def main():
     local = local % max(1, torch.cuda.device_count())  # 1-GPU rehearsal of N ranks
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
+    backend_label = None
     if world > 1:
         backend = os.environ.get("ASP_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
+        backend_label = "RCCL" if backend == "nccl" else f"{backend} (rehearsal, not RCCL)"
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:  # rehearsal only (several ranks sharing one GPU cannot use RCCL)
@@ -584,17 +589,11 @@ def main():
         step()
     drain()
     torch.cuda.synchronize()
-    # Stage breakdown: a few untimed steps with HIP events around every launch.  Each event
-    # pair costs the stream a few microseconds, so the timed steps below mark only the
-    # dominant kernel (the one the roofline reports).
-    _lib.profile(local, True)
-    for _ in range(args.profile_steps):
-        step()
-    drain()
-    torch.cuda.synchronize()
-    prof_all = _lib.profile_read(local)
-    dom = max(prof_all, key=lambda k: prof_all[k][0])
-    _lib.profile(local, args.stage_events, stages=[dom])
+    # Every kernel of the timed steps is bracketed by HIP events on the stream it runs on
+    # (the library's asp_profile): the stage breakdown AND the dominant kernel come from
+    # the timed steps themselves, never from an untimed pass (with several ranks on one
+    # device an untimed span measured waiting, not work).
+    _lib.profile(local, args.stage_events)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -607,8 +606,13 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t
     out0, out1 = last[0]
-    prof = _lib.profile_read(local)  # timed region: the dominant kernel only
+    prof = _lib.profile_read(local)  # timed region: every stage's events
     _lib.profile(local, False)
+    launched = {k: v for k, v in prof.items() if v[1]}
+    if not launched:
+        log("bench: no stage events in the timed region (--no-stage-events): no roofline")
+        launched = {"none": (0.0, 0)}
+    dom = max(launched, key=lambda k: launched[k][0])  # most device time in the timed steps
     # N > 1: the single-map LATENCY as well (each map's collective completed before the
     # next map starts), beside the overlapped throughput of the timed region
     latency_ms = None
@@ -647,11 +651,12 @@ def main():
     nout = 2 if a1 is not None else 1
     b_p = 4 * (3 + nout)  # u, v, h + one property per output map
     bytes_alg = n_local * b_p + nout * G * G * 4
-    stages = {k: {"ms_per_launch": (ms / n if n else 0.0), "launches": n}
-              for k, (ms, n) in prof_all.items() if n}
-    # Dominant kernel = most device time per step (untimed breakdown), its duration measured
-    # by HIP events over the timed steps (one launch per step).
-    dom_ms = prof[dom][0] / args.steps
+    stages = {k: {"ms_per_launch": (ms / n if n else 0.0), "launches": n,
+                  "ms_per_step": ms / args.steps}
+              for k, (ms, n) in launched.items() if n}
+    # Dominant kernel = most device time over the timed steps, its duration per step from
+    # the same HIP events (one launch per step unless the map runs as windows / batches).
+    dom_ms = launched[dom][0] / args.steps
     achieved = bytes_alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic = None
     traffic_src = None
@@ -683,9 +688,11 @@ def main():
         "config": {"workload": f"{cfg_tag}: {args.n:.0e} particles -> {G}^2 "
                                f"{'mass-weighted temperature' if ratio else 'surface density'} "
                                f"map, {args.kernel}, {args.h_law}-scale h, fp32"
-                               + (f", Z-slab x{world} + RCCL {args.op}" if world > 1 else ""),
+                               + (f", Z-slab x{world} + {backend_label} {args.op}"
+                                  if world > 1 else ""),
                    "particles": args.n, "grid": G, "kernel": args.kernel, "h_law": args.h_law,
                    "map": args.map, "parallelism": f"zslab{world}" if world > 1 else "single",
+                   **({"backend": backend_label} if world > 1 else {}),
                    "accumulation": "int64 fixed point" if args.deterministic else "fp64",
                    "collective_overlap": nbuf > 1,
                    **({"slab_weight": args.slab_weight, "collective": args.op,
@@ -701,7 +708,7 @@ def main():
                      "traffic": traffic, "traffic_source": traffic_src,
                      "bytes_alg_per_launch": bytes_alg,
                      "kernel_ms_per_step": round(dom_ms, 4),
-                     "kernel_launches_timed": prof[dom][1],
+                     "kernel_launches_timed": launched[dom][1],
                      "pipeline_frac": round(bytes_alg / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "stages": stages,
         "records_per_particle": round(st["records"] / max(1, n_local), 4),
@@ -713,6 +720,16 @@ def main():
         res["roofline"] = valu_roofline(valu, args.kernel, nout, dom, dom_ms, pm_stage)
         res["roofline"]["pipeline_frac"] = round(
             valu[0] * pair_flops(args.kernel, nout) / (ms_step * 1e-3) / 1e12 / VALU_PEAK_TFLOPS, 4)
+    # A fraction of a physical peak above 1 is a measurement error (e.g. events that timed
+    # waiting): refuse to publish it.
+    for key in ("roofline", "roofline_hbm"):
+        fr = res.get(key, {}).get("frac")
+        if fr is not None and fr > 1.0:
+            log(f"bench: {key}.frac = {fr} > 1 for kernel {res[key].get('kernel')!r} -- "
+                f"not a valid measurement; no line printed")
+            if world > 1:
+                dist.destroy_process_group()
+            sys.exit(4)
     want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
     if want_cpu:
         try:

@@ -96,6 +96,21 @@ int asp_project2d(const float *u, const float *v, const float *h, const float *a
                   int32_t flags, float *out0, float *out1, int32_t device, void *stream);
 
 /*
+ * Image rows [row_lo, row_hi) of asp_project2d's map only -- the row-slab (image-plane)
+ * decomposition of SURVEY.md §8(e) / H2, the reference's own image chunks
+ * (_projector.py:89-111) distributed: out0 / out1 hold (row_hi - row_lo) x ny pixels,
+ * element [(xi - row_lo) * ny + yi], each equal to the pixel asp_project2d writes for the
+ * whole image (same corners, pitches, chunk cull and decisions; particles whose footprint
+ * misses the rows are skipped).  row_lo must be a multiple of 64, row_hi a multiple of 64
+ * or nx.  Other arguments as asp_project2d.
+ */
+int asp_project2d_rows(const float *u, const float *v, const float *h, const float *a0,
+                       const float *a1, int64_t n, double u_min, double u_max, double v_min,
+                       double v_max, int32_t nx, int32_t ny, int32_t chunk_size, int32_t row_lo,
+                       int32_t row_hi, int32_t kernel_id, int32_t flags, float *out0,
+                       float *out1, int32_t device, void *stream);
+
+/*
  * create_image on the reader's own float64 arrays: the drop-in for create_image
  * (_projector.py:75-120) as it is called, with positions (n, 3) float64 row-major (the
  * reader's get_positions, _SnapshotBase.py:708-722), smoothing lengths and properties

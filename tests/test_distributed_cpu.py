@@ -326,3 +326,93 @@ def test_cube_plane_slabs_halo_exchange_world2():
     for r in range(world):
         np.testing.assert_allclose(out[r]["slab"], ref[:, :, K[r]:K[r + 1]], atol=tol, rtol=1e-6)
         np.testing.assert_allclose(out[r]["full"], ref, atol=tol, rtol=1e-6)
+
+
+# ------------------------------------------- 2-D row slabs (image-plane decomposition)
+GR = 192  # three tile rows of 64: unequal slabs for world 2
+
+
+def _oracle_rows(u, v, h, a0, a1, *, image_size, extent, chunk_size, kernel, ratio, out0,
+                 out1, rows):
+    """The local projection of project2d_rowslab on CPU: the oracle's map over the rank's
+    (routed) particles, rows [rows[0], rows[1]) kept (the GPU path is asp_project2d_rows)."""
+    import pyoracle
+    o0, o1 = pyoracle.project_scatter(u.numpy(), v.numpy(), h.numpy(), a0.numpy(),
+                                      None if a1 is None else a1.numpy(), image_size,
+                                      chunk_size, *extent, kernel=kernel)
+    r = slice(rows[0], rows[1])
+    o0, o1 = o0[r], (None if o1 is None else o1[r])
+    if ratio:
+        o0 = np.where(o1 != 0, o0 / np.where(o1 != 0, o1, 1), 0.0)
+    t0 = torch.from_numpy(np.ascontiguousarray(o0, np.float32))
+    t1 = None if o1 is None else torch.from_numpy(np.ascontiguousarray(o1, np.float32))
+    return t0, t1
+
+
+def _rows_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, PKG_ROOT)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from asp_amd.distributed import project2d_rowslab, route_rows, row_slabs
+        x, y, z, h, m, T = _data()
+        # an arbitrary input split (as a reader's MPI split): every other particle
+        keep = (torch.arange(x.numel()) % world) == rank
+        sl = [t[keep].contiguous() for t in (x, y, h, m, T)]
+        res = {}
+        slab, s1 = project2d_rowslab(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3],
+                                     image_size=(GR, GR), extent=EXT, chunk_size=16,
+                                     kernel="cubic", projector=_oracle_rows)
+        res["slab"] = (slab.numpy().copy(), s1.numpy().copy())
+        full, none = project2d_rowslab(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3],
+                                       image_size=(GR, GR), extent=EXT, chunk_size=16,
+                                       kernel="cubic", ratio=True, gather="all",
+                                       projector=_oracle_rows)
+        res["full_ratio"] = full.numpy().copy()
+        res["none"] = none
+        R = row_slabs(GR, world, x, EXT[:2])
+        res["bounds"] = R
+        r0, r1 = route_rows(x, h, EXT[:2], GR, R)
+        res["routed"] = int(((r0 <= rank) & (r1 >= rank)).sum())
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rowslab_world2():
+    """Row-slab ownership (H2): the all-to-all routes each particle to the ranks whose rows
+    its footprint reaches; each rank's slab equals the oracle's full map on those rows,
+    the ratio is formed locally, and the all-gathered ratio map is the full one."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rows_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    x, y, z, h, m, T = _data()
+    full0, full1 = pyoracle.project_scatter(x.numpy(), y.numpy(), h.numpy(), (m * T).numpy(),
+                                            m.numpy(), (GR, GR), 16, *EXT, kernel="cubic")
+    R = out[0]["bounds"]
+    assert R == out[1]["bounds"] and R[0] == 0 and R[-1] == GR and R[1] % 64 == 0
+    t0, t1 = 1e-5 * np.abs(full0).max(), 1e-5 * np.abs(full1).max()
+    cov = full1 > 1e-3 * full1.max()
+    want_ratio = np.where(full1 != 0, full0 / np.where(full1 != 0, full1, 1), 0.0)
+    for r in range(world):
+        rows = slice(R[r], R[r + 1])
+        np.testing.assert_allclose(out[r]["slab"][0], full0[rows], atol=t0, rtol=0)
+        np.testing.assert_allclose(out[r]["slab"][1], full1[rows], atol=t1, rtol=0)
+        np.testing.assert_allclose(out[r]["full_ratio"][cov], want_ratio[cov], rtol=1e-4)
+        assert out[r]["none"] is None
+    # every particle reaches some rank; the wide physical-h halo is duplicated, not all of it
+    assert x.numel() <= out[0]["routed"] + out[1]["routed"] < 2 * x.numel()

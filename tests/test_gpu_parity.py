@@ -588,3 +588,44 @@ def test_plugin_bins_once_many_batches(gpu, monkeypatch):
                      deterministic=True)
     np.testing.assert_array_equal(a, b)
     np.testing.assert_allclose(a, ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
+
+
+def test_plugin_zero_particles(gpu):
+    """An empty particle set through the plug-in session (nothing is binned: the emit must
+    not read records that were never written): zero maps in both modes, and per_pixel
+    still calls the callable once per pixel with empty arrays, as the reference does."""
+    from asp_amd.tools.projections import create_image, create_weighted_image
+    pos, h, A = np.zeros((0, 3)), np.zeros(0), np.zeros(0)
+    seen = []
+
+    def kern(r, hh):
+        seen.append(r.size)
+        return wendland_c2_numpy(r, hh)
+
+    ext = (-1.0, 1.0, -1.0, 1.0)
+    img = create_image(pos, h, A, (96, 80), 32, 2, *ext, kernel_func=kern,
+                       kernel_func_mode="per_pixel")
+    assert img.shape == (96, 80) and not img.any()
+    assert len(seen) == 96 * 80 and not any(seen)
+    seen.clear()
+    img = create_image(pos, h, A, (96, 80), 32, 2, *ext, kernel_func=kern)
+    assert img.shape == (96, 80) and not img.any() and not seen
+    w = create_weighted_image(pos, h, A, A, (70, 70), 32, 2, *ext, kernel_func=kern)
+    assert not w.any()
+
+
+def test_plugin_sessions_release_everything(gpu):
+    """Every plug-in session owns a workspace with a side stream, events and pinned
+    buffers; closing it must release them all (asp_pairs_end).  Hundreds of sessions in a
+    row stay correct and leave the device usable."""
+    from asp_amd.tools.projections import create_image
+    pos, h, A, size, cs, ext, ref = g3()
+    sub = slice(0, 500)
+    first = None
+    for _ in range(300):
+        img = create_image(pos[sub], h[sub], A[sub], (64, 64), 32, 2, *ext,
+                           kernel_func=lambda r, hh: wendland_c2_numpy(r, hh))
+        if first is None:
+            first = img
+        np.testing.assert_array_equal(img, first)
+    assert first.any()

@@ -133,3 +133,18 @@ def test_zslab_bounds_equal_count():
     counts = [int(((z >= e[r]) & (z < e[r + 1])).sum()) for r in range(4)]
     assert sum(counts) == z.numel()
     assert max(counts) - min(counts) < 0.02 * z.numel()
+
+
+def test_plugin_argument_lengths():
+    """The plug-in session reads len(h) rows of positions: mismatched arrays are a
+    ValueError before any native call (as the native path's device._f64_arg checks)."""
+    from asp_amd.tools.projections._plugin import project_callable
+    f = lambda r, h: r  # noqa: E731
+    pos = np.zeros((10, 3))
+    with pytest.raises(ValueError):
+        project_callable(pos, np.ones(12), [np.ones(12)], (2, 2), (8, 8), 4, (0, 1, 0, 1), f)
+    with pytest.raises(ValueError):
+        project_callable(pos, np.ones(10), [np.ones(9)], (2, 2), (8, 8), 4, (0, 1, 0, 1), f)
+    with pytest.raises(ValueError):
+        project_callable(np.zeros((10, 2)), np.ones(10), [np.ones(10)], (2, 2), (8, 8), 4,
+                         (0, 1, 0, 1), f)
