@@ -164,7 +164,9 @@ def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
     if op.startswith("reduce_scatter") and world > 1 and nx % world:
         raise ValueError("reduce_scatter needs nx divisible by the world size")
     proj = project2d if projector is None else projector
-    kw = {"deterministic": True} if deterministic else {}
+    # deterministic ratio maps: the components are quantised consistently (ASP_F_WEIGHTED)
+    # so the ratio formed after the sum stays a weighted mean
+    kw = {"deterministic": True, **({"weighted": True} if ratio else {})} if deterministic else {}
     o0, o1 = proj(u, v, h, a0, a1, image_size=image_size, extent=extent,
                   chunk_size=chunk_size, kernel=kernel, ratio=False, out0=out0, out1=out1, **kw)
     outs = [o0] if o1 is None else [o0, o1]
@@ -230,13 +232,14 @@ def project2d_sharded_host(positions, h, a0, a1=None, *, projection_axis=2, imag
 
 
 def project2d_f64_local(positions, h, a0, a1=None, *, projection_axis, image_size, extent,
-                        chunk_size, kernel, out0, out1, device, deterministic=False):
+                        chunk_size, kernel, out0, out1, device, deterministic=False,
+                        weighted=False):
     """One rank's fp64 host arrays -> its device map(s) (no ratio: formed after the sum)."""
     from .device import project2d_f64
     return project2d_f64(positions, h, a0, a1, projection_axis=projection_axis,
                          image_size=image_size, extent=extent, chunk_size=chunk_size,
                          kernel=kernel, out0=out0, out1=out1, device=device,
-                         deterministic=deterministic, device_out=True)
+                         deterministic=deterministic, device_out=True, weighted=weighted)
 
 
 # ---------------------------------------------------------------------------------------

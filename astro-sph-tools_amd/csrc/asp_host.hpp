@@ -143,6 +143,42 @@ inline void ws_teardown(Workspace& ws) {
 
 inline Workspace g_ws[64];
 
+// 2-D maps from DIFFERENT streams get different workspaces (slots), so consecutive
+// independent maps enqueued on two streams overlap on the device (the binning of map
+// i + 1 beside the deposit of map i).  Slot 0 is g_ws (shared with every
+// other entry point); a map call on a stream that already owns a slot reuses it, a new
+// stream takes the least recently used slot.  Within a slot calls stay ordered (ws_begin
+// waits for the slot's previous call); across slots the caller's streams order the work,
+// as for any two HIP streams.  ASP_MAP_SLOTS=1: one slot (every call ordered).
+constexpr int kMapSlots = 2;
+inline Workspace g_ws_alt[64][kMapSlots - 1];
+struct SlotTable {
+    std::mutex mu;
+    hipStream_t stream[kMapSlots] = {};
+    bool used[kMapSlots] = {};
+    int last = kMapSlots - 1;
+};
+inline SlotTable g_slots[64];
+inline Workspace& slot_ws(int device, int s) { return s == 0 ? g_ws[device] : g_ws_alt[device][s - 1]; }
+inline int map_slot(int device, hipStream_t st) {
+    static const int nslots = [] {
+        const char* e = getenv("ASP_MAP_SLOTS");
+        return e ? std::max(1, std::min(kMapSlots, atoi(e))) : kMapSlots;
+    }();
+    SlotTable& T = g_slots[device];
+    std::lock_guard<std::mutex> lock(T.mu);
+    int s = -1;
+    for (int k = 0; k < nslots && s < 0; ++k)
+        if (T.used[k] && T.stream[k] == st) s = k;
+    for (int k = 0; k < nslots && s < 0; ++k)
+        if (!T.used[k]) s = k;
+    if (s < 0) s = (T.last + 1) % nslots;  // the least recently used of two
+    T.used[s] = true;
+    T.stream[s] = st;
+    T.last = s;
+    return s;
+}
+
 inline int set_device(int device) {
     int ndev = 0;
     ASP_HIP(hipGetDeviceCount(&ndev));

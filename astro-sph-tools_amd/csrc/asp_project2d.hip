@@ -486,6 +486,8 @@ __device__ __forceinline__ void accumulate(const Prep& P, float r2, unsigned lon
                                            unsigned long long* acc1, int k) {
     float q = __builtin_amdgcn_sqrtf(r2) * P.hinv;  // v_sqrt_f32, 1 ulp
     float w = kernel_shape<KID>(q);
+    if constexpr (ACC == kAccFix && NOUT == 2)
+        if (fabsf(P.s1 * w) < P.tmin) return;  // weighted fixed point: both maps or neither
     acc_add<ACC>(&acc0[k], P.s0 * w);
     if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k], P.s1 * w);
 }
@@ -556,7 +558,8 @@ __device__ __forceinline__ bool clip(Box& b, int X0, int Y0, int TW, int TH) {
 // fixed-point mode the tile's power-of-two scale applied (ldexp: exact).
 template <int ACC>
 __device__ __forceinline__ void rec_prep(const float4& r0, const float4& r1, int X0, int Y0,
-                                         int2 kk, Prep& P) {
+                                         int2 kk, Prep& P, float tmin = 0.0f) {
+    P.tmin = tmin;
     P.u = r0.x;
     P.v = r0.y;
     P.h = r0.z;
@@ -585,6 +588,7 @@ __device__ __forceinline__ void load_rec(const float4* recs, long long i, float4
 constexpr int kTilePix = kTile * kTile;
 constexpr int kFlagAccumulate = 1;
 constexpr int kFlagRatio = 2;  // fused ratio: out0 <- map0 / map1
+constexpr int kFlagTail = 4;   // weighted fixed point (ASP_F_WEIGHTED): kTailUnits rule
 
 // Corner offset tables: xt[k] = fl32(k * pitch_x), yt[k] = fl32(k * pitch_y) for k < 64 --
 // the corner k pixels from a record's box origin, in the frame of the record's (u, v)
@@ -756,15 +760,18 @@ __device__ __forceinline__ bool small3_fast(const Prep& P, int bw, int bh, int X
         f2v t0 = w * P.s0, t1 = w * P.s1;
         f2v c = f2v{wc[i], wc[i]} * f2v{P.s0, P.s1};
         const int k = base + i * kRow;
-        if (r2[i].x < P.thr) {
+        // weighted fixed point: a pair whose weight term is below tmin units is dropped
+        // from both maps (tmin = 0 otherwise: the test is always true)
+        const bool keep = !(ACC == kAccFix && NOUT == 2);
+        if (r2[i].x < P.thr && (keep || fabsf(t1.x) >= P.tmin)) {
             acc_add<ACC>(&acc0[k], t0.x);
             if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k], t1.x);
         }
-        if (r2[i].y < P.thr) {
+        if (r2[i].y < P.thr && (keep || fabsf(t1.y) >= P.tmin)) {
             acc_add<ACC>(&acc0[k + 1], t0.y);
             if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k + 1], t1.y);
         }
-        if (r2c[i] < P.thr) {
+        if (r2c[i] < P.thr && (keep || fabsf(c.y) >= P.tmin)) {
             acc_add<ACC>(&acc0[k + 2], c.x);
             if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k + 2], c.y);
         }
@@ -782,7 +789,7 @@ template <int KID, int NOUT, int ACC>
 __device__ __forceinline__ void deferred(const Grid& g, const Src64& s,
                                          const float4* __restrict__ recs, long long start,
                                          const int* dlist, int first, int cnt, int X0, int Y0,
-                                         int2 kk, const float* xt, const float* yt,
+                                         int2 kk, float tmin, const float* xt, const float* yt,
                                          unsigned long long* acc0, unsigned long long* acc1,
                                          int lane) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -794,7 +801,7 @@ __device__ __forceinline__ void deferred(const Grid& g, const Src64& s,
     float4 r0, r1;
     load_rec(recs, start + idx, r0, r1);
     Prep P;
-    rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
+    rec_prep<ACC>(r0, r1, X0, Y0, kk, P, tmin);
     small_box<KID, NOUT, ACC, 4>(g, s, P, P.b.x1 - P.b.x0 + 1, P.b.y1 - P.b.y0 + 1, X0, Y0, xt,
                                  yt, acc0, acc1);
 }
@@ -835,6 +842,7 @@ struct GAcc {
     f2 p0[4], p1[4];                  // kAccF64 fp32 partials, pixels (2k, 2k + 1)
     double* t0;
     double* t1;
+    float tmin = 0.0f;  // kAccFix weighted maps: pairs with |s1 W| < tmin dropped from both
     __device__ __forceinline__ void init(double* tot) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -859,6 +867,7 @@ struct GAcc {
     // pixel j += w * (s0, s1)
     __device__ __forceinline__ void add(int j, float w, float s0, float s1) {
         if constexpr (ACC == kAccFix) {
+            if (NOUT == 2 && fabsf(s1 * w) < tmin) return;
             a0[j] += f2fix(s0 * w);
             if (NOUT == 2) a1[j] += f2fix(s1 * w);
         } else {
@@ -1141,6 +1150,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
         return;
     }
     const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
+    const float tmin = (ACC == kAccFix && (flags & kFlagTail)) ? kTailUnits : 0.0f;
     tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
     const int lane = threadIdx.x & 63;
     int* dlist = defer_lds[threadIdx.x >> 6];
@@ -1150,7 +1160,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
         Prep P;
         P.b = Box{0, -1, 0, -1};
         bool live = i < it.count;
-        if (live) rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
+        if (live) rec_prep<ACC>(r0, r1, X0, Y0, kk, P, tmin);
         live = live && P.b.x0 <= P.b.x1;  // (an empty box deposits nothing)
         const int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
         const bool small = live && is_small(bw, bh);
@@ -1172,7 +1182,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
                 if (ndef >= 64) {  // a full wave of deferred records
                     ndef -= 64;
                     deferred<KID, NOUT, ACC>(g, s, recs, it.start, dlist, ndef, 64, X0, Y0, kk,
-                                             xt, yt, acc0, acc1, lane);
+                                             tmin, xt, yt, acc0, acc1, lane);
                 }
             }
         }
@@ -1204,8 +1214,8 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
         q1 = n1;
     }
     if (ndef > 0)
-        deferred<KID, NOUT, ACC>(g, s, recs, it.start, dlist, 0, ndef, X0, Y0, kk, xt, yt, acc0,
-                                 acc1, lane);
+        deferred<KID, NOUT, ACC>(g, s, recs, it.start, dlist, 0, ndef, X0, Y0, kk, tmin, xt, yt,
+                                 acc0, acc1, lane);
     __syncthreads();
     if (it.slab >= 0) {  // split tile: partial sums, merged by K5 (slab layout unpadded)
         unsigned long long* dst = slabs + (long long)it.slab * NOUT * kTilePix;
@@ -1254,6 +1264,7 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(
     const GOwn o = gather_owner(blockIdx.x % kGatherRegions);
     GAcc<NOUT, ACC> ga;
     ga.init(tot);
+    ga.tmin = (ACC == kAccFix && (flags & kFlagTail)) ? kTailUnits : 0.0f;
     const GCorner cc = gather_corners(g, o);
     for (int base = 0; base < it.count; base += 64) {
         GEntry mine;
@@ -1329,7 +1340,7 @@ __global__ __launch_bounds__(kGatherThreads) void k_wide(
     Grid g, Src64 s, const float* __restrict__ u, const float* __restrict__ v,
     const float* __restrict__ h, const float* __restrict__ a0, const float* __restrict__ a1,
     const int* __restrict__ wide_list, int n_wide, const int* __restrict__ ctr,
-    float* __restrict__ out0, float* __restrict__ out1) {
+    float* __restrict__ out0, float* __restrict__ out1, int flags) {
     extern __shared__ __attribute__((aligned(16))) double tot[];
     const int t = blockIdx.x / kGatherRegions;
     const int tx = t / g.nty, ty = t - (t / g.nty) * g.nty;
@@ -1342,6 +1353,7 @@ __global__ __launch_bounds__(kGatherThreads) void k_wide(
     const GOwn o = gather_owner(blockIdx.x % kGatherRegions);
     GAcc<NOUT, ACC> ga;
     ga.init(tot);
+    ga.tmin = (ACC == kAccFix && (flags & kFlagTail)) ? kTailUnits : 0.0f;
     const GCorner cc = gather_corners(g, o);
     bool any = false;  // wave-uniform
     for (int c = 0; c < n_wide; c += 64) {
@@ -1848,7 +1860,8 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
     const bool fuse_ratio = ratio && pl.n_wide == 0;
     const unsigned long long* slabs = (const unsigned long long*)ws.slabs.p;
     const int dflags = ((flags & ASP_F_ACCUMULATE) ? kFlagAccumulate : 0) |
-                       (fuse_ratio ? kFlagRatio : 0);
+                       (fuse_ratio ? kFlagRatio : 0) |
+                       (NOUT == 2 && (flags & (ASP_F_WEIGHTED | ASP_F_RATIO)) ? kFlagTail : 0);
     if (!pre_scattered)
         ASP_TRY((launch_scatter<KID, NOUT, ACC>(g, s, ws, pl, u, v, h, a0, a1, 0x7fffffffLL,
                                                 0x7fffffff, st)));
@@ -1894,7 +1907,7 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
         hipLaunchKernelGGL((k_wide<KID, NOUT, ACC>), dim3(g.ntiles * kGatherRegions),
                            dim3(kGatherThreads), lds, st, g, s,
                            u, v, h, a0, a1, (const int*)ws.wide.p, pl.n_wide, (const int*)dc, o0,
-                           o1);
+                           o1, dflags);
         ASP_LAUNCHED();
         m.done();
     }
@@ -2138,6 +2151,7 @@ int project2d_full(Workspace& ws, const Grid& full, const Src64& s, const float*
     const long long B = max_batch();
     long long agg[kNStats] = {0};
     if (tile_hi < 0) tile_hi = full.ntx;
+    if (flags & ASP_F_RATIO) flags |= ASP_F_WEIGHTED;  // kept when batches defer the ratio
     for (int tx0 = tile_lo; tx0 < tile_hi; tx0 += wr) {
         const Grid g = window_grid(full, tx0, std::min(tx0 + wr, tile_hi));
         const long long off = (long long)(g.ox - tile_lo * kTile) * full.ny;
@@ -2183,6 +2197,9 @@ int project2d_full(Workspace& ws, const Grid& full, const Src64& s, const float*
     }
     for (int k : {0, 1, 2, 6, 7, 8, 9, 10, 11, 12}) ws.stats[k] = agg[k];
     ws.stats[4] = (tile_hi - tile_lo) * full.nty;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && &ws != &g_ws[dev])  // asp_last_stats reads slot 0
+        std::copy(ws.stats, ws.stats + kNStats, g_ws[dev].stats);
     return ASP_OK;
 }
 
@@ -2248,7 +2265,7 @@ static int project2d(const float* u, const float* v, const float* h, const float
                                      "of 64, row_hi a multiple of 64 or nx");
     nx = row_hi - row_lo;  // the rows this call writes (the grid keeps the whole image's)
     ASP_TRY(set_device(device));
-    Workspace& ws = g_ws[device];
+    Workspace& ws = slot_ws(device, map_slot(device, (hipStream_t)stream));
     std::lock_guard<std::mutex> lock(ws.mu);
     hipStream_t st = (hipStream_t)stream;
     ASP_TRY(ws_begin(ws, st));
@@ -2295,7 +2312,7 @@ static int project2d_f64(const double* pos, const double* h, const double* a0,
     ASP_TRY(setup_grid(x_min, x_max, y_min, y_max, nx, ny, cs, g));
     g.mixed = cull_axis != axis;
     ASP_TRY(set_device(device));
-    Workspace& ws = g_ws[device];
+    Workspace& ws = slot_ws(device, map_slot(device, (hipStream_t)stream));
     std::lock_guard<std::mutex> lock(ws.mu);
     hipStream_t st = (hipStream_t)stream;
     ASP_TRY(ws_begin(ws, st));
@@ -2794,20 +2811,22 @@ int asp_profile_stages(int32_t device, uint32_t stage_mask) {
     int ndev = asp_device_count();
     if (device < 0 || device >= ndev) return fail(ASP_ERR_INVALID, "bad device");
     ASP_HIP(hipSetDevice(device));
-    Workspace& ws = g_ws[device];
-    std::lock_guard<std::mutex> lock(ws.mu);
-    if (stage_mask && !ws.ev[0][0][0][0])
-        for (int q = 0; q < 2; ++q)
-            for (int k = 0; k < kStages; ++k)
-                for (int j = 0; j < kMarks; ++j)
-                    for (int e = 0; e < 2; ++e) ASP_HIP(hipEventCreate(&ws.ev[q][k][j][e]));
-    for (int k = 0; k < kStages; ++k) {
-        ws.stage_ms[k] = 0.0;
-        ws.stage_n[k] = 0;
-        ws.ev_live[0][k] = ws.ev_live[1][k] = 0;
+    for (int sl = 0; sl < kMapSlots; ++sl) {  // every map slot's workspace
+        Workspace& ws = slot_ws(device, sl);
+        std::lock_guard<std::mutex> lock(ws.mu);
+        if (stage_mask && !ws.ev[0][0][0][0])
+            for (int q = 0; q < 2; ++q)
+                for (int k = 0; k < kStages; ++k)
+                    for (int j = 0; j < kMarks; ++j)
+                        for (int e = 0; e < 2; ++e) ASP_HIP(hipEventCreate(&ws.ev[q][k][j][e]));
+        for (int k = 0; k < kStages; ++k) {
+            ws.stage_ms[k] = 0.0;
+            ws.stage_n[k] = 0;
+            ws.ev_live[0][k] = ws.ev_live[1][k] = 0;
+        }
+        ws.prof = stage_mask != 0u;
+        ws.prof_mask = stage_mask;
     }
-    ws.prof = stage_mask != 0u;
-    ws.prof_mask = stage_mask;
     return ASP_OK;
 }
 
@@ -2819,15 +2838,21 @@ int asp_profile_read(int32_t device, double* ms_sum, int64_t* launches, int32_t 
     t_err.clear();
     if (device < 0 || device >= 64 || !ms_sum || !launches)
         return fail(ASP_ERR_INVALID, "bad argument");
-    Workspace& ws = g_ws[device];
-    std::lock_guard<std::mutex> lock(ws.mu);
-    if (ws.prof) {
-        ASP_HIP(hipSetDevice(device));
-        ASP_TRY(prof_fold(ws));
-    }
     for (int k = 0; k < nstages; ++k) {
-        ms_sum[k] = k < kStages ? ws.stage_ms[k] : 0.0;
-        launches[k] = k < kStages ? ws.stage_n[k] : 0;
+        ms_sum[k] = 0.0;
+        launches[k] = 0;
+    }
+    for (int sl = 0; sl < kMapSlots; ++sl) {  // summed over the map slots
+        Workspace& ws = slot_ws(device, sl);
+        std::lock_guard<std::mutex> lock(ws.mu);
+        if (ws.prof) {
+            ASP_HIP(hipSetDevice(device));
+            ASP_TRY(prof_fold(ws));
+        }
+        for (int k = 0; k < nstages && k < kStages; ++k) {
+            ms_sum[k] += ws.stage_ms[k];
+            launches[k] += ws.stage_n[k];
+        }
     }
     return ASP_OK;
 }
@@ -2841,8 +2866,9 @@ int asp_last_stats(int32_t device, int64_t* stats, int32_t nstats) {
 int asp_release(int32_t device) {
     int lo = device < 0 ? 0 : device, hi = device < 0 ? 63 : device;
     int ndev = asp_device_count();
-    for (int d = lo; d <= hi && d < ndev; ++d) {
-        Workspace& ws = g_ws[d];
+    for (int d = lo; d <= hi && d < ndev; ++d)
+      for (int sl = 0; sl < kMapSlots; ++sl) {
+        Workspace& ws = slot_ws(d, sl);
         std::lock_guard<std::mutex> lock(ws.mu);
         if (hipSetDevice(d) != hipSuccess) continue;
         if (ws.last_ev) (void)hipEventSynchronize(ws.last_ev);

@@ -57,7 +57,7 @@ def parse():
                     help="N > 1 Z-slab edges: equal modelled work (distributed.slab_cost) or "
                          "equal particle counts")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
-    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="budget for the bounded CPU-baseline sample")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_latest.json"),
                     help="PMC summary (tools/pmc_summary.py) for roofline.traffic")
@@ -69,6 +69,10 @@ def parse():
                          "device fp32 SoA staging (SURVEY 8(f)); the last two are not the "
                          "driver's line")
     ap.add_argument("--cube", type=int, default=512, help="cube edge (voxels), --workload cube")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams consecutive maps alternate between (each its own "
+                         "workspace slot in the library): map i + 1's binning overlaps map "
+                         "i's deposit; 1 = one stream, maps strictly in sequence")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="N > 1: wait for each map's collective before the next map")
     ap.add_argument("--no-stage-events", dest="stage_events", action="store_false",
@@ -81,10 +85,42 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def chunk_cull_counts(pos, h, grid, cs, extent):
+    """Particles the reference's chunk cull admits into each cs x cs chunk (_projector.py:
+    38-48: u in [x_lo - 2h, x_hi + 2h) on both axes), per chunk (cx * ncy + cy): the
+    regressor of the CPU-baseline cost model (the reference's per-chunk work is the O(N)
+    cull plus one r^2 per (pixel, admitted particle)).  A 2-D difference array: O(N)."""
+    import numpy as np
+    nc = grid // cs
+    w = 2.0 * extent / nc
+    r = 2.0 * np.abs(h)
+    lo = lambda a: np.clip(np.ceil((a - r + extent) / w) - 1, 0, nc)  # noqa: E731
+    hi = lambda a: np.clip(np.floor((a + r + extent) / w), -1, nc - 1)  # noqa: E731
+    x0, x1, y0, y1 = lo(pos[:, 0]), hi(pos[:, 0]), lo(pos[:, 1]), hi(pos[:, 1])
+    ok = (x0 <= x1) & (y0 <= y1)
+    x0, x1, y0, y1 = (a[ok].astype(np.int64) for a in (x0, x1, y0, y1))
+    d = np.zeros((nc + 1, nc + 1), np.int64)
+    np.add.at(d, (x0, y0), 1)
+    np.add.at(d, (x1 + 1, y0), -1)
+    np.add.at(d, (x0, y1 + 1), -1)
+    np.add.at(d, (x1 + 1, y1 + 1), 1)
+    return np.cumsum(np.cumsum(d, 0), 1)[:nc, :nc].reshape(-1).astype(np.float64)
+
+
 def cpu_baseline(args, extent):
     """The oracle's gather restatement of the reference path on the host cores, over a
-    bounded random sample of the map's 64x64 chunks (all particles culled per chunk, as
-    the reference does); extrapolated to the full map."""
+    bounded sample of the map's 64x64 chunks (all particles culled per chunk, as the
+    reference does), extrapolated to the full map with a cost model.
+
+    Chunk costs span orders of magnitude (the Plummer core's chunks admit ~10^5 particles,
+    the outskirts' a few), so a plain random sample of a few dozen chunks extrapolates
+    poorly (round 3: relative standard error 0.29).  Here: every chunk's admitted-particle
+    count x_c is computed (chunk_cull_counts, O(N)); the chunks are stratified by x_c and
+    sampled in batches of `cores` chunks of one stratum (one chunk per thread, similar
+    costs, so a batch's wall time is its chunks' cost); the batch times fit
+    t = alpha + beta * x (least squares: the O(N) cull and the per-(pixel, particle) test)
+    and the map's time is sum_c (alpha + beta x_c) / cores, its standard error from the
+    fit's covariance."""
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
@@ -98,37 +134,67 @@ def cpu_baseline(args, extent):
     T = p["T"].astype(np.float32).astype(np.float64)
     del p
     maps = [m * T, m] if args.map == "weighted" else [m]
-    log(f"[cpu] host data {time.time() - t0:.1f}s; sampling chunks with {cores} threads")
     cs = 64
     nch = (args.grid // cs) ** 2
-    order = np.random.default_rng(0).permutation(nch)
-    done, spent, batch = 0, 0.0, max(cores, 8)
-    per_chunk = []  # seconds per chunk of each batch (the batches are random samples)
-    while done < nch and spent < args.cpu_seconds:
-        ids = order[done:done + batch]
+    x = chunk_cull_counts(pos, h, args.grid, cs, extent)
+    u, v = np.ascontiguousarray(pos[:, 0]), np.ascontiguousarray(pos[:, 1])
+    del pos
+    img = np.zeros((args.grid, args.grid))  # shared: calls write disjoint chunks
+    ext4 = [-extent, extent] * 2
+    log(f"[cpu] host data + chunk counts {time.time() - t0:.1f}s; sampling with {cores} threads")
+
+    def one_chunk(c):  # the chunk's reference-style create_image call(s), one thread
         t = time.perf_counter()
         for A in maps:
-            pyoracle.create_image(pos, h, A, (args.grid, args.grid), cs, 2, *([-extent, extent] * 2),
-                                  kernel=args.kernel, nthreads=cores, chunk_ids=ids)
-        dt = time.perf_counter() - t
-        spent += dt
-        done += ids.size
-        per_chunk.append(dt / ids.size)
-    full_s = spent * nch / done
+            pyoracle.create_image_cols(u, v, h, A, (args.grid, args.grid), cs, *ext4,
+                                       kernel=args.kernel, nthreads=1, chunk_ids=[c], out=img)
+        return time.perf_counter() - t
+
+    rng = np.random.default_rng(0)
+    S = 8  # strata: equal chunk counts, by admitted particles
+    order = np.argsort(x, kind="stable")
+    strata = [rng.permutation(order[k * nch // S:(k + 1) * nch // S]) for k in range(S)]
+    from concurrent.futures import ThreadPoolExecutor  # ctypes releases the GIL
+    ids, secs = [], []
+    spent, rounds = 0.0, 0
+    with ThreadPoolExecutor(cores) as pool:
+        # rounds of `cores` chunks, one per thread, drawn round-robin from the strata (so
+        # every round spans the x range); each chunk timed on its own thread while the
+        # other threads run theirs (the contention of the full-map run)
+        while spent < args.cpu_seconds and rounds < 64:
+            batch = [int(strata[(rounds * cores + j) % S][(rounds * cores + j) // S])
+                     for j in range(cores) if (rounds * cores + j) // S < nch // S]
+            if not batch:
+                break
+            t = time.perf_counter()
+            secs += list(pool.map(one_chunk, batch))
+            spent += time.perf_counter() - t
+            ids += batch
+            rounds += 1
+    ids = np.array(ids)
+    secs = np.array(secs)
+    done = ids.size
+    X = np.stack([np.ones(done), x[ids]], axis=1)
+    theta, *_ = np.linalg.lstsq(X, secs, rcond=None)
+    resid = secs - X @ theta
+    cov = (resid @ resid / max(1, done - 2)) * np.linalg.pinv(X.T @ X)
+    g = np.array([nch, x.sum()]) / cores  # all chunks, spread over the cores
+    full_s = float(g @ theta)
+    rse = float(np.sqrt(max(g @ cov @ g, 0.0)) / full_s) if full_s > 0 else None
+    model = {"alpha_s": float(theta[0]), "beta_s_per_particle": float(theta[1]),
+             "chunks_timed": int(done), "rounds": rounds,
+             "plain_extrapolation_mpix": round(args.grid ** 2 / (secs.mean() * nch / cores) / 1e6, 6)}
     mpix = args.grid * args.grid / full_s / 1e6
-    # standard error of the extrapolation: spread of the per-batch chunk times (random
-    # chunks: the Plummer core's chunks cost far more than the outskirts'), with the
-    # finite-population correction for sampling `done` of `nch` chunks
-    b = np.asarray(per_chunk)
-    rse = (float(b.std(ddof=1) / b.mean() / np.sqrt(b.size) * np.sqrt(1.0 - done / nch))
-           if b.size > 1 else None)
     return {"value": mpix, "unit": "Mpixels/s", "cores": cores, "kind": "port",
             "rel_stderr": None if rse is None else round(rse, 4),
-            "particles_per_s": args.n / full_s,
-            "sample": f"{done} of {nch} random 64x64 chunks of the {args.n:.0e}-particle "
-                      f"{args.grid}^2 map ({len(maps)} reference-style create_image call(s)), "
-                      f"oracle gather restatement (fp64, per-chunk O(N) cull), {spent:.1f}s "
-                      f"measured, extrapolated to the full map"}
+            "particles_per_s": args.n / full_s, "model": model,
+            "sample": f"{done} of {nch} 64x64 chunks of the {args.n:.0e}-particle "
+                      f"{args.grid}^2 map, each timed on one of {cores} concurrent threads "
+                      f"({len(maps)} reference-style create_image call(s) per chunk; chunks "
+                      f"drawn round-robin from {S} strata by admitted particles), oracle "
+                      f"gather restatement (fp64, per-chunk O(N) cull), {spent:.1f}s "
+                      f"measured; map time = sum over all {nch} chunks of the fitted "
+                      f"alpha + beta * admitted, / cores"}
 
 
 def run_cube(args, world, rank, local, dev):
@@ -554,35 +620,49 @@ def main():
     # N > 1 double-buffers them: the collective of map i (RCCL's stream) overlaps the
     # binning + deposit of map i + 1 (compute stream); map i + 2 reuses map i's buffer
     # only after its collective (stream-ordered wait).
-    nbuf = 2 if (world > 1 and args.pipeline) else 1
+    # Consecutive maps alternate between --streams HIP streams (each with its own output
+    # buffer; the library gives each stream its own workspace slot): the binning of map
+    # i + 1 runs beside the deposit of map i.  --streams 1: one stream.
+    ns = max(1, args.streams)
+    streams = ([torch.cuda.current_stream(dev)] if ns == 1 else
+               [torch.cuda.Stream(device=dev) for _ in range(ns)])
+    nbuf = max(ns, 2 if (world > 1 and args.pipeline) else 1)
     bufs = [torch.empty((2 if a1 is not None else 1, G, G), dtype=torch.float32, device=dev)
             for _ in range(nbuf)]
     pending = [None]
     it = [0]
     last = [None]  # the last completed map's (out0, out1) as the collective returns them
 
-    def step(pipelined=nbuf > 1):
-        maps = bufs[it[0] % nbuf]
+    def step(pipelined=world > 1 and args.pipeline):
+        k = it[0]
         it[0] += 1
+        maps = bufs[k % nbuf]
         o0, o1 = maps[0], (maps[1] if a1 is not None else None)
+        with torch.cuda.stream(streams[k % ns]):
+            if world > 1:
+                p = project2d_sharded(u, v, h, a0, a1, image_size=(G, G), extent=ext,
+                                      kernel=args.kernel, ratio=ratio, op=args.op, out0=o0,
+                                      out1=o1, deterministic=args.deterministic,
+                                      async_op=pipelined)
+            else:
+                last[0] = project2d(u, v, h, a0, a1, image_size=(G, G), extent=ext,
+                                    kernel=args.kernel, ratio=ratio, out0=o0, out1=o1,
+                                    deterministic=args.deterministic)
         if world > 1:
-            p = project2d_sharded(u, v, h, a0, a1, image_size=(G, G), extent=ext,
-                                  kernel=args.kernel, ratio=ratio, op=args.op, out0=o0,
-                                  out1=o1, deterministic=args.deterministic,
-                                  async_op=pipelined)
             if pipelined:
                 if pending[0] is not None:
-                    last[0] = pending[0].wait()  # map i - 1: stream-ordered, no host block
+                    # map k - 1's collective: the stream that next writes its buffer (map
+                    # k - 1 + nbuf) waits for it -- stream-ordered, no host block
+                    with torch.cuda.stream(streams[(k - 1 + nbuf) % ns]):
+                        last[0] = pending[0].wait()
                 pending[0] = p
             else:
                 last[0] = p
-            return
-        last[0] = project2d(u, v, h, a0, a1, image_size=(G, G), extent=ext, kernel=args.kernel,
-                            ratio=ratio, out0=o0, out1=o1, deterministic=args.deterministic)
 
     def drain():
         if pending[0] is not None:
-            last[0] = pending[0].wait()
+            with torch.cuda.stream(streams[(it[0] - 1) % ns]):
+                last[0] = pending[0].wait()
             pending[0] = None
 
     for _ in range(args.warmup):
@@ -616,17 +696,19 @@ def main():
     # N > 1: the single-map LATENCY as well (each map's collective completed before the
     # next map starts), beside the overlapped throughput of the timed region
     latency_ms = None
-    if world > 1 and nbuf > 1:
+    if nbuf > 1:
         k_lat = max(1, min(args.steps, 5))
-        dist.barrier()
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize()
         tl = time.perf_counter()
         for _ in range(k_lat):
             step(pipelined=False)
             torch.cuda.synchronize()
-        dist.barrier()
         tt = torch.tensor([time.perf_counter() - tl], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        if world > 1:
+            dist.barrier()
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         latency_ms = float(tt.item()) / k_lat * 1e3
         out0, out1 = last[0]
     st = stats(local)
@@ -694,15 +776,17 @@ def main():
                    "map": args.map, "parallelism": f"zslab{world}" if world > 1 else "single",
                    **({"backend": backend_label} if world > 1 else {}),
                    "accumulation": "int64 fixed point" if args.deterministic else "fp64",
-                   "collective_overlap": nbuf > 1,
+                   "collective_overlap": world > 1 and args.pipeline,
+                   "streams": ns,
                    **({"slab_weight": args.slab_weight, "collective": args.op,
                        "partition": "Z-slab split of the generated particles before the "
                                     "timed region (untimed, as a reader-split snapshot "
                                     "needs none)"} if world > 1 else {})},
         "particles_per_s": pps,
         **({"latency_ms_per_map": round(latency_ms, 4),
-            "latency_note": "one map at a time (--no-pipeline form): binning + deposit + "
-                            "collective + ratio, max over ranks"} if latency_ms else {}),
+            "latency_note": "one map at a time, synchronised (no overlap of maps): binning + "
+                            "deposit (+ collective) + ratio, max over ranks"}
+           if latency_ms else {}),
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,

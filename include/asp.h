@@ -53,6 +53,15 @@ extern "C" {
                                    * inputs go through pinned bounce buffers (two 32 MiB
                                    * pieces, CPU copy overlapping the DMA)                 */
 
+#define ASP_F_WEIGHTED 0x20 /* a1 is a weight and a0 = a1 * value (mass-weighted maps;
+                             * implied by ASP_F_RATIO).  With ASP_F_DETERMINISTIC the two
+                             * maps are quantised consistently: a pair whose weight term
+                             * a1 W is below 2^18 units of its tile's fixed-point scale
+                             * (2^-31 n_t max|a1 W|) is left out of BOTH maps, so every
+                             * pixel's out0 / out1 stays a weighted mean of the values to
+                             * 2^-18 of the tile's largest.  No effect on
+                             * the default fp64 accumulation.                          */
+
 /* asp_project2d_f64 axis: cull on axis c's columns (the reference's mixed spellings) */
 #define ASP_AXIS_CULL(c) (((c) + 1) << 4)
 

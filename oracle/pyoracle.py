@@ -105,17 +105,41 @@ def kernel_eval(kernel, r, h):
 
 def create_image(positions, smoothing_lengths, particle_properties, image_size, chunk_size,
                  projection_axis, x_min, x_max, y_min, y_max, kernel="cubic", nthreads=0,
-                 chunk_ids=None):
-    """Reference-exact restatement of ``create_image`` (gather, fp64)."""
+                 chunk_ids=None, out=None):
+    """Reference-exact restatement of ``create_image`` (gather, fp64).  ``out``: a
+    C-contiguous float64 (nx, ny) array written in place (with ``chunk_ids`` only those
+    chunks' pixels are touched, so concurrent calls on disjoint chunks may share it)."""
     u, v, cu, cv = _axes(positions, projection_axis)
     h, A = _f64(smoothing_lengths), _f64(particle_properties)
     nx, ny = int(image_size[0]), int(image_size[1])
-    img = np.zeros((nx, ny), dtype=np.float64)
+    if out is None:
+        img = np.zeros((nx, ny), dtype=np.float64)
+    else:
+        img = out
+        if img.shape != (nx, ny) or img.dtype != np.float64 or not img.flags.c_contiguous:
+            raise ValueError("out must be a C-contiguous float64 (nx, ny) array")
     ids = None if chunk_ids is None else np.ascontiguousarray(chunk_ids, dtype=np.int64)
     rc = lib().oracle_create_image(_p(u), _p(v), _p(cu), _p(cv), _p(h), _p(A), u.size, nx, ny, int(chunk_size),
                                    float(x_min), float(x_max), float(y_min), float(y_max),
                                    KERNELS[kernel], _p(ids, _i64), 0 if ids is None else ids.size,
                                    int(nthreads), _p(img))
+    if rc != 0:
+        raise RuntimeError(f"oracle_create_image failed ({rc})")
+    return img
+
+
+def create_image_cols(u, v, h, A, image_size, chunk_size, x_min, x_max, y_min, y_max,
+                      kernel="cubic", nthreads=0, chunk_ids=None, out=None):
+    """``create_image`` on prepared C-contiguous float64 columns (u, v = the projected
+    axes, cull on the same columns), no per-call column copies: the CPU baseline's
+    per-chunk timing calls this from a thread pool on a shared ``out``."""
+    nx, ny = int(image_size[0]), int(image_size[1])
+    img = np.zeros((nx, ny), dtype=np.float64) if out is None else out
+    ids = None if chunk_ids is None else np.ascontiguousarray(chunk_ids, dtype=np.int64)
+    rc = lib().oracle_create_image(_p(u), _p(v), None, None, _p(h), _p(A), u.size, nx, ny,
+                                   int(chunk_size), float(x_min), float(x_max), float(y_min),
+                                   float(y_max), KERNELS[kernel], _p(ids, _i64),
+                                   0 if ids is None else ids.size, int(nthreads), _p(img))
     if rc != 0:
         raise RuntimeError(f"oracle_create_image failed ({rc})")
     return img

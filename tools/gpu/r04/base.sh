@@ -14,12 +14,18 @@ fi
 step bench
 timeout -k 10 300 python bench.py --cpu-baseline off > $o/bench_n1.json 2> $o/bench_n1.err || { tail -5 $o/bench_n1.err; exit 1; }
 cut -c1-900 $o/bench_n1.json
+step bench one stream
+timeout -k 10 300 python bench.py --cpu-baseline off --streams 1 > $o/bench_s1.json 2> $o/bench_s1.err || { tail -5 $o/bench_s1.err; exit 1; }
+cut -c1-400 $o/bench_s1.json
 step bench no events
 timeout -k 10 300 python bench.py --cpu-baseline off --no-stage-events > $o/bench_noev.json 2> $o/bench_noev.err || { tail -5 $o/bench_noev.err; exit 1; }
 cut -c1-300 $o/bench_noev.json
+step bench deterministic
+timeout -k 10 300 python bench.py --cpu-baseline off --deterministic > $o/bench_det.json 2> $o/bench_det.err; echo "rc=$?"; tail -2 $o/bench_det.err
+python -c "import json;d=json.load(open('$o/bench_det.json'));print('det', d['ms_per_step'], d['output_ok'], {k:round(v['ms_per_step'],4) for k,v in d['stages'].items()})"
 step shard
 for i in 1 2; do
-timeout -k 10 300 python bench.py --cpu-baseline off --n 12500000 --steps 30 > $o/shard_$i.json 2> $o/shard_$i.err || { tail -5 $o/shard_$i.err; exit 1; }
+timeout -k 10 300 python bench.py --cpu-baseline off --n 12500000 --steps 30 --streams $i > $o/shard_$i.json 2> $o/shard_$i.err || { tail -5 $o/shard_$i.err; exit 1; }
 python -c "import json;d=json.load(open('$o/shard_$i.json'));print('shard', d['ms_per_step'], {k:round(v['ms_per_step'],4) for k,v in d['stages'].items()})"
 done
 if [ -z "$NOPROF" ]; then
@@ -33,4 +39,6 @@ step decomposition probe
 timeout -k 10 300 python tools/decomp_probe.py --interference --out $o/decomp.json > $o/decomp.log 2>&1 || { tail -5 $o/decomp.log; exit 1; }
 tail -8 $o/decomp.log
 fi
+step overlap probe
+timeout -k 10 300 python tools/overlap_probe.py --out $o/overlap.json > $o/overlap.log 2>&1; echo "rc=$?"; tail -6 $o/overlap.log
 step done
