@@ -22,7 +22,6 @@ ASP_F_RATIO = 0x2
 ASP_F_ACCUMULATE = 0x4
 ASP_F_DETERMINISTIC = 0x8
 ASP_F_DEVICE_OUTPUTS = 0x10
-ASP_F_WEIGHTED = 0x20
 
 ASP_PB_WRAP = 0x1
 ASP_PB_SHIFT_ORIGIN = 0x2

@@ -35,17 +35,13 @@ def _check(t, name, n=None, device=None):
 
 def project2d(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
               kernel="cubic", ratio: bool = False, accumulate: bool = False, out0=None,
-              out1=None, stream=None, deterministic: bool = False, rows=None,
-              weighted: bool = False):
+              out1=None, stream=None, deterministic: bool = False, rows=None):
     """Project device-resident particles; returns ``(out0, out1)`` (out1 None for one map).
 
     ``extent = (u_min, u_max, v_min, v_max)``; images are (nx, ny) float32 tensors on the
     particles' device.  ``ratio`` turns (sum a0 W, sum a1 W) into their ratio in out0.
     ``rows = (row_lo, row_hi)``: only those image rows (asp_project2d_rows, the row-slab
     decomposition): outputs are (row_hi - row_lo, ny), each pixel the whole image's.
-    ``weighted`` (ASP_F_WEIGHTED, implied by ``ratio``): a1 is a weight and a0 = a1 * value;
-    with ``deterministic`` the two maps are quantised consistently (a ratio formed later,
-    e.g. after a cross-GPU sum, stays a weighted mean).
     """
     import torch
     dev = u.device
@@ -56,6 +52,8 @@ def project2d(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
         _check(a1, "a1", n, dev)
     nx, ny = int(image_size[0]), int(image_size[1])
     r0, r1 = (0, nx) if rows is None else (int(rows[0]), int(rows[1]))
+    if not 0 <= r0 < r1 <= nx:
+        raise ValueError(f"rows must satisfy 0 <= row_lo < row_hi <= nx, got {(r0, r1)}")
     mx = r1 - r0  # rows written
     if out0 is None:
         out0 = torch.empty((mx, ny), dtype=torch.float32, device=dev)
@@ -72,8 +70,6 @@ def project2d(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
         flags |= _lib.ASP_F_ACCUMULATE
     if deterministic:
         flags |= _lib.ASP_F_DETERMINISTIC
-    if weighted:
-        flags |= _lib.ASP_F_WEIGHTED
     if stream is None:
         stream = torch.cuda.current_stream(dev).cuda_stream
     P = _lib.ptr
@@ -113,8 +109,7 @@ def _f64_arg(a, name, n, shape_tail=()):
 def project2d_f64(positions, h, a0, a1=None, *, projection_axis=2, image_size, extent,
                   chunk_size: int = 64, kernel="cubic", ratio: bool = False,
                   accumulate: bool = False, out0=None, out1=None, device: int = 0,
-                  stream=None, deterministic: bool = False, device_out: bool = False,
-                  weighted: bool = False):
+                  stream=None, deterministic: bool = False, device_out: bool = False):
     """asp_project2d_f64: the reader's float64 arrays (positions (N, 3), h, a0[, a1]) --
     host NumPy arrays or float64 device tensors -- projected with the reference's fp64
     decisions on those values.  ``projection_axis``: an axis (int 0/1/2, enum, "x") or a
@@ -147,8 +142,7 @@ def project2d_f64(positions, h, a0, a1=None, *, projection_axis=2, image_size, e
     nx, ny = int(image_size[0]), int(image_size[1])
     nout = 1 if a1 is None else 2
     flags = (_lib.ASP_F_RATIO if ratio else 0) | (_lib.ASP_F_ACCUMULATE if accumulate else 0) | \
-        (_lib.ASP_F_DETERMINISTIC if deterministic else 0) | \
-        (_lib.ASP_F_WEIGHTED if weighted else 0)
+        (_lib.ASP_F_DETERMINISTIC if deterministic else 0)
     if on_dev:
         dev = pos.device
         device = dev.index or 0

@@ -164,9 +164,7 @@ def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
     if op.startswith("reduce_scatter") and world > 1 and nx % world:
         raise ValueError("reduce_scatter needs nx divisible by the world size")
     proj = project2d if projector is None else projector
-    # deterministic ratio maps: the components are quantised consistently (ASP_F_WEIGHTED)
-    # so the ratio formed after the sum stays a weighted mean
-    kw = {"deterministic": True, **({"weighted": True} if ratio else {})} if deterministic else {}
+    kw = {"deterministic": True} if deterministic else {}
     o0, o1 = proj(u, v, h, a0, a1, image_size=image_size, extent=extent,
                   chunk_size=chunk_size, kernel=kernel, ratio=False, out0=out0, out1=out1, **kw)
     outs = [o0] if o1 is None else [o0, o1]
@@ -232,14 +230,13 @@ def project2d_sharded_host(positions, h, a0, a1=None, *, projection_axis=2, imag
 
 
 def project2d_f64_local(positions, h, a0, a1=None, *, projection_axis, image_size, extent,
-                        chunk_size, kernel, out0, out1, device, deterministic=False,
-                        weighted=False):
+                        chunk_size, kernel, out0, out1, device, deterministic=False):
     """One rank's fp64 host arrays -> its device map(s) (no ratio: formed after the sum)."""
     from .device import project2d_f64
     return project2d_f64(positions, h, a0, a1, projection_axis=projection_axis,
                          image_size=image_size, extent=extent, chunk_size=chunk_size,
                          kernel=kernel, out0=out0, out1=out1, device=device,
-                         deterministic=deterministic, device_out=True, weighted=weighted)
+                         deterministic=deterministic, device_out=True)
 
 
 # ---------------------------------------------------------------------------------------
@@ -339,47 +336,38 @@ def project3d_sharded(x, y, z, h, a, *, cube_size, extent, kernel="cubic",
 # particle goes to each rank whose rows its 2h footprint reaches; each rank projects only
 # its rows (asp_project2d_rows: fewer tiles binned per rank, no grid reduction at all).
 # ---------------------------------------------------------------------------------------
-TILE = 64
-
-
 def row_slabs(nx: int, world_size: int, u=None, u_extent=None, weights=None,
-              sample: int = 1 << 20, seed: int = 0):
-    """Row bounds R (world_size + 1 ints, R[0] = 0, R[-1] = nx), every inner bound a
-    multiple of 64 (whole GPU tile rows, as asp_project2d_rows requires).  Without ``u``
-    the tile rows are split evenly; with the particles' ``u`` (device or host tensor) and
-    ``u_extent`` = (u_min, u_max) the split equalises the particle count -- or the summed
-    ``weights`` -- per slab (a random subsample of 2^20 decides)."""
+              sample: int = 1 << 22, seed: int = 0):
+    """Row bounds R (world_size + 1 ints, R[0] = 0, R[-1] = nx, strictly increasing).
+    Without ``u`` the rows are split evenly; with the particles' ``u`` (device or host
+    tensor) and ``u_extent`` = (u_min, u_max) the split equalises the particle count -- or
+    the summed ``weights`` -- per slab, at one-row granularity (a random subsample of 2^22
+    decides; asp_project2d_rows takes any row range)."""
     import torch
-    T = -(-nx // TILE)
     W = int(world_size)
     if W <= 1:
         return [0, nx]
-    if T < W:
-        raise ValueError(f"{nx} rows are {T} tile rows of 64: fewer than {W} row slabs")
+    if nx < W:
+        raise ValueError(f"{nx} rows cannot make {W} row slabs")
     if u is None or u.shape[0] == 0:
-        inner = [TILE * ((T * r) // W) for r in range(1, W)]
+        inner = [(nx * r) // W for r in range(1, W)]
     else:
         lo, hi = (float(e) for e in u_extent)
         g = torch.Generator(device=u.device)
         g.manual_seed(seed)
         k = min(u.shape[0], sample)
         idx = torch.randint(0, u.shape[0], (k,), generator=g, device=u.device)
-        t = ((u[idx].double() - lo) / ((hi - lo) / nx) / TILE).floor().clamp(0, T - 1).long()
+        row = ((u[idx].double() - lo) / ((hi - lo) / nx)).floor().clamp(0, nx - 1).long()
         w = torch.ones(k, dtype=torch.float64, device=u.device) if weights is None \
             else weights[idx].double()
-        per = torch.zeros(T, dtype=torch.float64, device=u.device).index_add_(0, t, w)
+        per = torch.zeros(nx, dtype=torch.float64, device=u.device).index_add_(0, row, w)
         c = torch.cumsum(per, 0)
         tot = float(c[-1])
-        inner = []
-        for r in range(1, W):
-            # the first tile row at which the cumulative weight reaches r / W of the total
-            j = int(torch.searchsorted(c, torch.tensor([tot * r / W], dtype=torch.float64,
-                                                       device=c.device)).item()) + 1
-            inner.append(TILE * j)
-    # at least one tile row per slab: bound i in [64 i, 64 (T - W + i)], increasing
-    R = [0]
+        t = torch.tensor([tot * r / W for r in range(1, W)], dtype=torch.float64, device=c.device)
+        inner = [int(j) + 1 for j in torch.searchsorted(c, t).tolist()]
+    R = [0]  # strictly increasing: bound i in [i, nx - W + i]
     for i, b in enumerate(inner, start=1):
-        R.append(min(max(b, R[-1] + TILE), TILE * (T - W + i)))
+        R.append(min(max(b, R[-1] + 1), nx - W + i))
     R.append(nx)
     return R
 

@@ -63,14 +63,11 @@ def _run(positions, smoothing_lengths, props, projection_axis, image_size, chunk
     pos = np.asarray(positions)
     if pos.ndim != 2 or pos.shape[1] != 3:
         raise ValueError(f"positions must have shape (N, 3), got {pos.shape}")
-    # two maps are always (w * v, w) here: ASP_F_WEIGHTED keeps their fixed-point
-    # quantisation consistent when the ratio is formed on the host (return_components)
     return project2d_f64(pos, smoothing_lengths, props[0], props[1] if len(props) > 1 else None,
                          projection_axis=reference_axes(projection_axis), image_size=(nx, ny),
                          extent=tuple(float(np.asarray(e)) for e in extent),
                          chunk_size=chunk_size, kernel=kernel_id, ratio=ratio,
-                         deterministic=deterministic, device=device, out0=out0, out1=out1,
-                         weighted=len(props) > 1)
+                         deterministic=deterministic, device=device, out0=out0, out1=out1)
 
 
 def _run_callable(positions, smoothing_lengths, props, projection_axis, image_size, chunk_size,

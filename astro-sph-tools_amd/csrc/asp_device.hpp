@@ -41,10 +41,6 @@ constexpr int kWideTilesDefault = 256;  // particles overlapping more tiles take
 constexpr int kScaleBits = 49;     // per-tile bound n_t * max|c| maps to <= 2^49 (f2fix: < 2^51)
 constexpr int kAccF64 = 0;         // LDS fp64 accumulation
 constexpr int kAccFix = 1;         // LDS int64 fixed point (deterministic)
-// Weighted fixed point (ASP_F_WEIGHTED): pairs whose weight term (map 1) is below this many
-// units of the tile's scale are left out of both maps, so each kept term of the two maps
-// carries <= 2^-19 relative rounding and out0 / out1 stays a weighted mean.
-constexpr float kTailUnits = 262144.0f;  // 2^18
 
 struct Grid {
     double x_min, y_min;
@@ -99,7 +95,6 @@ struct Prep {
     float s0, s1;  // a * norm(h) (kAccF64) or a * norm(h) * 2^k_tile (kAccFix)
     float thr;   // (2h)^2 in fp32
     float band;  // |r2 - thr| <= band: the fp32 decision is not trusted (inf: never)
-    float tmin;  // kAccFix, weighted maps: terms with |s1 W| < tmin are dropped (0: none)
     int p;       // particle index (the fp64 re-decision reads the caller's arrays there)
     Box b;
 };
@@ -327,7 +322,6 @@ __device__ __forceinline__ bool prep_record(const Grid& g, const Src64& s, int p
     P.p = p;
     set_band(P, rec_thr(h), rec_band(g.mg, h));
     P.hinv = __builtin_amdgcn_rcpf(h);  // value path only (fp32 tolerance)
-    P.tmin = 0.0f;
     if constexpr (ACC == kAccFix) {
         P.s0 = (float)ldexp(term_coef<KID>(a0, h), k0);
         P.s1 = (float)ldexp(term_coef<KID>(a1, h), k1);

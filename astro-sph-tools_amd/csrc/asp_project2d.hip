@@ -486,8 +486,6 @@ __device__ __forceinline__ void accumulate(const Prep& P, float r2, unsigned lon
                                            unsigned long long* acc1, int k) {
     float q = __builtin_amdgcn_sqrtf(r2) * P.hinv;  // v_sqrt_f32, 1 ulp
     float w = kernel_shape<KID>(q);
-    if constexpr (ACC == kAccFix && NOUT == 2)
-        if (fabsf(P.s1 * w) < P.tmin) return;  // weighted fixed point: both maps or neither
     acc_add<ACC>(&acc0[k], P.s0 * w);
     if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k], P.s1 * w);
 }
@@ -558,8 +556,7 @@ __device__ __forceinline__ bool clip(Box& b, int X0, int Y0, int TW, int TH) {
 // fixed-point mode the tile's power-of-two scale applied (ldexp: exact).
 template <int ACC>
 __device__ __forceinline__ void rec_prep(const float4& r0, const float4& r1, int X0, int Y0,
-                                         int2 kk, Prep& P, float tmin = 0.0f) {
-    P.tmin = tmin;
+                                         int2 kk, Prep& P) {
     P.u = r0.x;
     P.v = r0.y;
     P.h = r0.z;
@@ -588,7 +585,6 @@ __device__ __forceinline__ void load_rec(const float4* recs, long long i, float4
 constexpr int kTilePix = kTile * kTile;
 constexpr int kFlagAccumulate = 1;
 constexpr int kFlagRatio = 2;  // fused ratio: out0 <- map0 / map1
-constexpr int kFlagTail = 4;   // weighted fixed point (ASP_F_WEIGHTED): kTailUnits rule
 
 // Corner offset tables: xt[k] = fl32(k * pitch_x), yt[k] = fl32(k * pitch_y) for k < 64 --
 // the corner k pixels from a record's box origin, in the frame of the record's (u, v)
@@ -760,18 +756,15 @@ __device__ __forceinline__ bool small3_fast(const Prep& P, int bw, int bh, int X
         f2v t0 = w * P.s0, t1 = w * P.s1;
         f2v c = f2v{wc[i], wc[i]} * f2v{P.s0, P.s1};
         const int k = base + i * kRow;
-        // weighted fixed point: a pair whose weight term is below tmin units is dropped
-        // from both maps (tmin = 0 otherwise: the test is always true)
-        const bool keep = !(ACC == kAccFix && NOUT == 2);
-        if (r2[i].x < P.thr && (keep || fabsf(t1.x) >= P.tmin)) {
+        if (r2[i].x < P.thr) {
             acc_add<ACC>(&acc0[k], t0.x);
             if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k], t1.x);
         }
-        if (r2[i].y < P.thr && (keep || fabsf(t1.y) >= P.tmin)) {
+        if (r2[i].y < P.thr) {
             acc_add<ACC>(&acc0[k + 1], t0.y);
             if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k + 1], t1.y);
         }
-        if (r2c[i] < P.thr && (keep || fabsf(c.y) >= P.tmin)) {
+        if (r2c[i] < P.thr) {
             acc_add<ACC>(&acc0[k + 2], c.x);
             if constexpr (NOUT == 2) acc_add<ACC>(&acc1[k + 2], c.y);
         }
@@ -789,7 +782,7 @@ template <int KID, int NOUT, int ACC>
 __device__ __forceinline__ void deferred(const Grid& g, const Src64& s,
                                          const float4* __restrict__ recs, long long start,
                                          const int* dlist, int first, int cnt, int X0, int Y0,
-                                         int2 kk, float tmin, const float* xt, const float* yt,
+                                         int2 kk, const float* xt, const float* yt,
                                          unsigned long long* acc0, unsigned long long* acc1,
                                          int lane) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -801,7 +794,7 @@ __device__ __forceinline__ void deferred(const Grid& g, const Src64& s,
     float4 r0, r1;
     load_rec(recs, start + idx, r0, r1);
     Prep P;
-    rec_prep<ACC>(r0, r1, X0, Y0, kk, P, tmin);
+    rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
     small_box<KID, NOUT, ACC, 4>(g, s, P, P.b.x1 - P.b.x0 + 1, P.b.y1 - P.b.y0 + 1, X0, Y0, xt,
                                  yt, acc0, acc1);
 }
@@ -842,7 +835,6 @@ struct GAcc {
     f2 p0[4], p1[4];                  // kAccF64 fp32 partials, pixels (2k, 2k + 1)
     double* t0;
     double* t1;
-    float tmin = 0.0f;  // kAccFix weighted maps: pairs with |s1 W| < tmin dropped from both
     __device__ __forceinline__ void init(double* tot) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -867,7 +859,6 @@ struct GAcc {
     // pixel j += w * (s0, s1)
     __device__ __forceinline__ void add(int j, float w, float s0, float s1) {
         if constexpr (ACC == kAccFix) {
-            if (NOUT == 2 && fabsf(s1 * w) < tmin) return;
             a0[j] += f2fix(s0 * w);
             if (NOUT == 2) a1[j] += f2fix(s1 * w);
         } else {
@@ -938,9 +929,12 @@ __device__ __forceinline__ GOwn gather_owner(int w) {  // w: the region (uniform
 __device__ __forceinline__ float corner_off_x(const Grid& g, int k) { return (float)((double)k * g.psx); }
 __device__ __forceinline__ float corner_off_y(const Grid& g, int k) { return (float)((double)k * g.psy_pix); }
 
-// The corner coordinates of the thread's pixels: 2 rows, 4 columns.
+// The corner coordinates of the thread's pixels: 2 rows, 4 columns; and (wave-uniform) the
+// corner span of each of the region's 8 x 16 half block rows: rows xl[r]..xh[r] of block
+// row r, columns yl[k]..yh[k] of column half k.
 struct GCorner {
     float X[2], Y[4];
+    float xl[2], xh[2], yl[2], yh[2];
 };
 __device__ __forceinline__ GCorner gather_corners(const Grid& g, const GOwn& o) {
     GCorner c;
@@ -948,7 +942,39 @@ __device__ __forceinline__ GCorner gather_corners(const Grid& g, const GOwn& o) 
     c.X[1] = corner_off_x(g, o.row(4));
 #pragma unroll
     for (int k = 0; k < 4; ++k) c.Y[k] = corner_off_y(g, o.col(k));
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        c.xl[r] = corner_off_x(g, o.r0 + 8 * r);
+        c.xh[r] = corner_off_x(g, o.r0 + 8 * r + 7);
+        c.yl[r] = corner_off_y(g, o.c0 + 16 * r);
+        c.yh[r] = corner_off_y(g, o.c0 + 16 * r + 15);
+    }
     return c;
+}
+
+// The region's half block rows the entry's DISC can reach (bit 2 r + k: block row r,
+// column half k), from the distance between (u, v) and each half row's corner rectangle
+// (closest point by clamping).  Conservative: a skipped half row has every pixel at
+// fp32 distance^2 >= lim = (2h)^2 (1 + 2^-8) from the particle -- far outside any rounding
+// of the pair distance -- so the edge form (§3) gives each of them exactly 0 and skipping
+// them changes no sum.  Computed per lane for its own entry before the walk (vectorised
+// over the 64 entries), so the walk tests bits instead of box bounds.
+__device__ __forceinline__ unsigned edge_mask(const GCorner& c, float u, float v, float thr) {
+    float dx2[2], dy2[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const float dx = u - fminf(fmaxf(u, c.xl[r]), c.xh[r]);
+        const float dy = v - fminf(fmaxf(v, c.yl[r]), c.yh[r]);
+        dx2[r] = dx * dx;
+        dy2[r] = dy * dy;
+    }
+    const float lim = thr * (1.0f + 0x1p-8f);
+    unsigned m = 0u;
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) m |= (dx2[r] + dy2[k] < lim) ? 1u << (2 * r + k) : 0u;
+    return m;
 }
 
 __device__ __forceinline__ GEntry make_gentry(const Prep& P, int X0, int Y0, float scale) {
@@ -987,41 +1013,11 @@ __device__ __forceinline__ unsigned block_hits(unsigned box, const GOwn& o) {
     return m;
 }
 
-// One (uniform) entry, edge-continuous kernel (cubic / Wendland) on a square grid
-// without a mixed cull: W by edge_shape for every pixel of every block the box meets --
-// no decision at all.  A pixel the reference excludes has exact r >= 2h, so its fp32 q is
-// >= 2 (1 - 2^-21) and its term 0 or < 2^-60 W(0); one it includes the same way.  Pixels
-// of a met block outside the box have r >= 2h as well (the box is a superset of the disc).
-template <int KID, int NOUT, int ACC>
-__device__ __forceinline__ void gather_entry_edge(const GEntry& E, const GOwn& o,
-                                                  const GCorner& c, GAcc<NOUT, ACC>& ga) {
-    // Met 8 x 16 half block rows are evaluated whole (2 pixels per lane, one packed op
-    // each): a pixel outside the box contributes exactly 0, as above.
-    const int x0 = E.box & 255u, x1 = (E.box >> 8) & 255u;
-    const int y0 = (E.box >> 16) & 255u, y1 = E.box >> 24;
-    const f2 hv = {-E.hinv, -E.hinv};
-    const f2 vs = {E.v * E.hinv, E.v * E.hinv};  // in units of h
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const int br = o.r0 + 8 * r;
-        if (x0 <= br + 7 && x1 >= br) {
-            const float dxs = (E.u - c.X[r]) * E.hinv;
-            const f2 dx2 = {dxs * dxs, dxs * dxs};
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int bc = o.c0 + 16 * k;
-                if (y0 <= bc + 15 && y1 >= bc) {
-                    const f2 dys = __builtin_elementwise_fma(hv, (f2){c.Y[2 * k], c.Y[2 * k + 1]}, vs);
-                    const f2 r2 = __builtin_elementwise_fma(dys, dys, dx2);
-                    f2 q;
-                    q.x = __builtin_amdgcn_sqrtf(r2.x);
-                    q.y = __builtin_amdgcn_sqrtf(r2.y);
-                    ga.add2(2 * r + k, edge_shape2<KID>(q), E.s0, E.s1);
-                }
-            }
-        }
-    }
-}
+// Edge-continuous kernels (cubic / Wendland) on a square grid without a mixed cull take no
+// decision at all (gather_entry_masked below): W by edge_shape for every pixel of every
+// 8 x 16 half block row the entry's disc reaches.  A pixel the reference excludes has
+// exact r >= 2h, so its fp32 q is >= 2 (1 - 2^-21) and its term 0 or < 2^-60 W(0); one it
+// includes the same way.
 
 // One (uniform) entry, every other case: the box's own rows and columns (non-square grids
 // and mixed culls clip the box to the chunk ranges), the error band and the fp64
@@ -1061,19 +1057,53 @@ __device__ __forceinline__ void gather_entry(const Grid& g, const Src64& s, cons
     }
 }
 
+// One (uniform) entry of the edge path given its half-row mask bm (edge_mask).
+template <int KID, int NOUT, int ACC>
+__device__ __forceinline__ void gather_entry_masked(float u, float vs, float hinv, float s0,
+                                                    float s1, unsigned bm, const GCorner& c,
+                                                    GAcc<NOUT, ACC>& ga) {
+    const f2 hv = {-hinv, -hinv};
+    const f2 vv = {vs, vs};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        if (bm & (3u << (2 * r))) {
+            const float dxs = (u - c.X[r]) * hinv;
+            const f2 dx2 = {dxs * dxs, dxs * dxs};
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (bm & (1u << (2 * r + k))) {
+                    const f2 dys = __builtin_elementwise_fma(hv, (f2){c.Y[2 * k], c.Y[2 * k + 1]}, vv);
+                    const f2 r2 = __builtin_elementwise_fma(dys, dys, dx2);
+                    f2 q;
+                    q.x = __builtin_amdgcn_sqrtf(r2.x);
+                    q.y = __builtin_amdgcn_sqrtf(r2.y);
+                    ga.add2(2 * r + k, edge_shape2<KID>(q), s0, s1);
+                }
+            }
+        }
+    }
+}
+
 // The wave's walk over its lanes' entries: those whose box meets the wave's region.
 template <int KID, int NOUT, int ACC>
 __device__ __forceinline__ void gather_walk(const Grid& g, const Src64& s, const GEntry& mine,
                                             int X0, int Y0, const GOwn& o, const GCorner& c,
                                             GAcc<NOUT, ACC>& ga) {
-    unsigned long long m = __ballot(meets_region(mine.box, o));
     if (KID != kKernelIndicator && !g.nonsquare && !g.mixed) {  // uniform
+        // edge path: each lane finds the half rows its entry's disc reaches, and precomputes
+        // v / h; the walk then reads 6 words per entry and tests mask bits
+        const unsigned em = mine.box == kNoBox ? 0u : edge_mask(c, mine.u, mine.v, mine.hi);
+        const float vs = mine.v * mine.hinv;
+        unsigned long long m = __ballot(em != 0u);
         while (m) {
             const int l = __builtin_ctzll(m);
             m &= m - 1;
-            gather_entry_edge<KID, NOUT, ACC>(lane_entry(mine, l), o, c, ga);
+            gather_entry_masked<KID, NOUT, ACC>(bcast(mine.u, l), bcast(vs, l), bcast(mine.hinv, l),
+                                                bcast(mine.s0, l), bcast(mine.s1, l),
+                                                (unsigned)bcast((int)em, l), c, ga);
         }
     } else {
+        unsigned long long m = __ballot(meets_region(mine.box, o));
         while (m) {
             const int l = __builtin_ctzll(m);
             m &= m - 1;
@@ -1150,7 +1180,6 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
         return;
     }
     const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
-    const float tmin = (ACC == kAccFix && (flags & kFlagTail)) ? kTailUnits : 0.0f;
     tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
     const int lane = threadIdx.x & 63;
     int* dlist = defer_lds[threadIdx.x >> 6];
@@ -1160,7 +1189,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
         Prep P;
         P.b = Box{0, -1, 0, -1};
         bool live = i < it.count;
-        if (live) rec_prep<ACC>(r0, r1, X0, Y0, kk, P, tmin);
+        if (live) rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
         live = live && P.b.x0 <= P.b.x1;  // (an empty box deposits nothing)
         const int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
         const bool small = live && is_small(bw, bh);
@@ -1182,7 +1211,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
                 if (ndef >= 64) {  // a full wave of deferred records
                     ndef -= 64;
                     deferred<KID, NOUT, ACC>(g, s, recs, it.start, dlist, ndef, 64, X0, Y0, kk,
-                                             tmin, xt, yt, acc0, acc1, lane);
+                                             xt, yt, acc0, acc1, lane);
                 }
             }
         }
@@ -1214,8 +1243,8 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
         q1 = n1;
     }
     if (ndef > 0)
-        deferred<KID, NOUT, ACC>(g, s, recs, it.start, dlist, 0, ndef, X0, Y0, kk, tmin, xt, yt,
-                                 acc0, acc1, lane);
+        deferred<KID, NOUT, ACC>(g, s, recs, it.start, dlist, 0, ndef, X0, Y0, kk, xt, yt, acc0,
+                                 acc1, lane);
     __syncthreads();
     if (it.slab >= 0) {  // split tile: partial sums, merged by K5 (slab layout unpadded)
         unsigned long long* dst = slabs + (long long)it.slab * NOUT * kTilePix;
@@ -1264,7 +1293,6 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(
     const GOwn o = gather_owner(blockIdx.x % kGatherRegions);
     GAcc<NOUT, ACC> ga;
     ga.init(tot);
-    ga.tmin = (ACC == kAccFix && (flags & kFlagTail)) ? kTailUnits : 0.0f;
     const GCorner cc = gather_corners(g, o);
     for (int base = 0; base < it.count; base += 64) {
         GEntry mine;
@@ -1340,7 +1368,7 @@ __global__ __launch_bounds__(kGatherThreads) void k_wide(
     Grid g, Src64 s, const float* __restrict__ u, const float* __restrict__ v,
     const float* __restrict__ h, const float* __restrict__ a0, const float* __restrict__ a1,
     const int* __restrict__ wide_list, int n_wide, const int* __restrict__ ctr,
-    float* __restrict__ out0, float* __restrict__ out1, int flags) {
+    float* __restrict__ out0, float* __restrict__ out1) {
     extern __shared__ __attribute__((aligned(16))) double tot[];
     const int t = blockIdx.x / kGatherRegions;
     const int tx = t / g.nty, ty = t - (t / g.nty) * g.nty;
@@ -1353,7 +1381,6 @@ __global__ __launch_bounds__(kGatherThreads) void k_wide(
     const GOwn o = gather_owner(blockIdx.x % kGatherRegions);
     GAcc<NOUT, ACC> ga;
     ga.init(tot);
-    ga.tmin = (ACC == kAccFix && (flags & kFlagTail)) ? kTailUnits : 0.0f;
     const GCorner cc = gather_corners(g, o);
     bool any = false;  // wave-uniform
     for (int c = 0; c < n_wide; c += 64) {
@@ -1387,21 +1414,25 @@ __global__ __launch_bounds__(kGatherThreads) void k_wide(
 //      8 x 8 block (decided path) -- as gather_entry_edge / gather_entry spend them.
 // evals[0] += small / mid, evals[1] += gather (records), evals[2] += wide particles.
 // ----------------------------------------------------------------------------------
-__device__ __forceinline__ long long gather_slots(const Grid& g, int kid, unsigned box) {
+__device__ __forceinline__ long long gather_slots(const Grid& g, int kid, unsigned box, float u,
+                                                  float v, float hi) {
     const int x0 = box & 255u, x1 = (box >> 8) & 255u, y0 = (box >> 16) & 255u, y1 = box >> 24;
     const bool edge = kid != kKernelIndicator && !g.nonsquare && !g.mixed;
     long long c = 0;
     for (int w = 0; w < kGatherRegions; ++w) {
         const int r0 = (w >> 1) * 16, c0 = (w & 1) * 32;
+        if (edge) {  // the half rows edge_mask lets through (u, v: tile frame)
+            GOwn o;
+            o.r0 = r0;
+            o.c0 = c0;
+            o.lr = o.lc = 0;
+            c += 128LL * __builtin_popcount(edge_mask(gather_corners(g, o), u, v, hi));
+            continue;
+        }
         for (int r = 0; r < 2; ++r) {
             const int br = r0 + 8 * r;
             if (!(x0 <= br + 7 && x1 >= br)) continue;
-            if (edge) {
-                for (int k = 0; k < 2; ++k) {
-                    const int bc = c0 + 16 * k;
-                    if (y0 <= bc + 15 && y1 >= bc) c += 128;
-                }
-            } else {
+            {
                 for (int k = 0; k < 4; ++k) {
                     const int bc = c0 + 8 * k;
                     if (y0 <= bc + 7 && y1 >= bc) c += 64;
@@ -1433,7 +1464,9 @@ __global__ __launch_bounds__(kBlock) void k_evals(Grid g, int kid, Src64 s,
             const int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
             if (bw <= 0) continue;  // an empty box
             if (it.mode == 1) {
-                c1 += gather_slots(g, kid, __float_as_uint(r1.w));
+                c1 += gather_slots(g, kid, __float_as_uint(r1.w),
+                                   P.u + corner_off_x(g, P.b.x0 - X0),
+                                   P.v + corner_off_y(g, P.b.y0 - Y0), P.hi);
             } else if (bw <= 3 && bh <= 3) {
                 c0 += 9;
             } else if (is_small(bw, bh)) {
@@ -1455,7 +1488,8 @@ __global__ __launch_bounds__(kBlock) void k_evals(Grid g, int kid, Src64 s,
                 clip(P.b, X0, Y0, TW, TH)) {
                 const unsigned box = (unsigned)(P.b.x0 - X0) | ((unsigned)(P.b.x1 - X0) << 8) |
                                      ((unsigned)(P.b.y0 - Y0) << 16) | ((unsigned)(P.b.y1 - Y0) << 24);
-                c2 += gather_slots(g, kid, box);
+                c2 += gather_slots(g, kid, box, (float)(src_u(s, p, P.u) - corner_x(g, X0)),
+                                   (float)(src_v(s, p, P.v) - corner_y(g, Y0)), P.hi);
             }
         }
     }
@@ -1770,13 +1804,17 @@ static_assert(kMaxTiles <= kScanThreads * 4, "k_tilescan holds <= 4 tiles per th
 static inline int window_rows(const Grid& full) {  // tile rows per window
     return std::max(1, std::min(full.ntx, kMaxTiles / full.nty));
 }
-static inline Grid window_grid(const Grid& full, int tx0, int tx1) {
+// Image rows [r0, r1) as a window (any r0: its tile grid starts at row r0).
+static inline Grid window_grid_rows(const Grid& full, int r0, int r1) {
     Grid g = full;
-    g.ox = tx0 * kTile;
-    g.nx = std::min(tx1 * kTile, full.gnx) - g.ox;
-    g.ntx = tx1 - tx0;
+    g.ox = r0;
+    g.nx = r1 - r0;
+    g.ntx = (g.nx + kTile - 1) / kTile;
     g.ntiles = g.ntx * g.nty;
     return g;
+}
+static inline Grid window_grid(const Grid& full, int tx0, int tx1) {  // whole tile rows
+    return window_grid_rows(full, tx0 * kTile, std::min(tx1 * kTile, full.gnx));
 }
 
 struct Plan {
@@ -1860,8 +1898,7 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
     const bool fuse_ratio = ratio && pl.n_wide == 0;
     const unsigned long long* slabs = (const unsigned long long*)ws.slabs.p;
     const int dflags = ((flags & ASP_F_ACCUMULATE) ? kFlagAccumulate : 0) |
-                       (fuse_ratio ? kFlagRatio : 0) |
-                       (NOUT == 2 && (flags & (ASP_F_WEIGHTED | ASP_F_RATIO)) ? kFlagTail : 0);
+                       (fuse_ratio ? kFlagRatio : 0);
     if (!pre_scattered)
         ASP_TRY((launch_scatter<KID, NOUT, ACC>(g, s, ws, pl, u, v, h, a0, a1, 0x7fffffffLL,
                                                 0x7fffffff, st)));
@@ -1907,7 +1944,7 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
         hipLaunchKernelGGL((k_wide<KID, NOUT, ACC>), dim3(g.ntiles * kGatherRegions),
                            dim3(kGatherThreads), lds, st, g, s,
                            u, v, h, a0, a1, (const int*)ws.wide.p, pl.n_wide, (const int*)dc, o0,
-                           o1, dflags);
+                           o1);
         ASP_LAUNCHED();
         m.done();
     }
@@ -2141,20 +2178,19 @@ static Src64 src_from(const Src64& s, long long b) {  // particles b.. of s
 // The whole call: every window of the image (window_grid) and, inside it, particle
 // batches of < 2^31 particles, each batch split in two while its records reach 2^31.
 // Batches after the first accumulate; the ratio of a batched map is formed at the end.
-// rows [row0, ...) of the image only (row0 = tile_lo * 64; asp_project2d_rows): tile rows
-// [tile_lo, tile_hi), d0 / d1 pointing at row row0 of the image.
+// rows [row_lo, row_hi) of the image only (asp_project2d_rows; default the whole image),
+// d0 / d1 pointing at row row_lo: windows of <= window_rows tile rows from row_lo on.
 int project2d_full(Workspace& ws, const Grid& full, const Src64& s, const float* du,
                    const float* dv, const float* dh, const float* da0, const float* da1,
                    long long n, int kid, int flags, float* d0, float* d1, hipStream_t st,
-                   int tile_lo = 0, int tile_hi = -1) {
+                   int row_lo = 0, int row_hi = -1) {
     const int wr = window_rows(full);
     const long long B = max_batch();
     long long agg[kNStats] = {0};
-    if (tile_hi < 0) tile_hi = full.ntx;
-    if (flags & ASP_F_RATIO) flags |= ASP_F_WEIGHTED;  // kept when batches defer the ratio
-    for (int tx0 = tile_lo; tx0 < tile_hi; tx0 += wr) {
-        const Grid g = window_grid(full, tx0, std::min(tx0 + wr, tile_hi));
-        const long long off = (long long)(g.ox - tile_lo * kTile) * full.ny;
+    if (row_hi < 0) row_hi = full.gnx;
+    for (int r0 = row_lo; r0 < row_hi; r0 += wr * kTile) {
+        const Grid g = window_grid_rows(full, r0, std::min(r0 + wr * kTile, row_hi));
+        const long long off = (long long)(g.ox - row_lo) * full.ny;
         float* w0 = d0 + off;
         float* w1 = d1 ? d1 + off : nullptr;
         std::vector<std::pair<long long, long long>> todo;  // batches, last first
@@ -2196,7 +2232,7 @@ int project2d_full(Workspace& ws, const Grid& full, const Src64& s, const float*
         }
     }
     for (int k : {0, 1, 2, 6, 7, 8, 9, 10, 11, 12}) ws.stats[k] = agg[k];
-    ws.stats[4] = (tile_hi - tile_lo) * full.nty;
+    ws.stats[4] = (long long)((row_hi - row_lo + kTile - 1) / kTile) * full.nty;
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess && &ws != &g_ws[dev])  // asp_last_stats reads slot 0
         std::copy(ws.stats, ws.stats + kNStats, g_ws[dev].stats);
@@ -2259,10 +2295,8 @@ static int project2d(const float* u, const float* v, const float* h, const float
     Grid g;
     ASP_TRY(setup_grid(x_min, x_max, y_min, y_max, nx, ny, cs, g));
     if (row_hi < 0) row_hi = nx;
-    if (row_lo < 0 || row_lo >= row_hi || row_hi > nx || row_lo % kTile != 0 ||
-        (row_hi % kTile != 0 && row_hi != nx))
-        return fail(ASP_ERR_INVALID, "rows: need 0 <= row_lo < row_hi <= nx, row_lo a multiple "
-                                     "of 64, row_hi a multiple of 64 or nx");
+    if (row_lo < 0 || row_lo >= row_hi || row_hi > nx)
+        return fail(ASP_ERR_INVALID, "rows: need 0 <= row_lo < row_hi <= nx");
     nx = row_hi - row_lo;  // the rows this call writes (the grid keeps the whole image's)
     ASP_TRY(set_device(device));
     Workspace& ws = slot_ws(device, map_slot(device, (hipStream_t)stream));
@@ -2289,8 +2323,8 @@ static int project2d(const float* u, const float* v, const float* h, const float
         ASP_TRY(host_outputs(ws, out0, out1, npix, flags, st, d0, d1));
     }
     const Src64 s{nullptr, nullptr, nullptr, nullptr, nullptr, 0, du, dv, dh};
-    ASP_TRY(project2d_full(ws, g, s, du, dv, dh, da0, da1, n, kid, flags, d0, d1, st,
-                           row_lo / kTile, (row_hi + kTile - 1) / kTile));
+    ASP_TRY(project2d_full(ws, g, s, du, dv, dh, da0, da1, n, kid, flags, d0, d1, st, row_lo,
+                           row_hi));
     if (!dev) ASP_TRY(host_results(out0, out1, d0, d1, npix, st));
     return ws_end_.finish();
 }

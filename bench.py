@@ -53,6 +53,11 @@ def parse():
     ap.add_argument("--map", default="weighted", choices=["weighted", "surface"])
     ap.add_argument("--op", default="reduce",
                     choices=["reduce", "allreduce", "reduce_scatter", "reduce_scatter_gather"])
+    ap.add_argument("--decomp", default="zslab", choices=["zslab", "rows"],
+                    help="N > 1: zslab = each rank's Z-slab onto the full grid + one grid "
+                         "collective (--op); rows = each rank owns image rows (particles "
+                         "routed by footprint, untimed), projects only them, one all-gather "
+                         "of the ratio map (no reduction)")
     ap.add_argument("--slab-weight", default="cost", choices=["cost", "count"],
                     help="N > 1 Z-slab edges: equal modelled work (distributed.slab_cost) or "
                          "equal particle counts")
@@ -69,10 +74,13 @@ def parse():
                          "device fp32 SoA staging (SURVEY 8(f)); the last two are not the "
                          "driver's line")
     ap.add_argument("--cube", type=int, default=512, help="cube edge (voxels), --workload cube")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=0,
                     help="HIP streams consecutive maps alternate between (each its own "
-                         "workspace slot in the library): map i + 1's binning overlaps map "
-                         "i's deposit; 1 = one stream, maps strictly in sequence")
+                         "workspace slot in the library), so map i + 1's launches overlap "
+                         "map i's tail; 1 = one stream, maps strictly in sequence; 0 (auto) "
+                         "= 2 for a rank's share of <= 3e7 particles (the N >= 4 shards: "
+                         "0.561 -> 0.518 ms at 1.25e7), else 1 (10^8: 3.28 vs 3.43 ms, the "
+                         "kernels already fill the GPU; DESIGN.md §9)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="N > 1: wait for each map's collective before the next map")
     ap.add_argument("--no-stage-events", dest="stage_events", action="store_false",
@@ -597,12 +605,24 @@ def main():
     ext = (-extent, extent, -extent, extent)
     t0 = time.time()
     d = plummer_torch(args.n, seed=0, h_law=args.h_law, extent=extent, grid=G, device=dev)
+    R = None  # --decomp rows: the row-slab bounds
     if world > 1:
-        from asp_amd.distributed import slab_cost
+        from asp_amd.distributed import route_rows, row_slabs, slab_cost
         w = None if args.slab_weight == "count" else slab_cost(d["x"], d["y"], d["h"], ext, 2 * extent / G)
-        e = zslab_bounds(d["z"], world, weights=w)
+        if args.decomp == "rows":
+            # image-plane ownership: this rank's rows, the particles whose footprints reach
+            # them (the partition is untimed, as the Z-slab split is)
+            Rt = torch.tensor(row_slabs(G, world, d["x"], ext[:2], weights=w), dtype=torch.int64,
+                              device=dev)
+            dist.broadcast(Rt, src=0)
+            R = Rt.tolist()
+            r0, r1 = route_rows(d["x"], d["h"], ext[:2], G, R)
+            keep = (r0 <= rank) & (r1 >= rank)
+            del r0, r1
+        else:
+            e = zslab_bounds(d["z"], world, weights=w)
+            keep = (d["z"] >= e[rank]) & (d["z"] < e[rank + 1])
         del w
-        keep = (d["z"] >= e[rank]) & (d["z"] < e[rank + 1])
         d = {k: v[keep].contiguous() for k, v in d.items()}
     u, v, h = d["x"], d["y"], d["h"]
     if args.map == "weighted":
@@ -623,7 +643,7 @@ def main():
     # Consecutive maps alternate between --streams HIP streams (each with its own output
     # buffer; the library gives each stream its own workspace slot): the binning of map
     # i + 1 runs beside the deposit of map i.  --streams 1: one stream.
-    ns = max(1, args.streams)
+    ns = args.streams if args.streams > 0 else (2 if n_local <= 30_000_000 else 1)
     streams = ([torch.cuda.current_stream(dev)] if ns == 1 else
                [torch.cuda.Stream(device=dev) for _ in range(ns)])
     nbuf = max(ns, 2 if (world > 1 and args.pipeline) else 1)
@@ -633,13 +653,43 @@ def main():
     it = [0]
     last = [None]  # the last completed map's (out0, out1) as the collective returns them
 
+    if R is not None:  # row slabs: this rank's rows (padded to the widest slab) + the map
+        rmax = max(R[i + 1] - R[i] for i in range(world))
+        my_rows = R[rank + 1] - R[rank]
+        sends = [torch.zeros((rmax, G), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+        fulls = [torch.empty((world * rmax, G), dtype=torch.float32, device=dev)
+                 for _ in range(nbuf)]
+
+    class _Gathered:  # the all-gather of one map's row slabs, waited for stream-ordered
+        def __init__(self, work, full, comp):
+            self.work, self.full, self.comp = work, full, comp
+
+        def wait(self):
+            if self.work is not None:
+                self.work.wait()
+                self.work = None
+            return self.full, self.comp
+
     def step(pipelined=world > 1 and args.pipeline):
         k = it[0]
         it[0] += 1
         maps = bufs[k % nbuf]
         o0, o1 = maps[0], (maps[1] if a1 is not None else None)
         with torch.cuda.stream(streams[k % ns]):
-            if world > 1:
+            if R is not None:
+                # this rank's rows (ratio formed locally: its rows' sums are complete), then
+                # ONE all-gather of the single map -- no grid reduction
+                s0 = sends[k % nbuf][:my_rows]
+                s1 = o1[:my_rows] if o1 is not None else None
+                project2d(u, v, h, a0, a1, image_size=(G, G), extent=ext, kernel=args.kernel,
+                          ratio=ratio, out0=s0, out1=s1, deterministic=args.deterministic,
+                          rows=(R[rank], R[rank + 1]))
+                work = dist.all_gather_into_tensor(fulls[k % nbuf], sends[k % nbuf],
+                                                   async_op=True)
+                p = _Gathered(work, fulls[k % nbuf], s1)
+                if not pipelined:
+                    last[0] = p.wait()
+            elif world > 1:
                 p = project2d_sharded(u, v, h, a0, a1, image_size=(G, G), extent=ext,
                                       kernel=args.kernel, ratio=ratio, op=args.op, out0=o0,
                                       out1=o1, deterministic=args.deterministic,
@@ -648,7 +698,7 @@ def main():
                 last[0] = project2d(u, v, h, a0, a1, image_size=(G, G), extent=ext,
                                     kernel=args.kernel, ratio=ratio, out0=o0, out1=o1,
                                     deterministic=args.deterministic)
-        if world > 1:
+        if world > 1 and not (R is not None and not pipelined):
             if pipelined:
                 if pending[0] is not None:
                     # map k - 1's collective: the stream that next writes its buffer (map
@@ -720,8 +770,12 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     # reduce_scatter: out0 / out1 are this rank's reduced row slab (ratio formed there)
+    if R is not None:  # the gathered row slabs (padded) -> the full map on every rank
+        out0 = torch.cat([out0[r * rmax:r * rmax + R[r + 1] - R[r]] for r in range(world)])
+        out1 = None
     ok = output_check(out0, out1, a0, a1, ratio, world,
-                      gathered_ratio=world > 1 and args.op == "reduce_scatter_gather")
+                      gathered_ratio=world > 1 and (args.op == "reduce_scatter_gather"
+                                                    or R is not None))
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -770,18 +824,28 @@ def main():
         "config": {"workload": f"{cfg_tag}: {args.n:.0e} particles -> {G}^2 "
                                f"{'mass-weighted temperature' if ratio else 'surface density'} "
                                f"map, {args.kernel}, {args.h_law}-scale h, fp32"
-                               + (f", Z-slab x{world} + {backend_label} {args.op}"
+                               + ((f", Z-slab x{world} + {backend_label} {args.op}"
+                                   if R is None else
+                                   f", image row slabs x{world} + {backend_label} all-gather")
                                   if world > 1 else ""),
                    "particles": args.n, "grid": G, "kernel": args.kernel, "h_law": args.h_law,
-                   "map": args.map, "parallelism": f"zslab{world}" if world > 1 else "single",
-                   **({"backend": backend_label} if world > 1 else {}),
+                   "map": args.map,
+                   "parallelism": (f"zslab{world}" if R is None else f"rows{world}")
+                   if world > 1 else "single",
+                   **({"backend": backend_label, "decomp": args.decomp,
+                       **({"row_bounds": R} if R is not None else {})} if world > 1 else {}),
                    "accumulation": "int64 fixed point" if args.deterministic else "fp64",
                    "collective_overlap": world > 1 and args.pipeline,
                    "streams": ns,
                    **({"slab_weight": args.slab_weight, "collective": args.op,
-                       "partition": "Z-slab split of the generated particles before the "
-                                    "timed region (untimed, as a reader-split snapshot "
-                                    "needs none)"} if world > 1 else {})},
+                       "partition": ("Z-slab split of the generated particles before the "
+                                     "timed region (untimed, as a reader-split snapshot "
+                                     "needs none)" if R is None else
+                                     "each rank keeps the generated particles whose 2h "
+                                     "footprint reaches its rows, before the timed region "
+                                     "(untimed; from a reader's arbitrary split this is "
+                                     "one all-to-all per snapshot, "
+                                     "distributed.exchange_rows)")} if world > 1 else {})},
         "particles_per_s": pps,
         **({"latency_ms_per_map": round(latency_ms, 4),
             "latency_note": "one map at a time, synchronised (no overlap of maps): binning + "

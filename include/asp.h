@@ -53,15 +53,6 @@ extern "C" {
                                    * inputs go through pinned bounce buffers (two 32 MiB
                                    * pieces, CPU copy overlapping the DMA)                 */
 
-#define ASP_F_WEIGHTED 0x20 /* a1 is a weight and a0 = a1 * value (mass-weighted maps;
-                             * implied by ASP_F_RATIO).  With ASP_F_DETERMINISTIC the two
-                             * maps are quantised consistently: a pair whose weight term
-                             * a1 W is below 2^18 units of its tile's fixed-point scale
-                             * (2^-31 n_t max|a1 W|) is left out of BOTH maps, so every
-                             * pixel's out0 / out1 stays a weighted mean of the values to
-                             * 2^-18 of the tile's largest.  No effect on
-                             * the default fp64 accumulation.                          */
-
 /* asp_project2d_f64 axis: cull on axis c's columns (the reference's mixed spellings) */
 #define ASP_AXIS_CULL(c) (((c) + 1) << 4)
 
@@ -110,8 +101,8 @@ int asp_project2d(const float *u, const float *v, const float *h, const float *a
  * (_projector.py:89-111) distributed: out0 / out1 hold (row_hi - row_lo) x ny pixels,
  * element [(xi - row_lo) * ny + yi], each equal to the pixel asp_project2d writes for the
  * whole image (same corners, pitches, chunk cull and decisions; particles whose footprint
- * misses the rows are skipped).  row_lo must be a multiple of 64, row_hi a multiple of 64
- * or nx.  Other arguments as asp_project2d.
+ * misses the rows are skipped).  Any 0 <= row_lo < row_hi <= nx (the GPU tiles of the
+ * call start at row_lo).  Other arguments as asp_project2d.
  */
 int asp_project2d_rows(const float *u, const float *v, const float *h, const float *a0,
                        const float *a1, int64_t n, double u_min, double u_max, double v_min,

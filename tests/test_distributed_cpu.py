@@ -329,7 +329,7 @@ def test_cube_plane_slabs_halo_exchange_world2():
 
 
 # ------------------------------------------- 2-D row slabs (image-plane decomposition)
-GR = 192  # three tile rows of 64: unequal slabs for world 2
+GR = 160  # rows split where the particle counts balance
 
 
 def _oracle_rows(u, v, h, a0, a1, *, image_size, extent, chunk_size, kernel, ratio, out0,
@@ -404,7 +404,7 @@ def test_rowslab_world2():
     full0, full1 = pyoracle.project_scatter(x.numpy(), y.numpy(), h.numpy(), (m * T).numpy(),
                                             m.numpy(), (GR, GR), 16, *EXT, kernel="cubic")
     R = out[0]["bounds"]
-    assert R == out[1]["bounds"] and R[0] == 0 and R[-1] == GR and R[1] % 64 == 0
+    assert R == out[1]["bounds"] and R[0] == 0 and R[-1] == GR and 0 < R[1] < GR
     t0, t1 = 1e-5 * np.abs(full0).max(), 1e-5 * np.abs(full1).max()
     cov = full1 > 1e-3 * full1.max()
     want_ratio = np.where(full1 != 0, full0 / np.where(full1 != 0, full1, 1), 0.0)

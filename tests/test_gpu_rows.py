@@ -22,6 +22,7 @@ def _data(n, seed, h_law, grid):
     (1024, 1024, [0, 192, 448, 1024], "physical"),
     (1000, 1024, [0, 64, 512, 960, 1000], "pixel"),
     (768, 640, [0, 384, 768], "physical"),
+    (1000, 1024, [0, 100, 333, 334, 999, 1000], "physical"),  # any rows: tiles start at row_lo
 ])
 def test_rows_equal_full_map(gpu, nx, ny, bounds, h_law, monkeypatch):
     import torch
@@ -70,6 +71,6 @@ def test_rows_argument_errors(gpu):
     import torch
     from asp_amd.device import project2d
     u, v, h, a0, a1 = _data(1000, 1, "pixel", 256)
-    for rows in ((32, 256), (0, 100), (128, 64), (0, 300), (-64, 64)):
+    for rows in ((128, 64), (0, 300), (-64, 64), (5, 5)):
         with pytest.raises(ValueError):
             project2d(u, v, h, a0, image_size=(256, 256), extent=(-4, 4, -4, 4), rows=rows)

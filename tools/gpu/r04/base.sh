@@ -39,6 +39,11 @@ step decomposition probe
 timeout -k 10 300 python tools/decomp_probe.py --interference --out $o/decomp.json > $o/decomp.log 2>&1 || { tail -5 $o/decomp.log; exit 1; }
 tail -8 $o/decomp.log
 fi
+step rehearsal N=2 gloo on one GPU
+for dc in zslab rows; do
+ASP_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --decomp $dc > $o/rehearsal_n2_$dc.json 2> $o/rehearsal_n2_$dc.err; echo "rc=$?"; tail -3 $o/rehearsal_n2_$dc.err | cut -c1-300
+cut -c1-600 $o/rehearsal_n2_$dc.json
+done
 step overlap probe
 timeout -k 10 300 python tools/overlap_probe.py --out $o/overlap.json > $o/overlap.log 2>&1; echo "rc=$?"; tail -6 $o/overlap.log
 step done
