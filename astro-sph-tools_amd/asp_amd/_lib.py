@@ -86,10 +86,11 @@ def lib():
     L.asp_project2d.argtypes = [_f, _f, _f, _f, _f, C.c_int64, C.c_double, C.c_double,
                                 C.c_double, C.c_double, C.c_int32, C.c_int32, C.c_int32,
                                 C.c_int32, C.c_int32, _f, _f, C.c_int32, C.c_void_p]
-    L.asp_project2d_rows.argtypes = [_f, _f, _f, _f, _f, C.c_int64, C.c_double, C.c_double,
-                                     C.c_double, C.c_double, C.c_int32, C.c_int32, C.c_int32,
-                                     C.c_int32, C.c_int32, C.c_int32, C.c_int32, _f, _f,
-                                     C.c_int32, C.c_void_p]
+    if hasattr(L, "asp_project2d_rows"):  # (absent from an older A/B build, ASP_LIB)
+      L.asp_project2d_rows.argtypes = [_f, _f, _f, _f, _f, C.c_int64, C.c_double, C.c_double,
+                                       C.c_double, C.c_double, C.c_int32, C.c_int32,
+                                       C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                       _f, _f, C.c_int32, C.c_void_p]
     L.asp_project2d_f64.argtypes = [_d, _d, _d, _d, C.c_int64, C.c_int32, C.c_double,
                                     C.c_double, C.c_double, C.c_double, C.c_int32, C.c_int32,
                                     C.c_int32, C.c_int32, C.c_int32, _f, _f, C.c_int32,

@@ -422,7 +422,7 @@ def exchange_rows(cols, u, h, *, u_extent, nx: int, bounds, group=None):
 def project2d_rowslab(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
                       kernel="cubic", ratio: bool = False, bounds=None, group=None,
                       gather: str = "none", exchange: bool = True, out0=None, out1=None,
-                      projector=None, deterministic: bool = False):
+                      projector=None, deterministic: bool = False, dst: int = 0):
     """The map on W ranks by image rows: rank r owns rows [R[r], R[r+1]) of ``bounds``
     (default :func:`row_slabs` balanced on the particles' u).  With ``exchange`` every
     rank passes ITS particles (any split) and one all-to-all routes them to the owners of
@@ -431,13 +431,15 @@ def project2d_rowslab(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
     (asp_project2d_rows) with the ratio formed locally -- its rows' sums are complete, so
     no grid collective runs.  ``gather="none"`` returns this rank's (rows, ny) slab(s);
     ``"all"`` all-gathers map 0 (the ratio map with ``ratio``) into the full (nx, ny) map
-    on every rank and returns ``(full, None)``.  ``projector`` replaces the local
-    projection (CPU tests); default the HIP path."""
+    on every rank and returns ``(full, None)``; ``"dst"`` sends every slab of map 0 to
+    rank ``dst`` (point-to-point, exact slab sizes -- the analogue of the Z-slab path's
+    reduce) and returns ``(full, None)`` there, ``(own slab, None)`` elsewhere.
+    ``projector`` replaces the local projection (CPU tests); default the HIP path."""
     import torch
     import torch.distributed as dist
     if ratio and a1 is None:
         raise ValueError("ratio needs a1")
-    if gather not in ("none", "all"):
+    if gather not in ("none", "all", "dst"):
         raise ValueError(f"unknown gather {gather!r}")
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -464,6 +466,17 @@ def project2d_rowslab(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
                   kernel=kernel, ratio=ratio, out0=out0, out1=out1, rows=(r0, r1), **kw)
     if gather == "none" or world == 1:
         return o0, o1
+    if gather == "dst":
+        if rank != dst:
+            dist.batch_isend_irecv([dist.P2POp(dist.isend, o0.contiguous(), dst, group)])[0].wait()
+            return o0, None
+        full = torch.empty((nx, ny), dtype=o0.dtype, device=o0.device)
+        full[r0:r1] = o0
+        ops = [dist.P2POp(dist.irecv, full[bounds[r]:bounds[r + 1]], r, group)
+               for r in range(world) if r != dst]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        return full, None
     rmax = max(bounds[r + 1] - bounds[r] for r in range(world))
     pad = torch.zeros((rmax, ny), dtype=o0.dtype, device=o0.device)
     pad[:r1 - r0] = o0

@@ -53,11 +53,17 @@ def parse():
     ap.add_argument("--map", default="weighted", choices=["weighted", "surface"])
     ap.add_argument("--op", default="reduce",
                     choices=["reduce", "allreduce", "reduce_scatter", "reduce_scatter_gather"])
-    ap.add_argument("--decomp", default="zslab", choices=["zslab", "rows"],
-                    help="N > 1: zslab = each rank's Z-slab onto the full grid + one grid "
-                         "collective (--op); rows = each rank owns image rows (particles "
-                         "routed by footprint, untimed), projects only them, one all-gather "
-                         "of the ratio map (no reduction)")
+    ap.add_argument("--decomp", default="rows", choices=["zslab", "rows"],
+                    help="N > 1: rows (default) = each rank owns image rows (particles "
+                         "routed by footprint before the timed region), projects only them "
+                         "with the ratio formed locally, and the ratio map's slabs go to "
+                         "rank 0 (--rows-gather) -- no grid reduction; zslab = each rank's "
+                         "Z-slab onto the full grid + one grid collective (--op).  One GPU, "
+                         "8 shares of the 10^8 map: rows max 0.50 ms vs zslab 0.59 ms + a "
+                         "2 x 64 MiB reduce (DESIGN.md §8)")
+    ap.add_argument("--rows-gather", default="dst", choices=["dst", "all"],
+                    help="--decomp rows: the ratio map's row slabs to rank 0 (point-to-point "
+                         "sends of the exact slabs) or all-gathered on every rank")
     ap.add_argument("--slab-weight", default="cost", choices=["cost", "count"],
                     help="N > 1 Z-slab edges: equal modelled work (distributed.slab_cost) or "
                          "equal particle counts")
@@ -548,6 +554,14 @@ def output_check(out0, out1, a0, a1, ratio, world=1, gathered_ratio=False):
     weighted MEAN of particle temperatures -- inside [min T, max T] wherever sum m W > 0,
     exactly 0 elsewhere."""
     import torch
+    lo = hi = None
+    if ratio:  # the collective first: every rank reaches it whatever its own checks say
+        t = a0 / a1
+        rng = torch.stack([-t.min(), t.max()]).double()
+        if world > 1:  # the reduced map averages every rank's particles
+            import torch.distributed as dist
+            dist.all_reduce(rng, op=dist.ReduceOp.MAX)
+        lo, hi = -float(rng[0].item()), float(rng[1].item())
     if not bool(torch.isfinite(out0).all().item()):
         return False
     if not ratio:
@@ -556,12 +570,6 @@ def output_check(out0, out1, a0, a1, ratio, world=1, gathered_ratio=False):
         out1 = out0     # this rank's own (unreduced) component: coverage from out0 itself
     if not bool(torch.isfinite(out1).all().item()) or not bool((out1 >= 0).all().item()):
         return False
-    t = a0 / a1
-    rng = torch.stack([-t.min(), t.max()]).double()
-    if world > 1:  # the reduced map averages every rank's particles
-        import torch.distributed as dist
-        dist.all_reduce(rng, op=dist.ReduceOp.MAX)
-    lo, hi = -float(rng[0].item()), float(rng[1].item())
     cov = out1 > 0
     inside = (out0[cov] >= lo * (1 - 1e-5)) & (out0[cov] <= hi * (1 + 1e-5))
     return (bool(cov.any().item()) and bool(inside.all().item())
@@ -653,22 +661,36 @@ def main():
     it = [0]
     last = [None]  # the last completed map's (out0, out1) as the collective returns them
 
-    if R is not None:  # row slabs: this rank's rows (padded to the widest slab) + the map
+    if R is not None:  # row slabs: this rank's rows, then the ratio map gathered
         rmax = max(R[i + 1] - R[i] for i in range(world))
         my_rows = R[rank + 1] - R[rank]
-        sends = [torch.zeros((rmax, G), dtype=torch.float32, device=dev) for _ in range(nbuf)]
-        fulls = [torch.empty((world * rmax, G), dtype=torch.float32, device=dev)
-                 for _ in range(nbuf)]
+        if args.rows_gather == "all":  # all-gather (equal sizes: slabs padded to rmax)
+            sends = [torch.zeros((rmax, G), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+            fulls = [torch.empty((world * rmax, G), dtype=torch.float32, device=dev)
+                     for _ in range(nbuf)]
+        else:  # to rank 0 over point-to-point sends of the exact slabs (the reduce's analogue)
+            fulls = [torch.empty((G, G), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+            sends = [f[R[rank]:R[rank + 1]] for f in fulls]
 
-    class _Gathered:  # the all-gather of one map's row slabs, waited for stream-ordered
-        def __init__(self, work, full, comp):
-            self.work, self.full, self.comp = work, full, comp
+    class _Gathered:  # the gather of one map's row slabs, waited for stream-ordered
+        def __init__(self, works, full, comp):
+            self.works, self.full, self.comp = works, full, comp
 
         def wait(self):
-            if self.work is not None:
-                self.work.wait()
-                self.work = None
+            for w in self.works:
+                w.wait()
+            self.works = []
             return self.full, self.comp
+
+    def gather_rows(b):
+        """Post the gather of buffer b's ratio map: all-gather, or p2p slabs to rank 0."""
+        if args.rows_gather == "all":
+            return [dist.all_gather_into_tensor(fulls[b], sends[b], async_op=True)]
+        if rank != 0:
+            ops = [dist.P2POp(dist.isend, sends[b], 0)]
+        else:
+            ops = [dist.P2POp(dist.irecv, fulls[b][R[r]:R[r + 1]], r) for r in range(1, world)]
+        return dist.batch_isend_irecv(ops)
 
     def step(pipelined=world > 1 and args.pipeline):
         k = it[0]
@@ -684,9 +706,7 @@ def main():
                 project2d(u, v, h, a0, a1, image_size=(G, G), extent=ext, kernel=args.kernel,
                           ratio=ratio, out0=s0, out1=s1, deterministic=args.deterministic,
                           rows=(R[rank], R[rank + 1]))
-                work = dist.all_gather_into_tensor(fulls[k % nbuf], sends[k % nbuf],
-                                                   async_op=True)
-                p = _Gathered(work, fulls[k % nbuf], s1)
+                p = _Gathered(gather_rows(k % nbuf), fulls[k % nbuf], s1)
                 if not pipelined:
                     last[0] = p.wait()
             elif world > 1:
@@ -770,8 +790,11 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     # reduce_scatter: out0 / out1 are this rank's reduced row slab (ratio formed there)
-    if R is not None:  # the gathered row slabs (padded) -> the full map on every rank
-        out0 = torch.cat([out0[r * rmax:r * rmax + R[r + 1] - R[r]] for r in range(world)])
+    if R is not None:  # the gathered row slabs -> the full map (rank 0; every rank: "all")
+        if args.rows_gather == "all":
+            out0 = torch.cat([out0[r * rmax:r * rmax + R[r + 1] - R[r]] for r in range(world)])
+        elif rank != 0:
+            out0 = out0[R[rank]:R[rank + 1]]  # (the rest of its buffer was never written)
         out1 = None
     ok = output_check(out0, out1, a0, a1, ratio, world,
                       gathered_ratio=world > 1 and (args.op == "reduce_scatter_gather"

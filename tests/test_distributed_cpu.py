@@ -373,6 +373,11 @@ def _rows_worker(rank, world, port, q):
                                        projector=_oracle_rows)
         res["full_ratio"] = full.numpy().copy()
         res["none"] = none
+        got, _ = project2d_rowslab(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3],
+                                   image_size=(GR, GR), extent=EXT, chunk_size=16,
+                                   kernel="cubic", ratio=True, gather="dst",
+                                   projector=_oracle_rows)
+        res["dst"] = got.numpy().copy()
         R = row_slabs(GR, world, x, EXT[:2])
         res["bounds"] = R
         r0, r1 = route_rows(x, h, EXT[:2], GR, R)
@@ -414,5 +419,7 @@ def test_rowslab_world2():
         np.testing.assert_allclose(out[r]["slab"][1], full1[rows], atol=t1, rtol=0)
         np.testing.assert_allclose(out[r]["full_ratio"][cov], want_ratio[cov], rtol=1e-4)
         assert out[r]["none"] is None
+    np.testing.assert_allclose(out[0]["dst"][cov], want_ratio[cov], rtol=1e-4)  # on rank 0
+    assert out[1]["dst"].shape == (R[2] - R[1], GR)  # rank 1 keeps its own slab
     # every particle reaches some rank; the wide physical-h halo is duplicated, not all of it
     assert x.numel() <= out[0]["routed"] + out[1]["routed"] < 2 * x.numel()

@@ -41,7 +41,14 @@ def test_rows_equal_full_map(gpu, nx, ny, bounds, h_law, monkeypatch):
         r0, r1 = bounds[r], bounds[r + 1]
         s0, s1 = project2d(u, v, h, a0, a1, deterministic=True, rows=(r0, r1), **kw)
         assert s0.shape == (r1 - r0, ny)
-        assert torch.equal(s0, f0[r0:r1]) and torch.equal(s1, f1[r0:r1])
+        # a window's tiles start at row_lo: tile-aligned windows have the full map's tiles
+        # (same records, same fixed-point scale: bit-identical), others are within rounding
+        aligned = r0 % 64 == 0 and (r1 % 64 == 0 or r1 == nx)
+        if aligned:
+            assert torch.equal(s0, f0[r0:r1]) and torch.equal(s1, f1[r0:r1])
+        else:
+            torch.testing.assert_close(s0, f0[r0:r1], rtol=1e-5, atol=1e-6 * float(f0.abs().max()))
+            torch.testing.assert_close(s1, f1[r0:r1], rtol=1e-5, atol=1e-6 * float(f1.abs().max()))
         sc, _ = project2d(u, v, h, torch.ones_like(h), image_size=(nx, ny), extent=ext,
                           kernel="indicator", rows=(r0, r1))
         assert torch.equal(sc, cnt[r0:r1])
@@ -63,7 +70,10 @@ def test_rows_equal_full_map(gpu, nx, ny, bounds, h_law, monkeypatch):
         k0, k1 = project2d(u[keep].contiguous(), v[keep].contiguous(), h[keep].contiguous(),
                            a0[keep].contiguous(), a1[keep].contiguous(), deterministic=True,
                            rows=(r0, r1), **kw)
-        assert torch.equal(k0, f0[r0:r1]) and torch.equal(k1, f1[r0:r1])
+        if aligned:
+            assert torch.equal(k0, f0[r0:r1]) and torch.equal(k1, f1[r0:r1])
+        else:
+            assert torch.equal(k0, s0) and torch.equal(k1, s1)  # the same window's records
     torch.cuda.synchronize()
 
 
