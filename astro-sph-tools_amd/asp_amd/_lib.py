@@ -38,7 +38,8 @@ ASP_ERR_UNSUPPORTED = -4
 
 # Every symbol include/asp.h declares (tests check the library exports all of them).
 EXPORTS = ("asp_version", "asp_last_error", "asp_device_count", "asp_project2d",
-           "asp_project2d_rows", "asp_project2d_f64", "asp_pairs_begin", "asp_pairs_emit", "asp_pairs_end",
+           "asp_project2d_rows", "asp_project2d_props", "asp_project2d_props_f64",
+           "asp_project2d_f64", "asp_pairs_begin", "asp_pairs_emit", "asp_pairs_end",
            "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges", "asp_pixel_neighbours", "asp_ratio",
            "asp_profile", "asp_profile_stages", "asp_profile_read", "asp_last_stats",
            "asp_release", "asp_stage_particles", "asp_periodic", "asp_wrapped_distance",
@@ -91,6 +92,16 @@ def lib():
                                        C.c_double, C.c_double, C.c_int32, C.c_int32,
                                        C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                        _f, _f, C.c_int32, C.c_void_p]
+    if hasattr(L, "asp_project2d_props"):  # (absent from an older A/B build, ASP_LIB)
+        L.asp_project2d_props.argtypes = [_f, _f, _f, C.POINTER(_f), C.c_int32, C.c_int64,
+                                          C.c_double, C.c_double, C.c_double, C.c_double,
+                                          C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                          C.POINTER(_f), C.c_int32, C.c_void_p]
+        L.asp_project2d_props_f64.argtypes = [_d, _d, C.POINTER(_d), C.c_int32, C.c_int64,
+                                              C.c_int32, C.c_double, C.c_double, C.c_double,
+                                              C.c_double, C.c_int32, C.c_int32, C.c_int32,
+                                              C.c_int32, C.c_int32, C.POINTER(_f), C.c_int32,
+                                              C.c_void_p]
     L.asp_project2d_f64.argtypes = [_d, _d, _d, _d, C.c_int64, C.c_int32, C.c_double,
                                     C.c_double, C.c_double, C.c_double, C.c_int32, C.c_int32,
                                     C.c_int32, C.c_int32, C.c_int32, _f, _f, C.c_int32,

@@ -86,6 +86,89 @@ def project2d(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
     return out0, (out1 if a1 is not None else None)
 
 
+def project2d_props(u, v, h, props, *, image_size, extent, chunk_size: int = 64,
+                    kernel="cubic", accumulate: bool = False, outs=None, stream=None):
+    """asp_project2d_props: one map per property of ``props`` (1..6 device float32 arrays)
+    from ONE binning of the particles -- the same neighbour sets, the counting and
+    scattering done once.  Returns the list of (nx, ny) float32 maps."""
+    import torch
+    dev = u.device
+    n = u.shape[0]
+    k = len(props)
+    if not 1 <= k <= 6:
+        raise ValueError("props: 1 .. 6 arrays")
+    for t, name in ((u, "u"), (v, "v"), (h, "h")):
+        _check(t, name, n, dev)
+    for j, a in enumerate(props):
+        _check(a, f"props[{j}]", n, dev)
+    nx, ny = int(image_size[0]), int(image_size[1])
+    if outs is None:
+        outs = [torch.empty((nx, ny), dtype=torch.float32, device=dev) for _ in range(k)]
+    if len(outs) != k:
+        raise ValueError("one output per property")
+    for t in outs:
+        if t.dtype != torch.float32 or t.device != dev or not t.is_contiguous() or \
+                t.numel() != nx * ny:
+            raise ValueError("outputs must be contiguous float32 (nx, ny) tensors on the device")
+    flags = _lib.ASP_F_DEVICE_PTRS | (_lib.ASP_F_ACCUMULATE if accumulate else 0)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    P = _lib.ptr
+    pa = (_lib._f * k)(*[P(a) for a in props])
+    po = (_lib._f * k)(*[P(o) for o in outs])
+    x_min, x_max, y_min, y_max = (float(e) for e in extent)
+    _lib.check(_lib.lib().asp_project2d_props(
+        P(u), P(v), P(h), pa, k, n, x_min, x_max, y_min, y_max, nx, ny, int(chunk_size),
+        kernel_id(kernel), flags, po, dev.index or 0, stream))
+    return outs
+
+
+def project2d_props_f64(positions, h, props, *, projection_axis=2, image_size, extent,
+                        chunk_size: int = 64, kernel="cubic", device: int = 0):
+    """asp_project2d_props_f64 on the reader's float64 arrays (host NumPy arrays or float64
+    device tensors; host arrays are copied to the device): the maps of every property from
+    one binning, every decision the reference's fp64 test.  Returns float32 device maps."""
+    import numpy as np
+    import torch
+    from ._axes import axis_index
+    if isinstance(projection_axis, tuple):  # (pixel axis, cull axis): reference_axes()
+        axis = int(projection_axis[0])
+        if int(projection_axis[1]) != axis:
+            axis |= (int(projection_axis[1]) + 1) << 4  # ASP_AXIS_CULL
+    else:
+        axis = axis_index(projection_axis)
+    k = len(props)
+    if not 1 <= k <= 6:
+        raise ValueError("props: 1 .. 6 arrays")
+    dev = positions.device if hasattr(positions, "is_cuda") and positions.is_cuda \
+        else torch.device("cuda", device)
+
+    def on_dev(a, shape):
+        t = a if hasattr(a, "is_cuda") and a.is_cuda else torch.from_numpy(
+            np.ascontiguousarray(np.asarray(a), dtype=np.float64))
+        t = t.to(device=dev, dtype=torch.float64).contiguous()
+        if tuple(t.shape) != shape:
+            raise ValueError(f"array of shape {tuple(t.shape)}, expected {shape}")
+        return t
+
+    n = int(positions.shape[0])
+    pos = on_dev(positions, (n, 3))
+    hh = on_dev(np.asarray(h).reshape(-1) if not hasattr(h, "is_cuda") else h.reshape(-1), (n,))
+    pr = [on_dev(np.asarray(a).reshape(-1) if not hasattr(a, "is_cuda") else a.reshape(-1), (n,))
+          for a in props]
+    nx, ny = int(image_size[0]), int(image_size[1])
+    outs = [torch.empty((nx, ny), dtype=torch.float32, device=dev) for _ in range(k)]
+    P = _lib.ptr
+    pa = (_lib._d * k)(*[P(a, _lib._d) for a in pr])
+    po = (_lib._f * k)(*[P(o) for o in outs])
+    x_min, x_max, y_min, y_max = (float(e) for e in extent)
+    _lib.check(_lib.lib().asp_project2d_props_f64(
+        P(pos, _lib._d), P(hh, _lib._d), pa, k, n, axis, x_min, x_max, y_min, y_max, nx, ny,
+        int(chunk_size), kernel_id(kernel), _lib.ASP_F_DEVICE_PTRS, po, dev.index or 0,
+        torch.cuda.current_stream(dev).cuda_stream))
+    return outs
+
+
 def _f64_arg(a, name, n, shape_tail=()):
     """A float64 input of create_image: a contiguous host array (NumPy / unyt) or a
     float64 device tensor; returns (object keeping it alive, ctypes pointer, on_device)."""

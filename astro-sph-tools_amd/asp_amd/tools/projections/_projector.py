@@ -155,6 +155,37 @@ def create_weighted_image(positions, smoothing_lengths, weights, values, image_s
     return r.astype(dtype, copy=False)
 
 
+def create_images(positions, smoothing_lengths, particle_properties, image_size, chunk_size,
+                  projection_axis, x_min, x_max, y_min, y_max,
+                  kernel_func=quartic_spline_kernel, *, device: int = 0, dtype=np.float64):
+    """One :func:`create_image` map per array of ``particle_properties`` (a sequence of 1..6
+    property arrays, e.g. mass, mass * temperature, ion masses) from ONE binning of the
+    particles: the callers that render several maps of one snapshot
+    (io/data_structures/_SnapshotBase.py:618-906) pay the counting and scattering once
+    (asp_project2d_props_f64).  Same semantics as ``create_image`` per map (the
+    reference's fp64 decisions on the reader's values); native kernels only."""
+    import torch
+    cs = _check_chunk_size(chunk_size)
+    kid = native_kernel_id(kernel_func)
+    props = [np.asarray(a, dtype=np.float64).reshape(-1) for a in particle_properties]
+    if not 1 <= len(props) <= 6:
+        raise ValueError("particle_properties: 1 .. 6 arrays")
+    for a in props:
+        _lengths(positions, smoothing_lengths, a)
+    nx, ny = int(image_size[0]), int(image_size[1])
+    if nx <= 0 or ny <= 0 or cs < 0:
+        return [np.zeros((max(nx, 0), max(ny, 0)), dtype=dtype) for _ in props]
+    _lib.require_gpu(device)
+    from ...device import project2d_props_f64
+    maps = project2d_props_f64(np.asarray(positions), smoothing_lengths, props,
+                               projection_axis=reference_axes(projection_axis),
+                               image_size=(nx, ny),
+                               extent=tuple(float(np.asarray(e)) for e in (x_min, x_max, y_min, y_max)),
+                               chunk_size=cs, kernel=kid, device=device)
+    torch.cuda.synchronize(maps[0].device)
+    return [m.cpu().numpy().astype(dtype, copy=False) for m in maps]
+
+
 def create_periodic_image(positions, smoothing_lengths, particle_properties, image_size,
                           chunk_size, projection_axis, box_width, centre=None,
                           kernel_func=quartic_spline_kernel, *, origin_is_centre: bool = False,

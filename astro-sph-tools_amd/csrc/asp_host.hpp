@@ -64,6 +64,8 @@ struct Workspace {
     Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
         wide, slabs, morton, aux[6], iorder;
     Buf in64[4];     // asp_project2d_f64: the caller's fp64 arrays, resident for exact decisions
+    Buf ext;         // asp_project2d_props: per record, the coefficients of properties 2..5
+    Buf inx[4];      // asp_project2d_props_f64: fp32 working copies of properties 2..5
     Buf pairs[4];    // asp_pair_list
     int* h_counters = nullptr;  // pinned
     int morton_ntx = -1, morton_nty = -1;
@@ -87,7 +89,9 @@ struct Workspace {
     int pin_next = 0;
     std::vector<Buf*> all_bufs() {
         std::vector<Buf*> v = {&hist, &cmx, &tile_total, &tile_start, &tile_k, &items, &merges,
-                               &counters, &recs, &wide, &slabs, &morton, &morton3, &iorder};
+                               &counters, &recs, &wide, &slabs, &morton, &morton3, &iorder,
+                               &ext};
+        for (auto& b : inx) v.push_back(&b);
         for (auto& b : in) v.push_back(&b);
         for (auto& b : out) v.push_back(&b);
         for (auto& b : aux) v.push_back(&b);

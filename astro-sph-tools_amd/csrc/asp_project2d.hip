@@ -245,14 +245,23 @@ __device__ __forceinline__ void load_props(const float* __restrict__ a0,
 // branches (the fp32 kernels carry no fp64 load path at all).
 // PROBE: 1 for the placement trials' launches (the same code under its own name, so that
 // profiles of the steady state show them apart).
-template <int KID, int NOUT, int ACC, bool CULL, int SRC, int PROBE>
+// Properties 2..5 of asp_project2d_props (NX = 1): their arrays (unused ones repeat
+// a[0]) and the per-record coefficient array ext (float4 {c2, c3, c4, c5} at the record's
+// slot), written beside the records so every further pair of maps deposits from the SAME
+// binning.
+struct XArgs {
+    const float* a[4];
+    float4* ext;
+};
+
+template <int KID, int NOUT, int ACC, bool CULL, int SRC, int PROBE, int NX = 0>
 __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
     const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long nblk,
     Grid g, Src64 s, const int* __restrict__ hist, const long long* __restrict__ tile_start,
     const int* __restrict__ tile_total, float4* __restrict__ recs, unsigned* __restrict__ cmx,
     int* __restrict__ wide_list, int* __restrict__ ctr, int grp, long long rec_cap,
-    int wide_cap) {
+    int wide_cap, XArgs xa) {
     // Speculative launch (enqueued before the host has read the counters): the record and
     // wide-list buffers were sized by an earlier call; if this call needs more, every
     // workgroup leaves at once and the host relaunches after growing them.
@@ -311,9 +320,21 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
         first_box[k] = 0u;
     }
     const bool al = aligned_vec<kUnroll>(u, v, h) && aligned_vec<kUnroll>(a0, NOUT == 2 ? a1 : a0, a0);
+    // NX: properties 2..5, loaded with the batch (software-pipelined like the others)
+    float px[NX ? 4 : 1][kUnroll];
+    const bool alx = NX && aligned_vec<kUnroll>(xa.a[0], xa.a[1], xa.a[2]) &&
+                     aligned_vec<kUnroll>(xa.a[3], xa.a[3], xa.a[3]);
+    auto load_x = [&](long long b, float (&dst)[NX ? 4 : 1][kUnroll]) {
+        if constexpr (NX) {
+            const long long q = b + (long long)threadIdx.x * kUnroll;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) load_vec<kUnroll>(xa.a[j], q, n, alx, dst[j]);
+        }
+    };
     load_batch<kUnroll>(u, v, h, p0, n, al, pu, pv, ph);
     load_props<NOUT>(a0, a1, p0, n, al, pa0, pa1);
     load_src(p0, pU, pV);
+    load_x(p0, px);
     for (long long base = p0, next; base < n; base = next) {
         next = batch_base(++c);
         float nu[kUnroll], nv[kUnroll], nh[kUnroll], na0[kUnroll], na1[kUnroll];
@@ -321,6 +342,8 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
         load_props<NOUT>(a0, a1, next, n, al, na0, na1);
         double nU[kUnroll], nV[kUnroll];
         load_src(next, nU, nV);
+        float nx_[NX ? 4 : 1][kUnroll];
+        load_x(next, nx_);
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
             const int p = (int)(base + (long long)threadIdx.x * kUnroll + k);
@@ -330,6 +353,12 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             // scales
             const float cf0 = (float)term_coef<KID>(pa0[k], ph[k]);
             const float cf1 = NOUT == 2 ? (float)term_coef<KID>(pa1[k], ph[k]) : 0.0f;
+            float4 cx = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if constexpr (NX)
+                cx = make_float4((float)term_coef<KID>(px[0][k], ph[k]),
+                                 (float)term_coef<KID>(px[1][k], ph[k]),
+                                 (float)term_coef<KID>(px[2][k], ph[k]),
+                                 (float)term_coef<KID>(px[3][k], ph[k]));
             unsigned c0 = 0u, c1 = 0u;
             if constexpr (ACC == kAccFix) {
                 c0 = __float_as_uint(fabsf(cf0));
@@ -362,6 +391,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                 const unsigned bp = tile_box(b, tx, ty);
                 const int col = mb && box_large(bp, g) ? t + g.ntiles : t;
                 int slot = atomicAdd(&cur[col], 1);
+                if constexpr (NX) rec_store(&xa.ext[slot], cx);
                 if constexpr (ACC == kAccFix) {
                     atomicMax(&cm[t * NOUT], c0);
                     if (NOUT == 2) atomicMax(&cm[t * NOUT + 1], c1);
@@ -424,6 +454,11 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             pU[k] = nU[k];
             pV[k] = nV[k];
         }
+        if constexpr (NX)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int k = 0; k < kUnroll; ++k) px[j][k] = nx_[j][k];
     }
     __syncthreads();
     if constexpr (ACC == kAccFix) {
@@ -580,6 +615,13 @@ __device__ __forceinline__ void rec_prep(const float4& r0, const float4& r1, int
 __device__ __forceinline__ void load_rec(const float4* recs, long long i, float4& r0, float4& r1) {
     r0 = recs[2 * i];
     r1 = recs[2 * i + 1];
+}
+
+// asp_project2d_props, pass 1 / 2: the record's coefficients of properties (2, 3) / (4, 5)
+// replace those of (0, 1) (EXT kernels; the binning, band and box are the record's own).
+__device__ __forceinline__ void ext_coef(Prep& P, const float4& e, int pass) {
+    P.s0 = pass == 1 ? e.x : e.z;
+    P.s1 = pass == 1 ? e.y : e.w;
 }
 
 constexpr int kTilePix = kTile * kTile;
@@ -778,9 +820,10 @@ constexpr int kDeferCap = 128;
 // Exact body for deferred records: lanes 0 .. cnt-1 take list entries first .. first+cnt-1
 // (record indices within the item), reload and re-prepare them and decide every pair
 // with the error-band / fp64 logic of small_box.  Wave-level: no block barrier.
-template <int KID, int NOUT, int ACC>
+template <int KID, int NOUT, int ACC, int EXT>
 __device__ __forceinline__ void deferred(const Grid& g, const Src64& s,
-                                         const float4* __restrict__ recs, long long start,
+                                         const float4* __restrict__ recs,
+                                         const float4* __restrict__ ext, int pass, long long start,
                                          const int* dlist, int first, int cnt, int X0, int Y0,
                                          int2 kk, const float* xt, const float* yt,
                                          unsigned long long* acc0, unsigned long long* acc1,
@@ -795,6 +838,7 @@ __device__ __forceinline__ void deferred(const Grid& g, const Src64& s,
     load_rec(recs, start + idx, r0, r1);
     Prep P;
     rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
+    if constexpr (EXT) ext_coef(P, ext[start + idx], pass);
     small_box<KID, NOUT, ACC, 4>(g, s, P, P.b.x1 - P.b.x0 + 1, P.b.y1 - P.b.y0 + 1, X0, Y0, xt,
                                  yt, acc0, acc1);
 }
@@ -1151,12 +1195,12 @@ constexpr size_t deposit_lds() {
     return (size_t)NOUT * kTileWords * 8 + 2 * kTile * 4;
 }
 
-template <int KID, int NOUT, int ACC>
+template <int KID, int NOUT, int ACC, int EXT = 0>
 __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_deposit(
     Grid g, Src64 s, const float4* __restrict__ recs, const Item* __restrict__ items,
     const int* __restrict__ order, const int2* __restrict__ tile_k,
     unsigned long long* __restrict__ slabs, float* __restrict__ out0, float* __restrict__ out1,
-    int flags) {
+    int flags, const float4* __restrict__ ext, int pass) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];
     unsigned long long* acc0 = acc;
     unsigned long long* acc1 = acc + kTileWords;
@@ -1185,11 +1229,14 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
     int* dlist = defer_lds[threadIdx.x >> 6];
     int ndef = 0;  // wave-uniform
     // One batch: record i (index within the item; r0, r1 its halves) of every thread.
-    auto batch = [&](int i, const float4& r0, const float4& r1) {
+    auto batch = [&](int i, const float4& r0, const float4& r1, const float4& e) {
         Prep P;
         P.b = Box{0, -1, 0, -1};
         bool live = i < it.count;
-        if (live) rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
+        if (live) {
+            rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
+            if constexpr (EXT) ext_coef(P, e, pass);
+        }
         live = live && P.b.x0 <= P.b.x1;  // (an empty box deposits nothing)
         const int bw = P.b.x1 - P.b.x0 + 1, bh = P.b.y1 - P.b.y0 + 1;
         const bool small = live && is_small(bw, bh);
@@ -1210,8 +1257,8 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
                 ndef += __popcll(am);
                 if (ndef >= 64) {  // a full wave of deferred records
                     ndef -= 64;
-                    deferred<KID, NOUT, ACC>(g, s, recs, it.start, dlist, ndef, 64, X0, Y0, kk,
-                                             xt, yt, acc0, acc1, lane);
+                    deferred<KID, NOUT, ACC, EXT>(g, s, recs, ext, pass, it.start, dlist, ndef,
+                                                  64, X0, Y0, kk, xt, yt, acc0, acc1, lane);
                 }
             }
         }
@@ -1230,21 +1277,30 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
     // before batch i leaves the batch just issued in flight (vmcnt(2); the register
     // rotation makes it wait for batch i + 1 too).  Loads under a branch made it
     // vmcnt(0), i.e. one full memory latency per batch: deposit 1.26 -> 1.22 ms (cfg 3).
-    float4 r0, r1, q0, q1;
+    float4 r0, r1, q0, q1, re, qe;  // (re, qe, ne: the EXT coefficients, pass > 0)
+    auto load_ext = [&](long long i, float4& e) {
+        if constexpr (EXT) e = ext[i];
+        else e = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    };
     load_rec(recs, it.start + min((int)threadIdx.x, last), r0, r1);
+    load_ext(it.start + min((int)threadIdx.x, last), re);
     load_rec(recs, it.start + min((int)threadIdx.x + kDepBlock, last), q0, q1);
+    load_ext(it.start + min((int)threadIdx.x + kDepBlock, last), qe);
     for (int base = 0; base < it.count; base += kDepBlock) {
-        float4 n0, n1;
+        float4 n0, n1, ne;
         load_rec(recs, it.start + min(base + (int)threadIdx.x + 2 * kDepBlock, last), n0, n1);
-        batch(base + threadIdx.x, r0, r1);
+        load_ext(it.start + min(base + (int)threadIdx.x + 2 * kDepBlock, last), ne);
+        batch(base + threadIdx.x, r0, r1, re);
         r0 = q0;
         r1 = q1;
+        re = qe;
         q0 = n0;
         q1 = n1;
+        qe = ne;
     }
     if (ndef > 0)
-        deferred<KID, NOUT, ACC>(g, s, recs, it.start, dlist, 0, ndef, X0, Y0, kk, xt, yt, acc0,
-                                 acc1, lane);
+        deferred<KID, NOUT, ACC, EXT>(g, s, recs, ext, pass, it.start, dlist, 0, ndef, X0, Y0, kk,
+                                      xt, yt, acc0, acc1, lane);
     __syncthreads();
     if (it.slab >= 0) {  // split tile: partial sums, merged by K5 (slab layout unpadded)
         unsigned long long* dst = slabs + (long long)it.slab * NOUT * kTilePix;
@@ -1272,12 +1328,12 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
 // meet its region (gather_walk).  The tile (or its partial slab) is written straight
 // from the registers.
 // ----------------------------------------------------------------------------------
-template <int KID, int NOUT, int ACC>
+template <int KID, int NOUT, int ACC, int EXT = 0>
 __global__ __launch_bounds__(kGatherThreads) void k_gather(
     Grid g, Src64 s, const float4* __restrict__ recs, const Item* __restrict__ items,
     const int* __restrict__ order, const int2* __restrict__ tile_k,
     unsigned long long* __restrict__ slabs, float* __restrict__ out0, float* __restrict__ out1,
-    int flags) {
+    int flags, const float4* __restrict__ ext, int pass) {
     extern __shared__ __attribute__((aligned(16))) double tot[];
     const Item it = items[order[blockIdx.x / kGatherRegions]];  // largest first
     if (it.mode != 1) return;
@@ -1288,8 +1344,9 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(
     // unconditional loads (index clamped to the item's last record), so no wait or copy
     // of the next batch is forced inside the walk
     const int last = it.count - 1;
-    float4 r0, r1;
+    float4 r0, r1, e = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     load_rec(recs, it.start + min(lane, last), r0, r1);
+    if constexpr (EXT) e = ext[it.start + min(lane, last)];
     const GOwn o = gather_owner(blockIdx.x % kGatherRegions);
     GAcc<NOUT, ACC> ga;
     ga.init(tot);
@@ -1300,12 +1357,14 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(
         if (base + lane < it.count) {
             Prep P;
             rec_prep<ACC>(r0, r1, X0, Y0, kk, P);
+            if constexpr (EXT) ext_coef(P, e, pass);
             P.u += corner_off_x(g, P.b.x0 - X0);  // box-origin frame -> tile frame
             P.v += corner_off_y(g, P.b.y0 - Y0);
             mine = make_gentry(P, X0, Y0, kShapeScale<KID>);
         }
         // the next 64 records load while this batch is walked
         load_rec(recs, it.start + min(base + 64 + lane, last), r0, r1);
+        if constexpr (EXT) e = ext[it.start + min(base + 64 + lane, last)];
         gather_walk<KID, NOUT, ACC>(g, s, mine, X0, Y0, o, cc, ga);
     }
     gather_emit<NOUT, ACC>(g, ga, o, X0, Y0, it.slab, slabs, kk.x, kk.y, out0, out1, flags);
@@ -1856,32 +1915,46 @@ static int allow_lds(K kern, size_t bytes) {
 
 // K3 on stream st.  rec_cap / wide_cap: the capacities the kernel checks against the
 // device counters (speculative launch; see project2d).
-template <int KID, int NOUT, int ACC, bool CULL, int SRC, int PROBE>
+template <int KID, int NOUT, int ACC, bool CULL, int SRC, int PROBE, int NX>
 static int scatter_variant(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl,
                            const float* u, const float* v, const float* h, const float* a0,
-                           const float* a1, long long rec_cap, int wide_cap, hipStream_t st) {
+                           const float* a1, long long rec_cap, int wide_cap, hipStream_t st,
+                           const XArgs& xa) {
     int* dc = (int*)ws.counters.p;
-    hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC, CULL, SRC, PROBE>), dim3((unsigned)pl.nblk_s),
+    hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC, CULL, SRC, PROBE, NX>), dim3((unsigned)pl.nblk_s),
                        dim3(kScatterBlock), scatter_lds(g, NOUT, ACC == kAccFix), st, u, v, h, a0,
                        a1, pl.n, pl.nblk, g, s, (const int*)ws.hist.p,
                        (const long long*)ws.tile_start.p, (const int*)ws.tile_total.p,
                        (float4*)ws.recs.p, (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc, pl.grp,
-                       rec_cap, wide_cap);
+                       rec_cap, wide_cap, xa);
     ASP_LAUNCHED();
     return ASP_OK;
 }
 
+// xa (asp_project2d_props): also write every record's coefficients of properties 2..5
+// (two-map fp64 calls only).
 template <int KID, int NOUT, int ACC>
 static int launch_scatter(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl,
                           const float* u, const float* v, const float* h, const float* a0,
                           const float* a1, long long rec_cap, int wide_cap, hipStream_t st,
-                          bool probe = false) {
+                          bool probe = false, const XArgs* xa = nullptr) {
     StageMark m(ws, kSScatter, st);
-#define ASP_SV(C, S, P) scatter_variant<KID, NOUT, ACC, C, S, P>(g, s, ws, pl, u, v, h, a0, a1, rec_cap, wide_cap, st)
+    const XArgs none{};
     int rc;
-    if (g.nonsquare || g.mixed) rc = probe ? ASP_SV(true, 2, 1) : ASP_SV(true, 2, 0);
-    else if (s.u64) rc = probe ? ASP_SV(false, 1, 1) : ASP_SV(false, 1, 0);
-    else rc = probe ? ASP_SV(false, 0, 1) : ASP_SV(false, 0, 0);
+#define ASP_SV(C, S, P, X) scatter_variant<KID, NOUT, ACC, C, S, P, X>(g, s, ws, pl, u, v, h, a0, a1, rec_cap, wide_cap, st, X ? *xa : none)
+    if constexpr (NOUT == 2 && ACC == kAccF64) {
+        if (xa) {
+            if (g.nonsquare || g.mixed) rc = ASP_SV(true, 2, 0, 1);
+            else if (s.u64) rc = ASP_SV(false, 1, 0, 1);
+            else rc = ASP_SV(false, 0, 0, 1);
+            ASP_TRY(rc);
+            m.done();
+            return ASP_OK;
+        }
+    }
+    if (g.nonsquare || g.mixed) rc = probe ? ASP_SV(true, 2, 1, 0) : ASP_SV(true, 2, 0, 0);
+    else if (s.u64) rc = probe ? ASP_SV(false, 1, 1, 0) : ASP_SV(false, 1, 0, 0);
+    else rc = probe ? ASP_SV(false, 0, 1, 0) : ASP_SV(false, 0, 0, 0);
 #undef ASP_SV
     ASP_TRY(rc);
     m.done();
@@ -1892,7 +1965,8 @@ static int launch_scatter(const Grid& g, const Src64& s, Workspace& ws, const Pl
 template <int KID, int NOUT, int ACC>
 static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl, const float* u,
                     const float* v, const float* h, const float* a0, const float* a1, float* o0,
-                    float* o1, int flags, hipStream_t st, bool pre_scattered) {
+                    float* o1, int flags, hipStream_t st, bool pre_scattered,
+                    const XArgs* xa = nullptr) {
     int* dc = (int*)ws.counters.p;
     const bool ratio = (flags & ASP_F_RATIO) != 0;
     const bool fuse_ratio = ratio && pl.n_wide == 0;
@@ -1901,7 +1975,7 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
                        (fuse_ratio ? kFlagRatio : 0);
     if (!pre_scattered)
         ASP_TRY((launch_scatter<KID, NOUT, ACC>(g, s, ws, pl, u, v, h, a0, a1, 0x7fffffffLL,
-                                                0x7fffffff, st)));
+                                                0x7fffffff, st, false, xa)));
     if (ACC == kAccFix) {
         StageMark m(ws, kSScale, st);
         hipLaunchKernelGGL((k_tilescale<NOUT>), dim3((g.ntiles + 63) / 64), dim3(kBlock), 0, st,
@@ -1915,7 +1989,7 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
         const size_t lds = deposit_lds<NOUT>();
         hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(pl.n_items), dim3(kDepBlock), lds, st, g, s, (const float4*)ws.recs.p,
                            (const Item*)ws.items.p, (const int*)ws.iorder.p, (const int2*)ws.tile_k.p,
-                           (unsigned long long*)ws.slabs.p, o0, o1, dflags);
+                           (unsigned long long*)ws.slabs.p, o0, o1, dflags, (const float4*)nullptr, 0);
         ASP_LAUNCHED();
         m.done();
     }
@@ -1926,7 +2000,7 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
                            dim3(kGatherThreads), lds, st, g,
                            s, (const float4*)ws.recs.p, (const Item*)ws.items.p,
                            (const int*)ws.iorder.p, (const int2*)ws.tile_k.p,
-                           (unsigned long long*)ws.slabs.p, o0, o1, dflags);
+                           (unsigned long long*)ws.slabs.p, o0, o1, dflags, (const float4*)nullptr, 0);
         ASP_LAUNCHED();
         m.done();
     }
@@ -1960,6 +2034,58 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
     return ASP_OK;
 }
 
+// asp_project2d_props, pass p = 1, 2: properties (2p, 2p + 1) deposited from the records
+// the pass-0 map binned and their ext coefficients (K4 / K4g / K5 / K6 as in run_tail, fp64
+// accumulation, no ratio) into o0 (, o1; NOUT = 1 for an odd last property).  xa0 / xa1:
+// the properties' fp32 arrays (the wide particles read them directly).
+template <int KID, int NOUT>
+static int run_ext_pass(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl,
+                        const float* u, const float* v, const float* h, const float* xa0,
+                        const float* xa1, float* o0, float* o1, int flags, hipStream_t st,
+                        int pass) {
+    int* dc = (int*)ws.counters.p;
+    const unsigned long long* slabs = (const unsigned long long*)ws.slabs.p;
+    const int dflags = (flags & ASP_F_ACCUMULATE) ? kFlagAccumulate : 0;
+    const float4* ext = (const float4*)ws.ext.p;
+    {
+        StageMark m(ws, kSDeposit, st);
+        hipLaunchKernelGGL((k_deposit<KID, NOUT, kAccF64, 1>), dim3(pl.n_items), dim3(kDepBlock),
+                           deposit_lds<NOUT>(), st, g, s, (const float4*)ws.recs.p,
+                           (const Item*)ws.items.p, (const int*)ws.iorder.p,
+                           (const int2*)ws.tile_k.p, (unsigned long long*)ws.slabs.p, o0, o1,
+                           dflags, ext, pass);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    if (pl.n_large > 0) {
+        StageMark m(ws, kSGather, st);
+        hipLaunchKernelGGL((k_gather<KID, NOUT, kAccF64, 1>), dim3(pl.n_items * kGatherRegions),
+                           dim3(kGatherThreads), (gather_lds<NOUT, kAccF64>()), st, g, s,
+                           (const float4*)ws.recs.p, (const Item*)ws.items.p,
+                           (const int*)ws.iorder.p, (const int2*)ws.tile_k.p,
+                           (unsigned long long*)ws.slabs.p, o0, o1, dflags, ext, pass);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    if (pl.n_merges > 0) {
+        StageMark m(ws, kSMerge, st);
+        hipLaunchKernelGGL((k_merge<NOUT, kAccF64>), dim3(pl.n_merges, kTilePix / kBlock),
+                           dim3(kBlock), 0, st, g, (const Merge*)ws.merges.p, slabs,
+                           (const int2*)ws.tile_k.p, o0, o1, dflags);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    if (pl.n_wide > 0) {
+        StageMark m(ws, kSWide, st);
+        hipLaunchKernelGGL((k_wide<KID, NOUT, kAccF64>), dim3(g.ntiles * kGatherRegions),
+                           dim3(kGatherThreads), (gather_lds<NOUT, kAccF64>()), st, g, s, u, v, h,
+                           xa0, xa1, (const int*)ws.wide.p, pl.n_wide, (const int*)dc, o0, o1);
+        ASP_LAUNCHED();
+        m.done();
+    }
+    return ASP_OK;
+}
+
 // Tunables read once per call (experiments; the defaults are the measured choices).
 static void grid_tunables(Grid& g) {
     if (const char* e = getenv("ASP_WIDE_TILES")) g.wide_tiles = std::max(1, atoi(e));
@@ -1974,10 +2100,14 @@ static void grid_tunables(Grid& g) {
 // ws for k_pairs -- and return the number of wide particles there.
 constexpr int kRetSplit = 1;  // internal: >= 2^31 records in one pass, nothing written
 
+// xa / nxp / xo (asp_project2d_props): nxp (1..4) further properties xa->a[0 ..] binned
+// with the first two (their coefficients beside each record) and deposited in further
+// passes into xo[0 ..] (two-map fp64 calls only).
 int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float* du,
                      const float* dv, const float* dh, const float* da0, const float* da1,
                      long long n, int kid, int flags, float* d0, float* d1, hipStream_t st,
-                     int* bin_only = nullptr) {
+                     int* bin_only = nullptr, const XArgs* xa = nullptr, int nxp = 0,
+                     float* const* xo = nullptr) {
     Grid g = gin;
     const int nout = d1 ? 2 : 1;
     const long long npix = (long long)g.nx * g.ny;
@@ -1993,6 +2123,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
             StageMark m(ws, kSMemset, st);
             ASP_HIP(hipMemsetAsync(d0, 0, npix * sizeof(float), st));
             if (d1) ASP_HIP(hipMemsetAsync(d1, 0, npix * sizeof(float), st));
+            for (int j = 0; j < nxp; ++j) ASP_HIP(hipMemsetAsync(xo[j], 0, npix * sizeof(float), st));
             m.done();
         }
         for (long long& x : ws.stats) x = 0;
@@ -2058,7 +2189,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     // < 2^31 - 1: the tilescan's clamped record count always exceeds it when it overflows
     const long long rec_cap = (long long)std::min<size_t>(ws.recs.cap / (2 * sizeof(float4)), 0x7ffffffe);
     const int wide_cap = (int)std::min<size_t>(ws.wide.cap / sizeof(int), 0x7fffffff);
-    const bool spec = ws.recs.p && ws.wide.p && getenv("ASP_NO_SPECULATE") == nullptr;
+    const bool spec = ws.recs.p && ws.wide.p && !xa && getenv("ASP_NO_SPECULATE") == nullptr;
     if (spec) {
 #define ASP_SC(K, N, A) \
     launch_scatter<K, N, A>(g, s, ws, pl, du, dv, dh, da0, da1, rec_cap, wide_cap, st)
@@ -2089,8 +2220,14 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     ASP_TRY(ensure(ws.recs, (size_t)pl.n_recs * 2 * sizeof(float4)));
     ASP_TRY(ensure(ws.wide, (size_t)pl.n_wide * sizeof(int)));
     ASP_TRY(ensure(ws.slabs, (size_t)pl.n_slabs * nout * kTilePix * sizeof(long long)));
+    XArgs xw{};
+    if (xa) {  // the extra properties' coefficient array, one float4 per record
+        ASP_TRY(ensure(ws.ext, (size_t)std::max(pl.n_recs, 1LL) * sizeof(float4)));
+        xw = *xa;
+        xw.ext = (float4*)ws.ext.p;
+    }
     bool placed = false;  // the records are already scattered (by the placement trials)
-    if (!bin_only && !pre && ws.recs.p != recs_before) {
+    if (!bin_only && !xa && !pre && ws.recs.p != recs_before) {
 #define ASP_SC(K, N, A) \
     launch_scatter<K, N, A>(g, s, ws, pl, du, dv, dh, da0, da1, 0x7fffffffLL, 0x7fffffff, st, true)
 #define ASP_SC2(K, A) (nout == 1 ? ASP_SC(K, 1, A) : ASP_SC(K, 2, A))
@@ -2114,8 +2251,9 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
         return ASP_OK;
     }
     int rc;
+    const XArgs* xp = xa ? &xw : nullptr;
 #define ASP_TAIL(K, N, A) \
-    run_tail<K, N, A>(g, s, ws, pl, du, dv, dh, da0, da1, d0, d1, flags, st, pre_all)
+    run_tail<K, N, A>(g, s, ws, pl, du, dv, dh, da0, da1, d0, d1, flags, st, pre_all, xp)
 #define ASP_TAIL2(K, A) (nout == 1 ? ASP_TAIL(K, 1, A) : ASP_TAIL(K, 2, A))
 #define ASP_TAIL3(A) (kid == 0 ? ASP_TAIL2(0, A) : kid == 1 ? ASP_TAIL2(1, A) : ASP_TAIL2(2, A))
     rc = det ? ASP_TAIL3(kAccFix) : ASP_TAIL3(kAccF64);
@@ -2123,6 +2261,17 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
 #undef ASP_TAIL2
 #undef ASP_TAIL
     if (rc != ASP_OK) return rc;
+    for (int pass = 1; xa && 2 * (pass - 1) < nxp; ++pass) {  // properties 2.. from the records
+        const int j = 2 * (pass - 1);
+        const bool two = j + 1 < nxp;
+        float* o1x = two ? xo[j + 1] : nullptr;
+        const int xflags = flags & ASP_F_ACCUMULATE;
+#define ASP_XP(K) (two ? run_ext_pass<K, 2>(g, s, ws, pl, du, dv, dh, xw.a[j], xw.a[j + 1], xo[j], o1x, xflags, st, pass) \
+                       : run_ext_pass<K, 1>(g, s, ws, pl, du, dv, dh, xw.a[j], xw.a[j], xo[j], o1x, xflags, st, pass))
+        rc = kid == 0 ? ASP_XP(0) : kid == 1 ? ASP_XP(1) : ASP_XP(2);
+#undef ASP_XP
+        if (rc != ASP_OK) return rc;
+    }
     for (int k = 9; k <= 12; ++k) ws.stats[k] = 0;  // the evals diagnostic of THIS pass only
     if (getenv("ASP_COUNT_EVALS")) {  // diagnostic: the deposit kernels' lane-slots
         ASP_TRY(ensure(ws.aux[5], 3 * sizeof(unsigned long long)));
@@ -2183,7 +2332,8 @@ static Src64 src_from(const Src64& s, long long b) {  // particles b.. of s
 int project2d_full(Workspace& ws, const Grid& full, const Src64& s, const float* du,
                    const float* dv, const float* dh, const float* da0, const float* da1,
                    long long n, int kid, int flags, float* d0, float* d1, hipStream_t st,
-                   int row_lo = 0, int row_hi = -1) {
+                   int row_lo = 0, int row_hi = -1, const XArgs* xa = nullptr, int nxp = 0,
+                   float* const* xo = nullptr) {
     const int wr = window_rows(full);
     const long long B = max_batch();
     long long agg[kNStats] = {0};
@@ -2193,6 +2343,8 @@ int project2d_full(Workspace& ws, const Grid& full, const Src64& s, const float*
         const long long off = (long long)(g.ox - row_lo) * full.ny;
         float* w0 = d0 + off;
         float* w1 = d1 ? d1 + off : nullptr;
+        float* wx[4] = {nullptr, nullptr, nullptr, nullptr};  // the extra properties' maps
+        for (int j = 0; j < nxp; ++j) wx[j] = xo[j] + off;
         std::vector<std::pair<long long, long long>> todo;  // batches, last first
         for (long long a = ((n - 1) / B) * B; a >= 0; a -= B)
             todo.push_back({a, std::min(n, a + B)});
@@ -2205,9 +2357,14 @@ int project2d_full(Workspace& ws, const Grid& full, const Src64& s, const float*
             int f = flags;
             if (batched || b - a < n) f &= ~ASP_F_RATIO;  // ratio after the last batch
             if (passes > 0) f |= ASP_F_ACCUMULATE;
+            XArgs xb{};
+            if (xa) {
+                xb = *xa;
+                for (int j = 0; j < 4; ++j) xb.a[j] += a;
+            }
             const int rc = project2d_device(ws, g, src_from(s, a), du + a, dv + a, dh + a,
                                             da0 + a, da1 ? da1 + a : nullptr, b - a, kid, f,
-                                            w0, w1, st);
+                                            w0, w1, st, nullptr, xa ? &xb : nullptr, nxp, wx);
             if (rc == kRetSplit) {
                 if (b - a < 2)
                     return fail(ASP_ERR_UNSUPPORTED, "one particle makes >= 2^31 records");
@@ -2286,11 +2443,31 @@ static int host_results(float* out0, float* out1, const float* d0, const float* 
     return ASP_OK;
 }
 
+// xprops / nxp / xouts: asp_project2d_props' properties 2.. (device pointers).
+static int check_props(int nxp, const void* const* xprops, float* const* xouts, int flags) {
+    if (nxp == 0) return ASP_OK;
+    if (nxp < 0 || nxp > 4) return fail(ASP_ERR_INVALID, "nprops must be 1 .. 6");
+    if (!xprops || !xouts) return fail(ASP_ERR_INVALID, "NULL props / outs");
+    for (int j = 0; j < nxp; ++j)
+        if (!xprops[j] || !xouts[j]) return fail(ASP_ERR_INVALID, "NULL property or output");
+    if (!(flags & ASP_F_DEVICE_PTRS))
+        return fail(ASP_ERR_UNSUPPORTED, "more than two properties: device pointers only "
+                                         "(ASP_F_DEVICE_PTRS)");
+    if (flags & (ASP_F_RATIO | ASP_F_DETERMINISTIC))
+        return fail(ASP_ERR_UNSUPPORTED, "more than two properties: no ASP_F_RATIO / "
+                                         "ASP_F_DETERMINISTIC (fp64 sums; ratios with asp_ratio)");
+    return ASP_OK;
+}
+
 static int project2d(const float* u, const float* v, const float* h, const float* a0,
                      const float* a1, long long n, double x_min, double x_max, double y_min,
                      double y_max, int nx, int ny, int cs, int kid, int flags, float* out0,
-                     float* out1, int device, void* stream, int row_lo = 0, int row_hi = -1) {
+                     float* out1, int device, void* stream, int row_lo = 0, int row_hi = -1,
+                     const float* const* xprops = nullptr, int nxp = 0,
+                     float* const* xouts = nullptr) {
     ASP_TRY(check_args(a1, out0, out1, n, kid, flags));
+    ASP_TRY(check_props(nxp, (const void* const*)xprops, xouts, flags));
+    if (nxp > 0 && !a1) return fail(ASP_ERR_INVALID, "properties 2.. need a1 / out1");
     if (n > 0 && (!u || !v || !h || !a0)) return fail(ASP_ERR_INVALID, "NULL particle array");
     Grid g;
     ASP_TRY(setup_grid(x_min, x_max, y_min, y_max, nx, ny, cs, g));
@@ -2323,19 +2500,32 @@ static int project2d(const float* u, const float* v, const float* h, const float
         ASP_TRY(host_outputs(ws, out0, out1, npix, flags, st, d0, d1));
     }
     const Src64 s{nullptr, nullptr, nullptr, nullptr, nullptr, 0, du, dv, dh};
+    XArgs xa{};
+    for (int j = 0; j < 4; ++j) xa.a[j] = j < nxp ? xprops[j] : (nxp ? xprops[0] : nullptr);
     ASP_TRY(project2d_full(ws, g, s, du, dv, dh, da0, da1, n, kid, flags, d0, d1, st, row_lo,
-                           row_hi));
+                           row_hi, nxp ? &xa : nullptr, nxp, xouts));
     if (!dev) ASP_TRY(host_results(out0, out1, d0, d1, npix, st));
     return ws_end_.finish();
 }
 
 // create_image on the reader's fp64 arrays: stage (axis selection, fp32 working copies in
 // HBM) and project with the fp64 values kept for the exact re-decisions.
+__global__ __launch_bounds__(kBlock) void k_to_f32(const double* __restrict__ a,
+                                                   float* __restrict__ b, long long n) {
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (long long)gridDim.x * kBlock)
+        b[i] = (float)a[i];  // round to nearest, as NumPy's astype(float32)
+}
+
 static int project2d_f64(const double* pos, const double* h, const double* a0,
                          const double* a1, long long n, int axis, double x_min, double x_max,
                          double y_min, double y_max, int nx, int ny, int cs, int kid, int flags,
-                         float* out0, float* out1, int device, void* stream) {
+                         float* out0, float* out1, int device, void* stream,
+                         const double* const* xprops = nullptr, int nxp = 0,
+                         float* const* xouts = nullptr) {
     ASP_TRY(check_args(a1, out0, out1, n, kid, flags));
+    ASP_TRY(check_props(nxp, (const void* const*)xprops, xouts, flags));
+    if (nxp > 0 && !a1) return fail(ASP_ERR_INVALID, "properties 2.. need a1 / out1");
     if (n > 0 && (!pos || !h || !a0)) return fail(ASP_ERR_INVALID, "NULL particle array");
     // axis: the pixel test's axis, | ASP_AXIS_CULL(c) to cull on axis c's columns
     const int cull_axis = (axis >> 4) ? (axis >> 4) - 1 : (axis & 15);
@@ -2378,8 +2568,20 @@ static int project2d_f64(const double* pos, const double* h, const double* a0,
     static const int cols[3][2] = {{1, 2}, {0, 2}, {0, 1}};  // _projector.py:38-46
     const Src64 s{dpos + cols[axis][0], dpos + cols[axis][1], dpos + cols[cull_axis][0],
                   dpos + cols[cull_axis][1], dh64, 3, f[0], f[1], f[2]};
+    XArgs xa{};
+    for (int j = 0; j < nxp; ++j) {  // fp32 working copies of properties 2..
+        ASP_TRY(ensure(ws.inx[j], (size_t)std::max(n, 1LL) * sizeof(float)));
+        if (n > 0) {
+            const long long blocks = std::min<long long>((n + kBlock - 1) / kBlock, 8192);
+            hipLaunchKernelGGL(k_to_f32, dim3((unsigned)blocks), dim3(kBlock), 0, st, xprops[j],
+                               (float*)ws.inx[j].p, n);
+            ASP_LAUNCHED();
+        }
+    }
+    for (int j = 0; j < 4; ++j) xa.a[j] = nxp ? (const float*)ws.inx[j < nxp ? j : 0].p : nullptr;
     ASP_TRY(project2d_full(ws, g, s, f[0], f[1], f[2], f[3], f[4], n, kid,
-                           (flags & ~ASP_F_DEVICE_OUTPUTS) | ASP_F_DEVICE_PTRS, d0, d1, st));
+                           (flags & ~ASP_F_DEVICE_OUTPUTS) | ASP_F_DEVICE_PTRS, d0, d1, st, 0, -1,
+                           nxp ? &xa : nullptr, nxp, xouts));
     if (!dev_out) ASP_TRY(host_results(out0, out1, d0, d1, npix, st));
     return ws_end_.finish();
 }
@@ -2643,6 +2845,36 @@ int asp_project2d_rows(const float* u, const float* v, const float* h, const flo
     t_err.clear();
     return project2d(u, v, h, a0, a1, n, u_min, u_max, v_min, v_max, nx, ny, chunk_size,
                      kernel_id, flags, out0, out1, device, stream, row_lo, row_hi);
+}
+
+int asp_project2d_props(const float* u, const float* v, const float* h, const float* const* props,
+                        int32_t nprops, int64_t n, double u_min, double u_max, double v_min,
+                        double v_max, int32_t nx, int32_t ny, int32_t chunk_size,
+                        int32_t kernel_id, int32_t flags, float* const* outs, int32_t device,
+                        void* stream) {
+    t_err.clear();
+    if (nprops < 1 || nprops > 6 || !props || !outs)
+        return fail(ASP_ERR_INVALID, "nprops must be 1 .. 6 with props / outs given");
+    return project2d(u, v, h, props[0], nprops > 1 ? props[1] : nullptr, n, u_min, u_max, v_min,
+                     v_max, nx, ny, chunk_size, kernel_id, flags, outs[0],
+                     nprops > 1 ? outs[1] : nullptr, device, stream, 0, -1,
+                     nprops > 2 ? props + 2 : nullptr, std::max(0, nprops - 2),
+                     nprops > 2 ? outs + 2 : nullptr);
+}
+
+int asp_project2d_props_f64(const double* positions, const double* h,
+                            const double* const* props, int32_t nprops, int64_t n, int32_t axis,
+                            double u_min, double u_max, double v_min, double v_max, int32_t nx,
+                            int32_t ny, int32_t chunk_size, int32_t kernel_id, int32_t flags,
+                            float* const* outs, int32_t device, void* stream) {
+    t_err.clear();
+    if (nprops < 1 || nprops > 6 || !props || !outs)
+        return fail(ASP_ERR_INVALID, "nprops must be 1 .. 6 with props / outs given");
+    return project2d_f64(positions, h, props[0], nprops > 1 ? props[1] : nullptr, n, axis, u_min,
+                         u_max, v_min, v_max, nx, ny, chunk_size, kernel_id, flags, outs[0],
+                         nprops > 1 ? outs[1] : nullptr, device, stream,
+                         nprops > 2 ? props + 2 : nullptr, std::max(0, nprops - 2),
+                         nprops > 2 ? outs + 2 : nullptr);
 }
 
 int asp_project2d_f64(const double* positions, const double* h, const double* a0,

@@ -849,7 +849,9 @@ def main():
                                f"map, {args.kernel}, {args.h_law}-scale h, fp32"
                                + ((f", Z-slab x{world} + {backend_label} {args.op}"
                                    if R is None else
-                                   f", image row slabs x{world} + {backend_label} all-gather")
+                                   f", image row slabs x{world} + {backend_label} "
+                                   + ("all-gather" if args.rows_gather == "all"
+                                      else "gather to rank 0"))
                                   if world > 1 else ""),
                    "particles": args.n, "grid": G, "kernel": args.kernel, "h_law": args.h_law,
                    "map": args.map,
@@ -860,7 +862,9 @@ def main():
                    "accumulation": "int64 fixed point" if args.deterministic else "fp64",
                    "collective_overlap": world > 1 and args.pipeline,
                    "streams": ns,
-                   **({"slab_weight": args.slab_weight, "collective": args.op,
+                   **({"slab_weight": args.slab_weight,
+                       "collective": args.op if R is None else
+                       ("all_gather" if args.rows_gather == "all" else "p2p_gather"),
                        "partition": ("Z-slab split of the generated particles before the "
                                      "timed region (untimed, as a reader-split snapshot "
                                      "needs none)" if R is None else

@@ -111,6 +111,33 @@ int asp_project2d_rows(const float *u, const float *v, const float *h, const flo
                        float *out1, int32_t device, void *stream);
 
 /*
+ * Several property maps from ONE binning (the callers render m, m*T, ion masses ... of
+ * the same particles: io/data_structures/_SnapshotBase.py:618-906): out_k = the
+ * asp_project2d map of props[k] for k < nprops <= 6, every map over the same neighbour
+ * sets.  The particles are counted and scattered once; the records carry the first two
+ * properties' coefficients and, beside them, those of properties 2..5, which further
+ * deposit passes read.  nprops <= 2 is asp_project2d; more need ASP_F_DEVICE_PTRS (device
+ * pointers) and fp64 accumulation (no ASP_F_RATIO / ASP_F_DETERMINISTIC: form ratios
+ * with asp_ratio).  props / outs are host arrays of nprops device pointers.
+ */
+int asp_project2d_props(const float *u, const float *v, const float *h,
+                        const float *const *props, int32_t nprops, int64_t n, double u_min,
+                        double u_max, double v_min, double v_max, int32_t nx, int32_t ny,
+                        int32_t chunk_size, int32_t kernel_id, int32_t flags,
+                        float *const *outs, int32_t device, void *stream);
+
+/*
+ * The same on the reader's float64 arrays (positions (n, 3), h, props[k] float64, all on
+ * the device: ASP_F_DEVICE_PTRS), with the exact fp64 decisions of asp_project2d_f64.
+ */
+int asp_project2d_props_f64(const double *positions, const double *h,
+                            const double *const *props, int32_t nprops, int64_t n,
+                            int32_t axis, double u_min, double u_max, double v_min,
+                            double v_max, int32_t nx, int32_t ny, int32_t chunk_size,
+                            int32_t kernel_id, int32_t flags, float *const *outs,
+                            int32_t device, void *stream);
+
+/*
  * create_image on the reader's own float64 arrays: the drop-in for create_image
  * (_projector.py:75-120) as it is called, with positions (n, 3) float64 row-major (the
  * reader's get_positions, _SnapshotBase.py:708-722), smoothing lengths and properties

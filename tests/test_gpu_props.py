@@ -1,0 +1,90 @@
+"""Several property maps from ONE binning (asp_project2d_props / _props_f64, create_images):
+each map equals the single-property projection of the same particles -- the same
+neighbour sets (indicator maps exact), values equal up to fp64 summation order -- for 1 to
+6 properties (odd counts included), at pixel and physical h (gathered large stream,
+wide particles, split tiles), and through the reference-style host API."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b):
+    import torch
+    torch.testing.assert_close(a, b, rtol=2e-6, atol=1e-7 * float(b.abs().max()) + 1e-30)
+
+
+@pytest.mark.parametrize("h_law,G,k,wide", [("pixel", 512, 6, None), ("physical", 512, 3, "16"),
+                                            ("physical", 1024, 5, None), ("pixel", 256, 4, None)])
+def test_props_equal_single_maps(gpu, h_law, G, k, wide, monkeypatch):
+    import torch
+    from asp_amd.device import project2d, project2d_props, stats
+    from asp_amd.plummer import plummer_torch
+    if wide:
+        monkeypatch.setenv("ASP_WIDE_TILES", wide)
+    d = plummer_torch(200_000, seed=7, h_law=h_law, extent=4.0, grid=G, device="cuda")
+    u, v, h, m, T = d["x"], d["y"], d["h"], d["m"], d["T"]
+    props = [m, (m * T).contiguous(), torch.ones_like(m), T, (m * m).contiguous(),
+             (T * 0.5 + 1.0).contiguous()][:k]
+    kw = dict(image_size=(G, G), extent=(-4.0, 4.0, -4.0, 4.0), kernel="wendland_c2")
+    outs = project2d_props(u, v, h, props, **kw)
+    st = stats(0)
+    if wide:
+        assert st["wide"] > 0
+    for a, o in zip(props, outs):
+        want, _ = project2d(u, v, h, a, **kw)
+        _close(o, want)
+    # the same neighbour sets: the indicator kernel's counts, exact
+    ones = torch.ones_like(m)
+    cnts = project2d_props(u, v, h, [ones] * k, image_size=(G, G), extent=kw["extent"],
+                           kernel="indicator")
+    want, _ = project2d(u, v, h, ones, image_size=(G, G), extent=kw["extent"], kernel="indicator")
+    for c in cnts:
+        assert torch.equal(c, want)
+
+
+def test_create_images_host_api(gpu, oracle):
+    """create_images on the reader's raw float64 arrays = create_image per property (the
+    fp64 decisions of asp_project2d_f64), and against the oracle within the value bar."""
+    from asp_amd.tools.projections import create_image, create_images, indicator_kernel
+    from test_gpu_parity import assert_map_close
+    rng = np.random.default_rng(4)
+    n = 30_000
+    pos = rng.normal(0, 0.6, (n, 3))
+    h = rng.uniform(0.01, 0.2, n)
+    m = rng.uniform(0.5, 1.5, n)
+    T = rng.uniform(1e3, 1e5, n)
+    size, ext = (300, 200), (-2.0, 2.0, -2.0, 2.0)
+    maps = create_images(pos, h, [m, m * T, np.ones(n)], size, 32, "y", *ext)
+    for a, got in zip((m, m * T), maps):
+        want = create_image(pos, h, a, size, 32, "y", *ext)
+        np.testing.assert_allclose(got, want, rtol=2e-6, atol=1e-7 * np.abs(want).max())
+    cnt = create_images(pos, h, [np.ones(n), np.ones(n), np.ones(n)], size, 32, 2, *ext,
+                        kernel_func=indicator_kernel)
+    want = create_image(pos, h, np.ones(n), size, 32, 2, *ext, kernel_func=indicator_kernel)
+    for c in cnt:
+        assert np.array_equal(c, want)
+    o0, _ = oracle.project_scatter(pos[:, 0], pos[:, 1], h, m * T, None, size, 32, *ext)
+    mz = create_images(pos, h, [m * T, m], size, 32, 2, *ext)
+    assert_map_close(mz[0], o0)
+
+
+def test_props_argument_errors(gpu):
+    import torch
+    from asp_amd import _lib
+    from asp_amd.device import project2d_props
+    from asp_amd.plummer import plummer_torch
+    d = plummer_torch(1000, seed=1, h_law="pixel", extent=4.0, grid=64, device="cuda")
+    kw = dict(image_size=(64, 64), extent=(-4, 4, -4, 4))
+    with pytest.raises(ValueError):
+        project2d_props(d["x"], d["y"], d["h"], [d["m"]] * 7, **kw)
+    with pytest.raises(ValueError):
+        project2d_props(d["x"], d["y"], d["h"], [], **kw)
+    P = _lib.ptr
+    outs = [torch.empty((64, 64), device="cuda") for _ in range(3)]
+    pa = (_lib._f * 3)(*[P(d["m"])] * 3)
+    po = (_lib._f * 3)(*[P(o) for o in outs])
+    rc = _lib.lib().asp_project2d_props(P(d["x"]), P(d["y"]), P(d["h"]), pa, 3, 1000, -4.0, 4.0,
+                                        -4.0, 4.0, 64, 64, 64, 1,
+                                        _lib.ASP_F_DEVICE_PTRS | _lib.ASP_F_RATIO, po, 0, None)
+    assert rc == _lib.ASP_ERR_UNSUPPORTED
