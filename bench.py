@@ -113,11 +113,10 @@ def chunk_cull_counts(pos, h, grid, cs, extent):
     x0, x1, y0, y1 = lo(pos[:, 0]), hi(pos[:, 0]), lo(pos[:, 1]), hi(pos[:, 1])
     ok = (x0 <= x1) & (y0 <= y1)
     x0, x1, y0, y1 = (a[ok].astype(np.int64) for a in (x0, x1, y0, y1))
-    d = np.zeros((nc + 1, nc + 1), np.int64)
-    np.add.at(d, (x0, y0), 1)
-    np.add.at(d, (x1 + 1, y0), -1)
-    np.add.at(d, (x0, y1 + 1), -1)
-    np.add.at(d, (x1 + 1, y1 + 1), 1)
+    m = nc + 1
+    cnt = lambda i, j: np.bincount(i * m + j, minlength=m * m)  # noqa: E731
+    d = cnt(x0, y0) - cnt(x1 + 1, y0) - cnt(x0, y1 + 1) + cnt(x1 + 1, y1 + 1)
+    d = d.reshape(m, m)
     return np.cumsum(np.cumsum(d, 0), 1)[:nc, :nc].reshape(-1).astype(np.float64)
 
 
