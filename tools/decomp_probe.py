@@ -95,13 +95,27 @@ def main():
             ms = timed(lambda: project2d(u, v, h, a0, m, image_size=(G, G), extent=ext,
                                          kernel="wendland_c2", ratio=True, out0=o0, out1=o1,
                                          rows=(R[r], R[r + 1])), a.reps)
+            # the bench's N > 1 form: consecutive maps alternate two streams (and buffers)
+            ss = [torch.cuda.Stream(device=dev) for _ in range(2)]
+            ob = [(o0, o1), (torch.empty_like(o0), torch.empty_like(o1))]
+
+            def two(k=8):
+                for q in range(k):
+                    with torch.cuda.stream(ss[q % 2]):
+                        project2d(u, v, h, a0, m, image_size=(G, G), extent=ext,
+                                  kernel="wendland_c2", ratio=True, out0=ob[q % 2][0],
+                                  out1=ob[q % 2][1], rows=(R[r], R[r + 1]))
+            ms2 = timed(two, a.reps) / 8
             rows.append({"rank": r, "rows": [R[r], R[r + 1]], "particles": int(keep.sum()),
-                         "ms": round(ms, 4)})
+                         "ms": round(ms, 4), "ms_two_streams": round(ms2, 4)})
             print("rows", rows[-1], flush=True)
             del u, v, h, m, a0, o0, o1
         shares["rows"] = rows
         res["rows_bounds"] = R
         res["rows_duplication"] = round(sum(x["particles"] for x in rows) / int(a.n), 5)
+        ms2 = [x["ms_two_streams"] for x in shares["rows"]]
+        res["rows_two_streams_max_ms"] = max(ms2)
+        print("rows, two streams: max %.4f mean %.4f" % (max(ms2), sum(ms2) / len(ms2)), flush=True)
         for k, rr in shares.items():
             ms = [x["ms"] for x in rr]
             res[k] = {"shares": rr, "max_ms": max(ms), "mean_ms": round(sum(ms) / len(ms), 4),
