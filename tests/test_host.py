@@ -148,3 +148,26 @@ def test_plugin_argument_lengths():
     with pytest.raises(ValueError):
         project_callable(np.zeros((10, 2)), np.ones(10), [np.ones(10)], (2, 2), (8, 8), 4,
                          (0, 1, 0, 1), f)
+
+
+def test_cpu_baseline_chunk_counts():
+    """bench.py's CPU-baseline regressor: the particles the reference's chunk cull admits
+    (_projector.py:38-48) into each chunk, by a 2-D difference array -- equal to the
+    brute-force count of the cull's inequalities for every chunk."""
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    rng = np.random.default_rng(5)
+    n, G, cs, ext = 20_000, 256, 32, 4.0
+    pos = rng.normal(0, 1.2, (n, 3))
+    h = rng.uniform(0.0, 0.3, n)
+    x = bench.chunk_cull_counts(pos, h, G, cs, ext)
+    nc, w = G // cs, 2 * ext / (G // cs)
+    u, v, r = pos[:, 0], pos[:, 1], 2 * np.abs(h)
+    want = np.zeros(nc * nc)
+    for cx in range(nc):
+        for cy in range(nc):
+            xl, yl = -ext + cx * w, -ext + cy * w
+            want[cx * nc + cy] = np.sum((u >= xl - r) & (u < xl + w + r) & (v >= yl - r) &
+                                        (v < yl + w + r))
+    assert np.abs(x - want).max() <= 0.001 * want.max()  # float edge cases at chunk bounds
