@@ -10,7 +10,7 @@
 // MI355X layout: particles sorted along a 63-bit Morton curve (21 bits per axis over the
 // bounding cube; rocPRIM radix sort), positions gathered into sorted fp64 SoA.  One wave
 // takes 64 consecutive particles of the curve (k_knn_wave):
-//   1. the curve window of W = 128 entries either side is streamed once per wave through
+//   1. the curve window of W = 64 entries either side is streamed once per wave through
 //      LDS (coalesced), every lane testing every entry; candidates below a lane's k-th
 //      distance so far are buffered in registers and merged into its register top-k a
 //      few at a time (the O(k) insertion does not run per candidate for the whole wave);
@@ -201,9 +201,20 @@ __device__ __forceinline__ long long lower_bound(const unsigned long long* __res
 // Cell table of one Morton level L (the finest level with about one particle per cell):
 // tab[c] = the first sorted index whose key lies in cell c or later (c < 8^L), tab[8^L] = n.
 // A cell of any level <= L is then a range [tab[.], tab[.]) by two loads instead of two
-// binary searches over the whole array; finer cells search inside their level-L cell only.
+// binary searches over the whole array.  The grid spans the bounding cube, so in a
+// centrally concentrated set the level-L cells of the dense part hold thousands of
+// particles (10^7 Plummer: median 5400 per particle's cell at L = 8); a level-L cell with
+// more than kSubMin particles gets a sub-table over its 8^3 cells three levels down
+// (same form: the first index of each sub-cell, entry 512 = the cell's end), so a finer
+// cell is two table loads plus a binary search inside its sub-cell (median 11 particles
+// at L + 3) instead of one over the whole level-L cell.
+constexpr int kSubLevels = 3;
+constexpr int kSubCells = 1 << (3 * kSubLevels);  // 512 sub-cells per sub-table
+constexpr int kSubMin = 64;                       // level-L cells above this get one
 struct CellTab {
     const int* tab;
+    const int* sub;     // per level-L cell: its sub-table, or -1
+    const int* subtab;  // sub-tables, kSubCells + 1 entries each
     int sh;  // 63 - 3 L: key >> sh = the level-L cell
 };
 
@@ -216,13 +227,52 @@ __global__ __launch_bounds__(kKnnBlock) void k_cell_table(const unsigned long lo
     for (long long q = cp + 1; q <= c; ++q) tab[q] = (int)i;  // the cells starting here
 }
 
-// First index with key >= k0 (k0 < 2^63), through the table.
+// Sub-table slots of the dense level-L cells (slot order does not matter).
+__global__ __launch_bounds__(kKnnBlock) void k_sub_slots(const int* __restrict__ tab, long long ncell,
+                                                          int* __restrict__ sub, int* __restrict__ nslot) {
+    long long c = (long long)blockIdx.x * kKnnBlock + threadIdx.x;
+    if (c >= ncell) return;
+    sub[c] = tab[c + 1] - tab[c] > kSubMin ? atomicAdd(nslot, 1) : -1;
+}
+
+// Per particle of a dense cell: the sub-cells starting at it (as k_cell_table), and the
+// cell's last particle closes the table.
+__global__ __launch_bounds__(kKnnBlock) void k_sub_table(const unsigned long long* __restrict__ keys,
+                                                          long long n, int sh,
+                                                          const int* __restrict__ tab,
+                                                          const int* __restrict__ sub,
+                                                          int* __restrict__ subtab) {
+    long long i = (long long)blockIdx.x * kKnnBlock + threadIdx.x;
+    if (i >= n) return;
+    const long long c = (long long)(keys[i] >> sh);
+    const int s = sub[c];
+    if (s < 0) return;
+    const int sh2 = sh - 3 * kSubLevels;
+    int* st = subtab + (long long)s * (kSubCells + 1);
+    const int q = (int)((keys[i] >> sh2) & (kSubCells - 1));
+    const int first = tab[c], end = tab[c + 1];
+    const int qp = i == first ? -1 : (int)((keys[i - 1] >> sh2) & (kSubCells - 1));
+    for (int r = qp + 1; r <= q; ++r) st[r] = (int)i;
+    if (i == end - 1)
+        for (int r = q + 1; r <= kSubCells; ++r) st[r] = end;
+}
+
+// First index with key >= k0 (k0 < 2^63), through the tables.
 __device__ __forceinline__ long long cell_lower(const unsigned long long* __restrict__ keys,
                                                 long long n, const CellTab& T,
                                                 unsigned long long k0) {
     const long long c = (long long)(k0 >> T.sh);
     const long long a = T.tab[c];
     if ((unsigned long long)c << T.sh == k0) return a;  // k0 starts a level-L cell
+    const int s = T.sub[c];
+    if (s >= 0) {
+        const int sh2 = T.sh - 3 * kSubLevels;
+        const int* st = T.subtab + (long long)s * (kSubCells + 1);
+        const int q = (int)((k0 >> sh2) & (kSubCells - 1));
+        const long long a2 = st[q];
+        if ((k0 >> sh2) << sh2 == k0) return a2;  // k0 starts a sub-cell
+        return a2 + lower_bound(keys + a2, st[q + 1] - a2, k0);
+    }
     const long long b = T.tab[c + 1];
     return a + lower_bound(keys + a, b - a, k0);
 }
@@ -346,7 +396,7 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn(const double* __restrict__ xs
 // nothing.
 // ----------------------------------------------------------------------------------
 constexpr int kBufSlots = 8;
-constexpr int kWinHalf = 128;  // W: curve window each side of the wave (swept: 64-512)
+constexpr int kWinHalf = 64;   // W: curve window each side of the wave (swept: 64-512; 64 since the sub-tables)
 constexpr int kCellFine = 1;   // verification cells >= half the ball radius (swept: 0-3)
 
 template <int K>
@@ -456,6 +506,8 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict
             ca[a] = max(0LL, quant(c3[a] - R, G.lo[a], G.scale) - 1) >> shift;
             cb[a] = min(kQMax, quant(c3[a] + R, G.lo[a], G.scale) + 1) >> shift;
         }
+        long long pj1 = 0;           // the last lookup's end index ...
+        unsigned long long pk1 = 1;  // ... and key (1: none yet -- no range ends there)
         for (long long cx = ca[0]; cx <= cb[0]; ++cx)
             for (long long cy = ca[1]; cy <= cb[1]; ++cy)
                 for (long long cz = ca[2]; cz <= cb[2]; ++cz) {
@@ -473,8 +525,12 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict
                     unsigned long long k0 = sh3 >= 63 ? 0ULL : p << sh3;
                     unsigned long long k1 = sh3 >= 63 ? ~0ULL : (p + 1) << sh3;  // exclusive
                     if (k0 >= klo && k1 <= khi) continue;  // inside the window already
-                    long long j0 = cell_lower(keys, n, CT, k0);
-                    long long j1 = sh3 >= 63 || (k1 >> 63) ? n : cell_lower(keys, n, CT, k1);
+                    // a cell adjacent in key order to the last one looked up (the z pairs
+                    // of a column, ...) starts where that one ended: one lookup instead of two
+                    const long long j0 = k0 == pk1 ? pj1 : cell_lower(keys, n, CT, k0);
+                    const long long j1 = sh3 >= 63 || (k1 >> 63) ? n : cell_lower(keys, n, CT, k1);
+                    pk1 = k1;
+                    pj1 = j1;
                     scan_range<K>(j0, min(j1, win0), xs, ys, zs, x, y, z, C.T);
                     scan_range<K>(max(j0, win1), j1, xs, ys, zs, x, y, z, C.T);
                 }
@@ -545,10 +601,25 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     ASP_TRY(ensure(ws.knn[7], (size_t)(ncell + 1) * sizeof(int)));
     int* tab = (int*)ws.knn[7].p;
     ASP_HIP(hipMemsetD32Async((hipDeviceptr_t)tab, (int)n, (size_t)(ncell + 1), st));
-    const CellTab CT{tab, 63 - 3 * L};
     hipLaunchKernelGGL(k_cell_table, dim3(grid), dim3(kKnnBlock), 0, st,
-                       (const unsigned long long*)kout, (long long)n, CT.sh, tab);
+                       (const unsigned long long*)kout, (long long)n, 63 - 3 * L, tab);
     ASP_LAUNCHED();
+    // sub-tables of the dense level-L cells: at most n / (kSubMin + 1) of them
+    const long long nslot_max = n / (kSubMin + 1) + 1;
+    ASP_TRY(ensure(ws.knn[8], (size_t)(ncell + 1) * sizeof(int)));
+    ASP_TRY(ensure(ws.knn[9], (size_t)nslot_max * (kSubCells + 1) * sizeof(int)));
+    int* sub = (int*)ws.knn[8].p;
+    int* nslot = sub + ncell;
+    int* subtab = (int*)ws.knn[9].p;
+    ASP_HIP(hipMemsetAsync(nslot, 0, sizeof(int), st));
+    hipLaunchKernelGGL(k_sub_slots, dim3((unsigned)((ncell + kKnnBlock - 1) / kKnnBlock)),
+                       dim3(kKnnBlock), 0, st, (const int*)tab, ncell, sub, nslot);
+    ASP_LAUNCHED();
+    hipLaunchKernelGGL(k_sub_table, dim3(grid), dim3(kKnnBlock), 0, st,
+                       (const unsigned long long*)kout, (long long)n, 63 - 3 * L,
+                       (const int*)tab, (const int*)sub, subtab);
+    ASP_LAUNCHED();
+    const CellTab CT{tab, sub, subtab, 63 - 3 * L};
     // diagnostics only: ASP_KNN_THREAD = one lane per particle throughout;
     // ASP_KNN_DIAG = 1: the window pass alone (wrong results, timing)
     const bool per_thread = getenv("ASP_KNN_THREAD") != nullptr;
