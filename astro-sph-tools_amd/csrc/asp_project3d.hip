@@ -55,7 +55,7 @@ constexpr int kMaxBricks = 16384;            // C1/C3 LDS: one int per brick (64
 static_assert(kMaxBricks <= kScanThreads * kScanPer, "k_tilescan holds <= kScanPer bricks per thread");
 constexpr int k3Block = 512;                 // count / scatter / deposit workgroup
 #ifndef ASP_CUBE_LANE_COLS
-#define ASP_CUBE_LANE_COLS 40
+#define ASP_CUBE_LANE_COLS 48
 #endif
 constexpr int kLaneCols = ASP_CUBE_LANE_COLS;  // boxes up to this many (i, j) columns:
                                                // lane-per-record, wider: a wave per record
@@ -85,6 +85,7 @@ struct Grid3 {
                              // multiple of kBX; the whole slab unless it has > kMaxBricks)
     int nbx, nby, nbz, nb;   // bricks over the output slab
     int lane_cols;           // deposit: boxes up to this many columns lane-per-record
+    int diag;                // timing diagnostic (ASP_CUBE_DIAG): 1 skip the wave class, 2 the lane classes
 };
 
 struct Box3 {
@@ -299,15 +300,21 @@ __device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, i
         const f2 sc2 = {sc, sc};
         double* col = acc + lds_at(li, lj, 0);
         f2 lk2 = {(float)a, (float)(a + 1)};
-        for (int lk = a; lk <= b; lk += 2) {  // planes lk, lk + 1 (the second may pass b)
-            const f2 dz = __builtin_elementwise_fma(lk2, npz, zr2);
+        auto planes2 = [&](f2 pl) {
+            const f2 dz = __builtin_elementwise_fma(pl, npz, zr2);
             const f2 r2 = __builtin_elementwise_fma(dz, dz, sf2);
             const f2 q = f2{__builtin_amdgcn_sqrtf(r2.x), __builtin_amdgcn_sqrtf(r2.y)} * hi2;
-            const f2 w = edge_shape2<KID>(q) * sc2;
+            return edge_shape2<KID>(q) * sc2;
+        };
+        // whole plane pairs without a per-pair branch, then the odd last plane
+        int lk = a;
+        for (; lk < b; lk += 2) {
+            const f2 w = planes2(lk2);
             atomicAdd(&col[lk], (double)w.x);
-            if (lk < b) atomicAdd(&col[lk + 1], (double)w.y);
+            atomicAdd(&col[lk + 1], (double)w.y);
             lk2 += (f2){2.0f, 2.0f};
         }
+        if (lk == b) atomicAdd(&col[lk], (double)planes2(lk2).x);
     }
 }
 
@@ -401,6 +408,7 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
                 if (bw > 0 && bh > 0 && bd > 0) {
                     const int cols = bw * bh, vol = cols * bd;
                     c = cols > g.lane_cols ? 0 : vol > kV1 ? 1 : vol > kV2 ? 2 : vol > kV3 ? 3 : 4;
+                    if ((g.diag == 1 && c == 0) || (g.diag == 2 && c > 0)) c = -1;
                 }
             }
             cr[q] = c < 0 ? 0xffffffffu : ((unsigned)c << 16) | (unsigned)atomicAdd(&qcnt[c], 1);
@@ -460,10 +468,19 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
             const bool live = i >= 0 && prep(q0, q1, R);
             const int bw = R.b.i1 - R.b.i0 + 1, bh = R.b.j1 - R.b.j0 + 1;
             if (cls > 0) {  // lane classes: lane-per-record
-                if (live)
-                    for (int li = R.b.i0; li <= R.b.i1; ++li)
-                        for (int lj = R.b.j0; lj <= R.b.j1; ++lj)
-                            column3<KID>(g, R, li, lj, K0, xt, yt, zt, acc);
+                // one flat loop over the box's columns: a wave runs max(bw * bh) column
+                // steps, where nested i / j loops ran about max(bw) * max(bh) over its lanes
+                if (live) {
+                    const int nc = bw * bh;
+                    int li = R.b.i0, lj = R.b.j0;
+                    for (int c = 0; c < nc; ++c) {
+                        column3<KID>(g, R, li, lj, K0, xt, yt, zt, acc);
+                        if (++lj > R.b.j1) {
+                            lj = R.b.j0;
+                            ++li;
+                        }
+                    }
+                }
             } else {
                 unsigned long long big = __ballot(live);
                 while (big) {
@@ -482,10 +499,18 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
                     Q.b.k0 = bcast(R.b.k0, l);
                     Q.b.k1 = bcast(R.b.k1, l);
                     int qw = bcast(bw, l), qh = bcast(bh, l);
-                    // lanes take the box's (i, j) columns
+                    // lanes take the box's (i, j) columns: column cc = ci * qh + cj, the
+                    // next one of a lane 64 further on (one division per record, not per column)
+                    const int di = 64 / qh, dj = 64 - di * qh;
+                    int ci = lane / qh, cj = lane - ci * qh;
                     for (int cc = lane; cc < qw * qh; cc += 64) {
-                        int ci = cc / qh, cj = cc - ci * qh;
                         column3<KID>(g, Q, Q.b.i0 + ci, Q.b.j0 + cj, K0, xt, yt, zt, acc);
+                        ci += di;
+                        cj += dj;
+                        if (cj >= qh) {
+                            cj -= qh;
+                            ++ci;
+                        }
                     }
                 }
             }
@@ -600,6 +625,7 @@ static bool make_grid3(const double* ext, int nx, int ny, int nz, int k_lo, int 
     g.nb = (long long)g.nby * g.nbz > kMaxBricks ? -1 : (int)std::min<long long>(nb, 0x7fffffff);
     g.lane_cols = kLaneCols;
     if (const char* e = getenv("ASP_CUBE_LANE_COLS")) g.lane_cols = std::max(0, atoi(e));
+    g.diag = getenv("ASP_CUBE_DIAG") ? atoi(getenv("ASP_CUBE_DIAG")) : 0;
 
     return true;
 }
