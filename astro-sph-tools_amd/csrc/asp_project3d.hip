@@ -41,12 +41,21 @@ constexpr int kBrickVox = kBX * kBY * kBZ;   // 8192 -> 64 KiB of fp64 accumulat
 #ifndef ASP_CUBE_PAD
 #define ASP_CUBE_PAD 1
 #endif
-// LDS accumulator rows padded to kBZP doubles: a 32-double (256-B) row stride puts the same
-// k of adjacent columns in the same LDS bank, and lanes walk adjacent columns
+#ifndef ASP_CUBE_PLANES
+#define ASP_CUBE_PLANES 1
+#endif
+// LDS accumulator layout.  Plane-major (ASP_CUBE_PLANES, default): voxel (i, j, k) at
+// k * 256 + i * 16 + j, so a plane is 256 doubles = 8 x 64 banks and a voxel's bank pair
+// depends on its column only -- the lanes of a wave walking adjacent columns from
+// different first planes never share a bank pair.  Column-major (0): rows of a column
+// padded to kBZP doubles (a 32-double row stride put the same k of adjacent columns in
+// one bank), the bank then shifting with each lane's first plane.
 constexpr int kBZP = kBZ + ASP_CUBE_PAD;
-constexpr int kBrickLds = kBX * kBY * kBZP;
+constexpr int kPlane = kBX * kBY;
+constexpr int kKStride = ASP_CUBE_PLANES ? kPlane : 1;  // LDS step from plane k to k + 1
+constexpr int kBrickLds = ASP_CUBE_PLANES ? kBZ * kPlane : kBX * kBY * kBZP;
 __device__ __forceinline__ int lds_at(int li, int lj, int lk) {
-    return (li * kBY + lj) * kBZP + lk;
+    return ASP_CUBE_PLANES ? lk * kPlane + li * kBY + lj : (li * kBY + lj) * kBZP + lk;
 }
 __device__ __forceinline__ int lds_vox(int v) {  // dense brick index -> padded LDS index
     return lds_at(v >> (kBYs + kBZs), (v >> kBZs) & (kBY - 1), v & (kBZ - 1));
@@ -310,11 +319,11 @@ __device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, i
         int lk = a;
         for (; lk < b; lk += 2) {
             const f2 w = planes2(lk2);
-            atomicAdd(&col[lk], (double)w.x);
-            atomicAdd(&col[lk + 1], (double)w.y);
+            atomicAdd(&col[lk * kKStride], (double)w.x);
+            atomicAdd(&col[(lk + 1) * kKStride], (double)w.y);
             lk2 += (f2){2.0f, 2.0f};
         }
-        if (lk == b) atomicAdd(&col[lk], (double)planes2(lk2).x);
+        if (lk == b) atomicAdd(&col[lk * kKStride], (double)planes2(lk2).x);
     }
 }
 
@@ -521,6 +530,27 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
             q1 = n1;
         }
         __syncthreads();  // the round's list is reused by the next round
+    }
+    if constexpr (ASP_CUBE_PLANES) {
+        // thread t: column c = t mod 256, planes [kh, kh + 16) -- conflict-free LDS reads
+        // (adjacent lanes, adjacent columns), 16 consecutive outputs per thread
+        static_assert(k3Block == 2 * kPlane && kBZ == 32, "two half-columns per thread pair");
+        const int c = (int)threadIdx.x & (kPlane - 1), kh = ((int)threadIdx.x / kPlane) * (kBZ / 2);
+        if (it.slab >= 0) {  // dense brick order (c * kBZ + k), as k3_merge reads it
+            double* dst = slabs + (long long)it.slab * kBrickVox + c * kBZ + kh;
+#pragma unroll
+            for (int q = 0; q < kBZ / 2; ++q) dst[q] = acc[(kh + q) * kPlane + c];
+            return;
+        }
+        const int li = c >> kBYs, lj = c & (kBY - 1);
+        if (li >= TW || lj >= TH) return;
+        float* o = out + ((long long)(I0 - g.i_lo + li) * g.ny + (J0 + lj)) * g.nzl + (K0 - g.k_lo) + kh;
+        const int nq = min(kBZ / 2, TD - kh);
+        for (int q = 0; q < nq; ++q) {
+            const float val = (float)acc[(kh + q) * kPlane + c];
+            o[q] = accumulate ? o[q] + val : val;
+        }
+        return;
     }
     if (it.slab >= 0) {
         double* dst = slabs + (long long)it.slab * kBrickVox;
