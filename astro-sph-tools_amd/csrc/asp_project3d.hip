@@ -229,6 +229,7 @@ struct Rec3 {
     float hinv, s;        // 1 / h, a * norm(h)
     float kc;             // brick-local plane coordinate of z, (z - z_min) / pz - K0
     float lx, ly;         // fl32(x - X[i0]), fl32(y - Y[j0]): offsets from the box's first column
+    float zr, thrf;       // fl32(z - Z[0]) (from the brick's first plane), fl32(thr)
     Box3 b;               // clipped to the brick, brick-local indices
 };
 
@@ -297,7 +298,7 @@ __device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, i
         const float dx = fmaf(-(float)(li - R.b.i0), (float)g.px, R.lx);
         const float dy = fmaf(-(float)(lj - R.b.j0), (float)g.py, R.ly);
         const float sf = fmaf(dx, dx, dy * dy);
-        const float thr = (float)R.thr;
+        const float thr = R.thrf;
         if (!(sf < thr * (1.0f + 0x1p-20f))) return;  // the column misses the sphere
         // the planes of q < 2 (W > 0): |dz| < sqrt(thr - s), widened well past the roundings
         float rz = __builtin_amdgcn_sqrtf(fmaxf(thr - sf, 0.0f) + thr * 0x1p-20f) * (float)g.ipz;
@@ -306,7 +307,7 @@ __device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, i
         const float fb = fminf(floorf(kc + rz), (float)R.b.k1);
         if (!(fa <= fb)) return;
         const int a = (int)fa, b = (int)fb;
-        const float zr = (float)(R.z - zt[0]);  // z relative to the brick's first plane
+        const float zr = R.zr;  // z relative to the brick's first plane
         const f2 zr2 = {zr, zr}, npz = {-(float)g.pz, -(float)g.pz}, sf2 = {sf, sf};
         const f2 hi2 = {hinv, hinv};
         const float sc = rs * kShapeScale<KID>;  // edge_shape2 returns f / kShapeScale
@@ -390,6 +391,8 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         const bool ok = R.b.i0 <= R.b.i1 && R.b.j0 <= R.b.j1 && R.b.k0 <= R.b.k1;
         R.lx = ok ? (float)(R.x - xt[R.b.i0]) : 0.0f;
         R.ly = ok ? (float)(R.y - yt[R.b.j0]) : 0.0f;
+        R.zr = (float)(R.z - zt[0]);
+        R.thrf = (float)R.thr;
         return ok;
     };
     // The item's records are taken in rounds of kRound.  Each round is first CLASSIFIED:
@@ -512,6 +515,8 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
                     Q.kc = bcast(R.kc, l);
                     Q.lx = bcast(R.lx, l);
                     Q.ly = bcast(R.ly, l);
+                    Q.zr = bcast(R.zr, l);
+                    Q.thrf = bcast(R.thrf, l);
                     Q.b.i0 = bcast(R.b.i0, l);
                     Q.b.j0 = bcast(R.b.j0, l);
                     Q.b.k0 = bcast(R.b.k0, l);
