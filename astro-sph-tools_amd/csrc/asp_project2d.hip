@@ -1893,7 +1893,12 @@ static int item_order_identity() {
     }();
     return identity;
 }
-static inline size_t item_cap(const Grid& g) { return (size_t)2 * g.ntiles + kTargetItems2d + kTargetItems1 + 16; }
+// deposit work items per map (ASP_ITEMS overrides kTargetItems2d; tuning only)
+static inline int item_target() {
+    static const int t = getenv("ASP_ITEMS") ? std::max(64, atoi(getenv("ASP_ITEMS"))) : kTargetItems2d;
+    return t;
+}
+static inline size_t item_cap(const Grid& g) { return (size_t)2 * g.ntiles + item_target() + kTargetItems1 + 16; }
 static inline size_t merge_cap(const Grid& g) { return (size_t)g.ntiles + 16; }
 
 static inline size_t scatter_lds(const Grid& g, int nout, bool det) {
@@ -2171,7 +2176,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
         hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
                            (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles, 2,
                            (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p, dc,
-                           (int*)ws.iorder.p, item_order_identity(), kTargetItems2d);
+                           (int*)ws.iorder.p, item_order_identity(), item_target());
         ASP_LAUNCHED();
         m.done();
     }

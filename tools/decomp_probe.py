@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--interference", action="store_true")
     ap.add_argument("--skip-decomp", action="store_true")
+    ap.add_argument("--stages", action="store_true", help="per-stage device times of each row share")
     ap.add_argument("--out")
     a = ap.parse_args()
     import torch
@@ -92,9 +93,19 @@ def main():
             a0 = (m * d["T"][keep]).contiguous()
             o0 = torch.empty((R[r + 1] - R[r], G), dtype=torch.float32, device=dev)
             o1 = torch.empty_like(o0)
-            ms = timed(lambda: project2d(u, v, h, a0, m, image_size=(G, G), extent=ext,
-                                         kernel="wendland_c2", ratio=True, out0=o0, out1=o1,
-                                         rows=(R[r], R[r + 1])), a.reps)
+            one = lambda: project2d(u, v, h, a0, m, image_size=(G, G), extent=ext,  # noqa: E731
+                                    kernel="wendland_c2", ratio=True, out0=o0, out1=o1,
+                                    rows=(R[r], R[r + 1]))
+            ms = timed(one, a.reps)
+            stages = None
+            if a.stages:  # device time per stage and call (HIP events, asp_profile)
+                from asp_amd import _lib
+                _lib.profile(0, True)
+                for _ in range(a.reps):
+                    one()
+                torch.cuda.synchronize()
+                stages = {k: round(t / a.reps, 4) for k, (t, n) in _lib.profile_read(0).items() if n}
+                _lib.profile(0, False)
             # the bench's N > 1 form: consecutive maps alternate two streams (and buffers)
             ss = [torch.cuda.Stream(device=dev) for _ in range(2)]
             ob = [(o0, o1), (torch.empty_like(o0), torch.empty_like(o1))]
@@ -107,7 +118,8 @@ def main():
                                   out1=ob[q % 2][1], rows=(R[r], R[r + 1]))
             ms2 = timed(two, a.reps) / 8
             rows.append({"rank": r, "rows": [R[r], R[r + 1]], "particles": int(keep.sum()),
-                         "ms": round(ms, 4), "ms_two_streams": round(ms2, 4)})
+                         "ms": round(ms, 4), "ms_two_streams": round(ms2, 4),
+                         **({"stages_ms": stages} if stages else {})})
             print("rows", rows[-1], flush=True)
             del u, v, h, m, a0, o0, o1
         shares["rows"] = rows
