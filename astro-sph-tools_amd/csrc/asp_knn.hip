@@ -229,10 +229,11 @@ __global__ __launch_bounds__(kKnnBlock) void k_cell_table(const unsigned long lo
 
 // Sub-table slots of the dense level-L cells (slot order does not matter).
 __global__ __launch_bounds__(kKnnBlock) void k_sub_slots(const int* __restrict__ tab, long long ncell,
-                                                          int* __restrict__ sub, int* __restrict__ nslot) {
+                                                          int submin, int* __restrict__ sub,
+                                                          int* __restrict__ nslot) {
     long long c = (long long)blockIdx.x * kKnnBlock + threadIdx.x;
     if (c >= ncell) return;
-    sub[c] = tab[c + 1] - tab[c] > kSubMin ? atomicAdd(nslot, 1) : -1;
+    sub[c] = tab[c + 1] - tab[c] > submin ? atomicAdd(nslot, 1) : -1;
 }
 
 // Per particle of a dense cell: the sub-cells starting at it (as k_cell_table), and the
@@ -605,7 +606,8 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
                        (const unsigned long long*)kout, (long long)n, 63 - 3 * L, tab);
     ASP_LAUNCHED();
     // sub-tables of the dense level-L cells: at most n / (kSubMin + 1) of them
-    const long long nslot_max = n / (kSubMin + 1) + 1;
+    const int submin = getenv("ASP_KNN_SUBMIN") ? std::max(8, atoi(getenv("ASP_KNN_SUBMIN"))) : kSubMin;
+    const long long nslot_max = n / (submin + 1) + 1;
     ASP_TRY(ensure(ws.knn[8], (size_t)(ncell + 1) * sizeof(int)));
     ASP_TRY(ensure(ws.knn[9], (size_t)nslot_max * (kSubCells + 1) * sizeof(int)));
     int* sub = (int*)ws.knn[8].p;
@@ -613,7 +615,7 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     int* subtab = (int*)ws.knn[9].p;
     ASP_HIP(hipMemsetAsync(nslot, 0, sizeof(int), st));
     hipLaunchKernelGGL(k_sub_slots, dim3((unsigned)((ncell + kKnnBlock - 1) / kKnnBlock)),
-                       dim3(kKnnBlock), 0, st, (const int*)tab, ncell, sub, nslot);
+                       dim3(kKnnBlock), 0, st, (const int*)tab, ncell, submin, sub, nslot);
     ASP_LAUNCHED();
     hipLaunchKernelGGL(k_sub_table, dim3(grid), dim3(kKnnBlock), 0, st,
                        (const unsigned long long*)kout, (long long)n, 63 - 3 * L,
