@@ -399,6 +399,7 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn(const double* __restrict__ xs
 constexpr int kBufSlots = 8;
 constexpr int kWinHalf = 64;   // W: curve window each side of the wave (swept: 64-512; 64 since the sub-tables)
 constexpr int kCellFine = 1;   // verification cells >= half the ball radius (swept: 0-3)
+constexpr int kWindowF32 = 1;  // the window pass with the fp32 prefilter (wave_scan32)
 
 template <int K>
 struct Cand {
@@ -468,6 +469,86 @@ __device__ __forceinline__ void scan_range(long long a, long long b, const doubl
     for (; j < b; ++j) T.insert(dist2(x, y, z, xs[j], ys[j], zs[j]));
 }
 
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// The window pass with an fp32 prefilter.  Entries go to LDS twice: fp64 (for the exact
+// distance) and fp32 relative to a wave origin O (lane 0's particle).  Every lane tests
+// every entry in fp32, d32 = ((dx dx + dy dy) + dz dz) from fl32(x - O) - fl32(e - O),
+// against a bound T that no pair with fp64 d < mx can exceed: with u = 2^-24 and M the
+// largest |coordinate - O| of the chunk and the wave's particles, each fp32 difference is
+// within 2.01 u M + 1.01 u |dx| of the exact one and the rounded sum within (1 + 5u), so
+// d32 <= (1 + 5u) (sqrt(mx) (1 + 1.01u) + 3.49 u M)^2 < T := (sqrt(mx) (1 + 2^-22) +
+// 2^-21 M)^2 (1 + 2^-21), rounded up to fp32.  Passing entries are buffered by LDS index
+// (8 per lane); a flush computes their exact fp64 distances (the reference's expression)
+// and inserts them -- lanes in step, so the fp64 work runs once per candidate, not once
+// per entry for every lane whenever any lane has a candidate.  The buffer is flushed
+// before the chunk's LDS is rewritten.  Results are the fp64 path's exactly (mx only
+// shrinks, so a bound from an earlier mx stays valid).
+template <int K>
+__device__ __forceinline__ void wave_scan32(long long a, long long b, const double* __restrict__ xs,
+                                            const double* __restrict__ ys,
+                                            const double* __restrict__ zs, double* lx, double* ly,
+                                            double* lz, float* fx, float* fy, float* fz, int lane,
+                                            double x, double y, double z, TopK<K>& T) {
+    const double ox = __shfl(x, 0, 64), oy = __shfl(y, 0, 64), oz = __shfl(z, 0, 64);
+    const double rx = x - ox, ry = y - oy, rz = z - oz;
+    const float qx = (float)rx, qy = (float)ry, qz = (float)rz;
+    const double mq = wave_max(fmax(fabs(rx), fmax(fabs(ry), fabs(rz))));
+    int ib[kBufSlots];
+    int cnt = 0;
+    for (long long c = a; c < b; c += 64) {
+        const int m = (int)min(64LL, b - c);
+        double me = 0.0;
+        if (lane < m) {
+            const double ex = xs[c + lane], ey = ys[c + lane], ez = zs[c + lane];
+            lx[lane] = ex;
+            ly[lane] = ey;
+            lz[lane] = ez;
+            const double dx = ex - ox, dy = ey - oy, dz = ez - oz;
+            fx[lane] = (float)dx;
+            fy[lane] = (float)dy;
+            fz[lane] = (float)dz;
+            me = fmax(fabs(dx), fmax(fabs(dy), fabs(dz)));
+        }
+        const double M = fmax(mq, wave_max(me));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        auto bound = [&]() -> float {
+            if (!(T.mx < INFINITY)) return INFINITY;
+            const double r = sqrt(T.mx) * (1.0 + 0x1p-22) + 0x1p-21 * M;
+            return (float)(r * r * (1.0 + 0x1p-21)) * (1.0f + 0x1p-22f);
+        };
+        auto flush = [&]() {
+#pragma unroll
+            for (int q = 0; q < kBufSlots; ++q)
+                if (q < cnt) T.insert(dist2(x, y, z, lx[ib[q]], ly[ib[q]], lz[ib[q]]));
+            cnt = 0;
+        };
+        float tb = bound();
+        for (int q = 0; q < m; ++q) {
+            const float dx = qx - fx[q], dy = qy - fy[q], dz = qz - fz[q];
+            const float d32 = (dx * dx + dy * dy) + dz * dz;
+            if (d32 <= tb) {
+#pragma unroll
+                for (int t = 0; t < kBufSlots; ++t)
+                    if (t == cnt) ib[t] = q;
+                ++cnt;
+            }
+            if (__builtin_amdgcn_ballot_w64(cnt == kBufSlots)) {
+                flush();
+                tb = bound();
+            }
+        }
+        flush();  // the chunk is rewritten next
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 template <int K>
 __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict__ xs,
                                                         const double* __restrict__ ys,
@@ -476,8 +557,10 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict
                                                         const int* __restrict__ idx, long long n,
                                                         int k, const KGrid* __restrict__ g,
                                                         double* __restrict__ h, int diag,
-                                                        int whalf, int fine, CellTab CT) {
+                                                        int whalf, int fine, CellTab CT,
+                                                        int f32) {
     __shared__ double sx[kKnnBlock / 64][64], sy[kKnnBlock / 64][64], sz[kKnnBlock / 64][64];
+    __shared__ float fx[kKnnBlock / 64][64], fy[kKnnBlock / 64][64], fz[kKnnBlock / 64][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long long base = ((long long)blockIdx.x * (kKnnBlock / 64) + wv) * 64;
     if (base >= n) return;  // wave-uniform
@@ -490,8 +573,13 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict
     C.T.init(k);
     C.cnt = 0;
     const long long win0 = max(0LL, base - whalf), win1 = min(n, base + 64 + whalf);
-    wave_scan<K>(win0, win1, xs, ys, zs, sx[wv], sy[wv], sz[wv], lane, x, y, z, C);
-    C.flush();
+    if (f32) {
+        wave_scan32<K>(win0, win1, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv], fy[wv], fz[wv], lane,
+                       x, y, z, C.T);
+    } else {
+        wave_scan<K>(win0, win1, xs, ys, zs, sx[wv], sy[wv], sz[wv], lane, x, y, z, C);
+        C.flush();
+    }
     if (act && n >= k && diag == 0) {
         // key span the window covers completely (open at the ends of the array)
         const unsigned long long klo = win0 == 0 ? 0ULL : keys[win0] + 1;
@@ -628,6 +716,7 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     const int diag = getenv("ASP_KNN_DIAG") ? atoi(getenv("ASP_KNN_DIAG")) : 0;
     const int whalf = getenv("ASP_KNN_WINDOW") ? atoi(getenv("ASP_KNN_WINDOW")) : kWinHalf;
     const int fine = getenv("ASP_KNN_FINE") ? atoi(getenv("ASP_KNN_FINE")) : kCellFine;
+    const int f32 = getenv("ASP_KNN_F32") ? atoi(getenv("ASP_KNN_F32")) : kWindowF32;
 #define ASP_KNN(KN)                                                                               \
     do {                                                                                          \
         if (per_thread)                                                                           \
@@ -640,7 +729,7 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
                                dim3(kKnnBlock), 0, st, (const double*)xs, (const double*)ys,      \
                                (const double*)zs, (const unsigned long long*)kout,                \
                                (const int*)iout, (long long)n, k, (const KGrid*)dg, dh, diag, whalf,  \
-                               fine, CT);    \
+                               fine, CT, f32);\
     } while (0)
     if (k <= 32)
         ASP_KNN(32);
