@@ -126,6 +126,36 @@ __device__ __forceinline__ bool footprint3(const Grid3& g, float x, float y, flo
            axis_cells(z, rad, g.z_min, g.ipz, g.k_lo, g.k_lo + g.nzl - 1, b.k0, b.k1);
 }
 
+// The deposit's box in fp32: the same superset with an fp32-sized margin (2^-20 relative
+// to the operand magnitudes in cells, plus 2^-10 cell; the fp32 roundings of the operands
+// and products stay below 2^-21 relative), about a third of the fp64 form's cost.  The
+// box only bounds the columns and planes walked -- every voxel in it is still tested
+// (fp64 for the indicator kernel, the edge form for the others) -- so any superset is
+// exact; count and scatter keep the fp64 box (which bricks a particle is binned to).
+struct Grid3f {
+    float x_min, y_min, z_min, ipx, ipy, ipz;
+};
+__device__ __forceinline__ bool axis_cells_f(float w, float rad, float w_min, float ip, int lo,
+                                             int hi, int& a, int& b) {
+    const float t0 = (w - rad - w_min) * ip, t1 = (w + rad - w_min) * ip;
+    const float d = (fabsf(w) + rad + fabsf(w_min)) * ip * 0x1p-20f + 0x1p-10f;
+    const float f0 = fmaxf(ceilf(t0 - d), (float)lo);
+    const float f1 = fminf(floorf(t1 + d), (float)hi);
+    if (!(f0 <= f1)) return false;
+    a = (int)f0;
+    b = (int)f1;
+    return true;
+}
+__device__ __forceinline__ bool footprint3f(const Grid3& g, const Grid3f& f, float x, float y,
+                                            float z, float h, Box3& b) {
+    const float rad = fabsf(2.0f * h);
+    if (!(rad > 0.0f) || !__builtin_isfinite(rad)) return false;
+    if (!__builtin_isfinite(x) || !__builtin_isfinite(y) || !__builtin_isfinite(z)) return false;
+    return axis_cells_f(x, rad, f.x_min, f.ipx, g.i_lo, g.i_lo + g.nxl - 1, b.i0, b.i1) &&
+           axis_cells_f(y, rad, f.y_min, f.ipy, 0, g.ny - 1, b.j0, b.j1) &&
+           axis_cells_f(z, rad, f.z_min, f.ipz, g.k_lo, g.k_lo + g.nzl - 1, b.k0, b.k1);
+}
+
 __device__ __forceinline__ void load3(const float* __restrict__ x, const float* __restrict__ y,
                                       const float* __restrict__ z, const float* __restrict__ h,
                                       long long p, long long p1, float& px, float& py, float& pz,
@@ -380,10 +410,12 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         zt[threadIdx.x - kBX - kBY] = g.z_min + (double)(K0 + (int)threadIdx.x - kBX - kBY) * g.pz;
     __syncthreads();
     const int lane = threadIdx.x & 63;
+    const Grid3f gf = {(float)g.x_min, (float)g.y_min, (float)g.z_min,
+                       (float)g.ipx, (float)g.ipy, (float)g.ipz};
     // A record's state for the walk: its box clipped to the brick (brick-local), the fp64
     // centre and threshold, 1/h, the term coefficient and the brick-local plane of z.
     auto prep = [&](const float4& q0, const float4& q1, Rec3& R) -> bool {
-        if (!footprint3(g, q0.x, q0.y, q0.z, q0.w, R.b)) return false;
+        if (!footprint3f(g, gf, q0.x, q0.y, q0.z, q0.w, R.b)) return false;
         R.b.i0 = max(R.b.i0, I0) - I0;
         R.b.i1 = min(R.b.i1, I0 + TW - 1) - I0;
         R.b.j0 = max(R.b.j0, J0) - J0;
@@ -430,7 +462,7 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
             const float4 q0 = recs[2 * (it.start + r0i + min(i, nr - 1))];
             Box3 b;
             int c = -1;
-            if (i < nr && footprint3(g, q0.x, q0.y, q0.z, q0.w, b)) {
+            if (i < nr && footprint3f(g, gf, q0.x, q0.y, q0.z, q0.w, b)) {
                 const int bw = min(b.i1, I0 + TW - 1) - max(b.i0, I0) + 1;
                 const int bh = min(b.j1, J0 + TH - 1) - max(b.j0, J0) + 1;
                 const int bd = min(b.k1, K0 + TD - 1) - max(b.k0, K0) + 1;
