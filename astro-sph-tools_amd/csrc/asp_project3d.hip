@@ -175,17 +175,21 @@ __global__ __launch_bounds__(k3Block) void k3_count(const float* __restrict__ x,
                                                     const float* __restrict__ z,
                                                     const float* __restrict__ h, long long n,
                                                     long long per_block, Grid3 g,
-                                                    int* __restrict__ hist) {
+                                                    int* __restrict__ hist, int inter) {
     extern __shared__ __attribute__((aligned(16))) int lh[];
     for (int t = threadIdx.x; t < g.nb; t += k3Block) lh[t] = 0;
     __syncthreads();
-    long long p0 = (long long)blockIdx.x * per_block;
-    long long p1 = min(n, p0 + per_block);
+    // inter: block b takes the k3Block-particle batches b, b + nblk, ... (the whole grid
+    // streams one window of the arrays at a time, as the 2-D count does); else one
+    // contiguous range per block
+    const long long stride = inter ? (long long)gridDim.x * k3Block : k3Block;
+    const long long p0 = inter ? (long long)blockIdx.x * k3Block : (long long)blockIdx.x * per_block;
+    const long long p1 = inter ? n : min(n, p0 + per_block);
     float cx, cy, cz, ch;
     load3(x, y, z, h, p0 + threadIdx.x, p1, cx, cy, cz, ch);
-    for (long long base = p0; base < p1; base += k3Block) {
+    for (long long base = p0; base < p1; base += stride) {
         float nx_, ny_, nz_, nh_;
-        load3(x, y, z, h, base + k3Block + threadIdx.x, p1, nx_, ny_, nz_, nh_);
+        load3(x, y, z, h, base + stride + threadIdx.x, p1, nx_, ny_, nz_, nh_);
         Box3 b;
         if (footprint3(g, cx, cy, cz, ch, b)) {
             int bi0 = (b.i0 - g.i_lo) >> kBXs, bi1 = (b.i1 - g.i_lo) >> kBXs;
@@ -214,19 +218,21 @@ __global__ __launch_bounds__(k3Block) void k3_scatter(
     const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
     const float* __restrict__ h, const float* __restrict__ a, long long n, long long per_block,
     Grid3 g, const int* __restrict__ hist, const long long* __restrict__ brick_start,
-    float4* __restrict__ recs) {
+    float4* __restrict__ recs, int inter) {
     extern __shared__ __attribute__((aligned(16))) int cur[];
     const int* row = hist + (long long)blockIdx.x * g.nb;
     for (int t = threadIdx.x; t < g.nb; t += k3Block) cur[t] = (int)brick_start[t] + row[t];
     __syncthreads();
-    long long p0 = (long long)blockIdx.x * per_block;
-    long long p1 = min(n, p0 + per_block);
+    // the count's batch assignment (k3_count)
+    const long long stride = inter ? (long long)gridDim.x * k3Block : k3Block;
+    const long long p0 = inter ? (long long)blockIdx.x * k3Block : (long long)blockIdx.x * per_block;
+    const long long p1 = inter ? n : min(n, p0 + per_block);
     float cx, cy, cz, ch, ca;
     load3(x, y, z, h, p0 + threadIdx.x, p1, cx, cy, cz, ch);
     ca = p0 + threadIdx.x < p1 ? a[p0 + threadIdx.x] : 0.0f;
-    for (long long base = p0; base < p1; base += k3Block) {
+    for (long long base = p0; base < p1; base += stride) {
         float nx_, ny_, nz_, nh_, na_;
-        long long q = base + k3Block + threadIdx.x;
+        long long q = base + stride + threadIdx.x;
         load3(x, y, z, h, q, p1, nx_, ny_, nz_, nh_);
         na_ = q < p1 ? a[q] : 0.0f;
         Box3 b;
@@ -727,6 +733,8 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
     int n_items = 0, n_merges = 0, n_slabs = 0;
     ASP_TRY(ensure_morton3(ws, g, st));
     long long nblk = std::min<long long>(512, std::max<long long>(1, (n + 8191) / 8192));
+    // batch-interleaved count / scatter (ASP_CUBE_INTERLEAVE=0: contiguous ranges per block)
+    static const int inter = getenv("ASP_CUBE_INTERLEAVE") ? atoi(getenv("ASP_CUBE_INTERLEAVE")) : 1;
     long long per_block = (n + nblk - 1) / nblk;
     nblk = (n + per_block - 1) / per_block;
     ASP_TRY(ensure(ws.hist, (size_t)nblk * g.nb * sizeof(int)));
@@ -742,7 +750,7 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
     {
         StageMark m(ws, kS3Count, st);
         hipLaunchKernelGGL(k3_count, dim3((unsigned)nblk), dim3(k3Block), lds_bins, st, dx, dy,
-                           dz, dh, n, per_block, g, (int*)ws.hist.p);
+                           dz, dh, n, per_block, g, (int*)ws.hist.p, inter);
         ASP_LAUNCHED();
         m.done();
     }
@@ -785,7 +793,7 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
         hipLaunchKernelGGL(probe ? k3_scatter<1> : k3_scatter<0>, dim3((unsigned)nblk),
                            dim3(k3Block), lds_bins, st, dx,
                            dy, dz, dh, da, n, per_block, g, (const int*)ws.hist.p,
-                           (const long long*)ws.tile_start.p, (float4*)ws.recs.p);
+                           (const long long*)ws.tile_start.p, (float4*)ws.recs.p, inter);
         ASP_LAUNCHED();
         m.done();
         return ASP_OK;
