@@ -91,3 +91,24 @@ def test_knn_device_tensor_and_large(gpu):
     assert h.is_cuda
     want = KDTree(pos).query(pos, k=32, workers=-1)[0][:, 31]
     assert np.array_equal(bits(h.cpu().numpy()), bits(want))
+
+
+@pytest.mark.gpu
+def test_knn_fp32_window_prefilter_far_coordinates(gpu, monkeypatch):
+    """The window pass's fp32 prefilter (asp_knn.hip wave_scan32) takes coordinates
+    relative to each wave's first particle; its bound grows with the largest such offset.
+    Clusters far from the origin (|x| ~ 1e6, separations ~1e-3) and a few remote outliers
+    (1e9) stress that bound: the result must stay bit-identical to scipy and to the fp64
+    window (ASP_KNN_F32=0)."""
+    from asp_amd.knn import knn_smoothing_lengths
+    rng = np.random.default_rng(7)
+    pos = np.concatenate([rng.uniform(0.0, 1.0, (40_000, 3)) + np.array([1e6, -2e6, 5e5]),
+                          rng.standard_normal((20_000, 3)) * 1e-3 + np.array([1e6, -2e6, 5e5]),
+                          rng.uniform(-1e9, 1e9, (50, 3))])
+    rng.shuffle(pos)
+    want = scipy_h(pos, 32)
+    h32 = knn_smoothing_lengths(pos, 32)
+    monkeypatch.setenv("ASP_KNN_F32", "0")
+    h64 = knn_smoothing_lengths(pos, 32)
+    assert np.array_equal(bits(h32), bits(want))
+    assert np.array_equal(bits(h64), bits(want))
