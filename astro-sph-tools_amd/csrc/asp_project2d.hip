@@ -750,10 +750,25 @@ __device__ __forceinline__ f2v sqrt2(f2v x) {
 // common case: the nine fp32 r2 and kernel values are computed branch-free in packed
 // fp32, and every pair with r2 < (2h)^2 is added.  Valid only when no pair lies in the
 // error band (min |r2 - thr| > band): returns false for such a record WITHOUT touching the
-// tile; the caller defers it to the exact path (small_box).
+// tile; the caller defers it to the exact path (small_box).  The three corner offsets per
+// axis come from registers (Corner3: the corner tables' first entries, the same fp32
+// values), not LDS: a table read here made every batch wait (lgkmcnt) for the previous
+// batch's LDS atomics, which complete in order ahead of it.
+struct Corner3 {
+    float x[3], y[3];
+};
+__device__ __forceinline__ Corner3 corner3(const Grid& g) {  // = xt[0..2], yt[0..2]
+    Corner3 c;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        c.x[k] = (float)((double)k * g.psx);
+        c.y[k] = (float)((double)k * g.psy_pix);
+    }
+    return c;
+}
 template <int KID, int NOUT, int ACC>
 __device__ __forceinline__ bool small3_fast(const Prep& P, int bw, int bh, int X0, int Y0,
-                                            const float* xt, const float* yt,
+                                            const Corner3& cc,
                                             unsigned long long* acc0, unsigned long long* acc1) {
     constexpr float kFar = 1e18f;  // outside the box: r2 ~ 1e36, far from any threshold
     float dx2[3];
@@ -761,14 +776,14 @@ __device__ __forceinline__ bool small3_fast(const Prep& P, int bw, int bh, int X
     float dyc2;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        float d = P.u - xt[min(i, bw - 1)];
+        float d = P.u - cc.x[i];
         d = i < bw ? d : kFar;
         dx2[i] = d * d;
     }
     {
-        float d0 = P.v - yt[0];
-        float d1 = P.v - yt[min(1, bh - 1)];
-        float d2 = P.v - yt[min(2, bh - 1)];
+        float d0 = P.v - cc.y[0];
+        float d1 = P.v - cc.y[1];
+        float d2 = P.v - cc.y[2];
         d1 = bh > 1 ? d1 : kFar;
         d2 = bh > 2 ? d2 : kFar;
         f2v d = f2v{d0, d1};
@@ -1226,6 +1241,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
     const int2 kk = ACC == kAccFix ? tile_k[it.tile] : make_int2(0, 0);
     tile_prologue<NOUT, kDepBlock>(g, X0, Y0, acc, xt, yt);
     const int lane = threadIdx.x & 63;
+    const Corner3 c3 = corner3(g);
     int* dlist = defer_lds[threadIdx.x >> 6];
     int ndef = 0;  // wave-uniform
     // One batch: record i (index within the item; r0, r1 its halves) of every thread.
@@ -1246,7 +1262,7 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
             // body; 4-wide boxes and records with a pair in the error band are deferred to
             // the exact body, a full wave of them at a time
             if (bw <= 3 && bh <= 3)
-                amb = !small3_fast<KID, NOUT, ACC>(P, bw, bh, X0, Y0, xt, yt, acc0, acc1);
+                amb = !small3_fast<KID, NOUT, ACC>(P, bw, bh, X0, Y0, c3, acc0, acc1);
             else
                 amb = true;
         }
