@@ -417,9 +417,11 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         R.s = (float)term_coef<KID>(q1.x, q0.w);
         R.kc = (float)((R.z - g.z_min) * g.ipz - (double)K0);
         const bool ok = R.b.i0 <= R.b.i1 && R.b.j0 <= R.b.j1 && R.b.k0 <= R.b.k1;
-        R.lx = ok ? (float)(R.x - xt[R.b.i0]) : 0.0f;
-        R.ly = ok ? (float)(R.y - yt[R.b.j0]) : 0.0f;
-        R.zr = (float)(R.z - zt[0]);
+        // the corner coordinates by the tables' own fp64 expressions (identical values): an
+        // LDS table read here would wait (lgkmcnt) behind the wave's in-flight atomics
+        R.lx = ok ? (float)(R.x - (g.x_min + (double)(I0 + R.b.i0) * g.px)) : 0.0f;
+        R.ly = ok ? (float)(R.y - (g.y_min + (double)(J0 + R.b.j0) * g.py)) : 0.0f;
+        R.zr = (float)(R.z - (g.z_min + (double)K0 * g.pz));
         R.thrf = (float)R.thr;
         return ok;
     };
