@@ -46,7 +46,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=100_000_000)
+    # (--particles: the same; under torch.distributed.run "--n" is ambiguous with its own
+    # options and is rejected before bench.py sees it)
+    ap.add_argument("--n", "--particles", dest="n", type=int, default=100_000_000)
     ap.add_argument("--grid", type=int, default=4096)
     ap.add_argument("--h-law", default="pixel", choices=["pixel", "physical"])
     ap.add_argument("--kernel", default="wendland_c2", choices=["wendland_c2", "cubic"])
