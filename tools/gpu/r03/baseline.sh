@@ -17,6 +17,6 @@ timeout -k 10 300 python bench.py --cpu-baseline off --n 10000000 --grid 2048 --
 python -c "import json;d=json.load(open('$o/bench_cfg2_physical.json'));print(d['ms_per_step'], json.dumps(d['roofline']))"
 if [ -z "$TAG" ]; then
 step microbench lds
-hipcc -O3 --offload-arch=gfx950 -munsafe-fp-atomics -o /tmp/mb_lds tools/microbench_lds.hip && timeout -k 10 120 /tmp/mb_lds > $o/microbench_lds.txt 2>&1; cat $o/microbench_lds.txt
+hipcc -O3 --offload-arch=gfx950 -munsafe-fp-atomics -o /tmp/mb_lds tools/microbench/lds.hip && timeout -k 10 120 /tmp/mb_lds > $o/microbench_lds.txt 2>&1; cat $o/microbench_lds.txt
 fi
 step done

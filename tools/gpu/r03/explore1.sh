@@ -8,5 +8,5 @@ mkdir -p $o
 VARIANTS="order pairs order pairs" bash tools/gpu/r03/ab_map.sh || exit 1
 hipcc -O3 --offload-arch=gfx950 -o /tmp/mb_pairs tools/microbench/pairs.hip || exit 2
 timeout -k 10 120 /tmp/mb_pairs > $o/mb_pairs.txt 2>&1; rc=$?; cat $o/mb_pairs.txt; [ $rc -eq 0 ] || exit $rc
-hipcc -O3 --offload-arch=gfx950 -munsafe-fp-atomics -o /tmp/mb_lds tools/microbench_lds.hip || exit 3
+hipcc -O3 --offload-arch=gfx950 -munsafe-fp-atomics -o /tmp/mb_lds tools/microbench/lds.hip || exit 3
 timeout -k 10 120 /tmp/mb_lds > $o/mb_lds.txt 2>&1; rc=$?; cat $o/mb_lds.txt; exit $rc

@@ -10,7 +10,7 @@
 //   G32h  as G32, tiles drawn from a Plummer-like concentrated distribution
 //   C32   coalesced stores (floor)
 // Build & run:
-//   hipcc -O3 --offload-arch=gfx950 -o tools/mb_group tools/microbench_group.hip && ./tools/mb_group
+//   hipcc -O3 --offload-arch=gfx950 -o tools/mb_group tools/microbench/group.hip && ./tools/mb_group
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

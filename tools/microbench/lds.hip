@@ -1,6 +1,6 @@
 // Microbenchmark: LDS accumulation primitives on gfx950 (random addresses in a 64x64x2
 // fp32 tile, the deposit kernel's access pattern).  Build & run:
-//   hipcc -O3 --offload-arch=gfx950 -o /tmp/mb tools/microbench_lds.hip && /tmp/mb
+//   hipcc -O3 --offload-arch=gfx950 -o /tmp/mb tools/microbench/lds.hip && /tmp/mb
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

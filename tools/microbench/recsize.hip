@@ -9,7 +9,7 @@
 //   S128  128-B records (one full line), eight lanes per record
 //   C32   32-B records to coalesced slots (reference)
 // Every store is bounds-checked against the allocation.  Build & run:
-//   hipcc -O3 --offload-arch=gfx950 -o tools/mb_recsize tools/microbench_recsize.hip
+//   hipcc -O3 --offload-arch=gfx950 -o tools/mb_recsize tools/microbench/recsize.hip
 //   ./tools/mb_recsize
 #include <hip/hip_runtime.h>
 #include <cstdio>

@@ -3,7 +3,7 @@
 // (workgroup, tile) pair owns a contiguous run (the production layout), and records arrive
 // in pseudo-random tile order.  Measures how the store cost depends on K (open lines per
 // workgroup) and on the record layout.  Build & run:
-//   hipcc -O3 --offload-arch=gfx950 -o /tmp/mbs tools/microbench_scatter.hip && /tmp/mbs
+//   hipcc -O3 --offload-arch=gfx950 -o /tmp/mbs tools/microbench/scatter.hip && /tmp/mbs
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

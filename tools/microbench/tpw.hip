@@ -4,7 +4,7 @@
 // writes only to the TPW tiles of its tile group (b / 8) % (4096 / TPW) -- the groups
 // are spread so that the 32 workgroups of one XCD (b % 8 equal) cover all groups.
 // Open record lines per XCD = 32 x TPW.
-//   hipcc -O3 --offload-arch=gfx950 -o tools/mb_tpw tools/microbench_tpw.hip && ./tools/mb_tpw
+//   hipcc -O3 --offload-arch=gfx950 -o tools/mb_tpw tools/microbench/tpw.hip && ./tools/mb_tpw
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
