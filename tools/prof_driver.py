@@ -21,10 +21,30 @@ def main():
     ap.add_argument("--map", default="weighted")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--deterministic", action="store_true")
+    ap.add_argument("--workload", default="map", choices=["map", "cube", "knn"],
+                    help="cube: --n particles (physical h) -> 512^3 (bench --workload cube); "
+                         "knn: k = 32 smoothing lengths of --n particles")
     a = ap.parse_args()
     import torch
     from asp_amd.device import project2d, stats
     from asp_amd.plummer import plummer_torch
+    if a.workload == "cube":
+        from asp_amd.device import project3d
+        d = plummer_torch(a.n, seed=0, h_law="physical", extent=4.0, grid=512, device="cuda:0")
+        out = torch.empty((512, 512, 512), device="cuda:0")
+        for _ in range(a.iters):
+            project3d(d["x"], d["y"], d["z"], d["h"], d["m"], cube_size=(512, 512, 512),
+                      extent=(-4.0, 4.0) * 3, kernel=a.kernel, planes=(0, 512), out=out)
+        torch.cuda.synchronize()
+        return
+    if a.workload == "knn":
+        from asp_amd.knn import knn_smoothing_lengths
+        d = plummer_torch(a.n, seed=0, h_law="pixel", extent=4.0, grid=64, device="cuda:0")
+        pos = torch.stack([d["x"], d["y"], d["z"]], dim=1).double().contiguous()
+        for _ in range(a.iters):
+            knn_smoothing_lengths(pos, 32)
+        torch.cuda.synchronize()
+        return
     G = a.grid
     d = plummer_torch(a.n, seed=0, h_law=a.h_law, extent=4.0, grid=G, device="cuda:0")
     u, v, h = d["x"], d["y"], d["h"]
