@@ -109,6 +109,22 @@ def test_create_image_argument_errors(asp):
     assert img.shape == (4, 5) and img.dtype == np.float64 and not img.any()
 
 
+def test_create_images_argument_errors(asp):
+    """create_images (several maps from one binning): the property count and each array's
+    length are checked before the device is touched, and the no-GPU shortcuts of
+    create_image (negative chunk size -> zero maps) hold per map."""
+    from asp_amd.tools.projections import create_images
+    pos, h = np.zeros((3, 3)), np.ones(3)
+    with pytest.raises(ValueError):
+        create_images(pos, h, [], (4, 4), 4, 2, -1, 1, -1, 1)
+    with pytest.raises(ValueError):
+        create_images(pos, h, [np.ones(3)] * 7, (4, 4), 4, 2, -1, 1, -1, 1)
+    with pytest.raises(ValueError):
+        create_images(pos, h, [np.ones(3), np.ones(2)], (4, 4), 4, 2, -1, 1, -1, 1)
+    maps = create_images(pos, h, [np.ones(3), np.ones(3)], (4, 5), -2, 2, -1, 1, -1, 1)
+    assert len(maps) == 2 and all(m.shape == (4, 5) and not m.any() for m in maps)
+
+
 def test_plummer_laws():
     from asp_amd.plummer import plummer
     p = plummer(20000, seed=0, h_law="physical")
