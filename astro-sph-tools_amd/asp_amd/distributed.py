@@ -153,6 +153,8 @@ def project2d_sharded(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
     import torch.distributed as dist
     if ratio and a1 is None:
         raise ValueError("ratio needs a1")
+    if ratio and deterministic:
+        raise ValueError("ratio=True cannot use the deterministic fixed point (DESIGN.md §4)")
     if op not in ("reduce", "allreduce", "reduce_scatter", "reduce_scatter_gather"):
         raise ValueError(f"unknown op {op!r}")
     if op == "reduce_scatter_gather" and a1 is not None and not ratio:
@@ -337,34 +339,47 @@ def project3d_sharded(x, y, z, h, a, *, cube_size, extent, kernel="cubic",
 # its rows (asp_project2d_rows: fewer tiles binned per rank, no grid reduction at all).
 # ---------------------------------------------------------------------------------------
 def row_slabs(nx: int, world_size: int, u=None, u_extent=None, weights=None,
-              sample: int = 1 << 22, seed: int = 0):
+              sample: int = 1 << 22, seed: int = 0, group=None):
     """Row bounds R (world_size + 1 ints, R[0] = 0, R[-1] = nx, strictly increasing).
     Without ``u`` the rows are split evenly; with the particles' ``u`` (device or host
     tensor) and ``u_extent`` = (u_min, u_max) the split equalises the particle count -- or
-    the summed ``weights`` -- per slab, at one-row granularity (a random subsample of 2^22
-    decides; asp_project2d_rows takes any row range)."""
+    the summed ``weights`` -- per slab, at one-row granularity (a random subsample of up to
+    2^22 decides; asp_project2d_rows takes any row range).  With ``group`` (an initialised
+    process group) every rank passes ITS particles: the per-row histograms of all ranks'
+    samples are summed (one all-reduce of nx words), so the bounds balance the union of
+    the ranks' particles however the reader split them, and every rank gets the same R."""
     import torch
     W = int(world_size)
     if W <= 1:
         return [0, nx]
     if nx < W:
         raise ValueError(f"{nx} rows cannot make {W} row slabs")
-    if u is None or u.shape[0] == 0:
+    if u is None or (u.shape[0] == 0 and group is None):
         inner = [(nx * r) // W for r in range(1, W)]
     else:
         lo, hi = (float(e) for e in u_extent)
-        g = torch.Generator(device=u.device)
-        g.manual_seed(seed)
-        k = min(u.shape[0], sample)
-        idx = torch.randint(0, u.shape[0], (k,), generator=g, device=u.device)
-        row = ((u[idx].double() - lo) / ((hi - lo) / nx)).floor().clamp(0, nx - 1).long()
-        w = torch.ones(k, dtype=torch.float64, device=u.device) if weights is None \
-            else weights[idx].double()
-        per = torch.zeros(nx, dtype=torch.float64, device=u.device).index_add_(0, row, w)
+        per = torch.zeros(nx, dtype=torch.float64, device=u.device)
+        if u.shape[0] > 0:
+            g = torch.Generator(device=u.device)
+            g.manual_seed(seed)
+            k = min(u.shape[0], sample)
+            idx = torch.randint(0, u.shape[0], (k,), generator=g, device=u.device)
+            row = ((u[idx].double() - lo) / ((hi - lo) / nx)).floor().clamp(0, nx - 1).long()
+            w = torch.ones(k, dtype=torch.float64, device=u.device) if weights is None \
+                else weights[idx].double()
+            # a rank's sample stands for all of its particles
+            per.index_add_(0, row, w * (u.shape[0] / k))
+        if group is not None:
+            import torch.distributed as dist
+            dist.all_reduce(per, op=dist.ReduceOp.SUM, group=group)
         c = torch.cumsum(per, 0)
         tot = float(c[-1])
-        t = torch.tensor([tot * r / W for r in range(1, W)], dtype=torch.float64, device=c.device)
-        inner = [int(j) + 1 for j in torch.searchsorted(c, t).tolist()]
+        if not tot > 0:
+            inner = [(nx * r) // W for r in range(1, W)]
+        else:
+            t = torch.tensor([tot * r / W for r in range(1, W)], dtype=torch.float64,
+                             device=c.device)
+            inner = [int(j) + 1 for j in torch.searchsorted(c, t).tolist()]
     R = [0]  # strictly increasing: bound i in [i, nx - W + i]
     for i, b in enumerate(inner, start=1):
         R.append(min(max(b, R[-1] + 1), nx - W + i))
@@ -439,19 +454,22 @@ def project2d_rowslab(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
     import torch.distributed as dist
     if ratio and a1 is None:
         raise ValueError("ratio needs a1")
+    if ratio and deterministic:
+        raise ValueError("ratio=True cannot use the deterministic fixed point (DESIGN.md §4)")
     if gather not in ("none", "all", "dst"):
         raise ValueError(f"unknown gather {gather!r}")
+    if gather != "none" and a1 is not None and not ratio:
+        # one map is gathered: two component maps would need two gathers
+        raise ValueError(f"gather={gather!r} gathers ONE map: with a1 it needs ratio=True")
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     nx, ny = int(image_size[0]), int(image_size[1])
     if bounds is None:
-        if world > 1:  # every rank must agree: balance on rank 0's sample, broadcast
-            R = torch.tensor(row_slabs(nx, world, u, extent[:2]), dtype=torch.int64,
-                             device=u.device)
-            dist.broadcast(R, src=0, group=group)
-            bounds = R.tolist()
-        else:
-            bounds = [0, nx]
+        # every rank must agree: the row histogram of ALL ranks' particles (one
+        # all-reduce), not one rank's sample -- a spatial reader split skews any one rank
+        bounds = row_slabs(nx, world, u, extent[:2],
+                           group=group if group is not None else dist.group.WORLD) \
+            if world > 1 else [0, nx]
     if len(bounds) != world + 1 or bounds[0] != 0 or bounds[-1] != nx:
         raise ValueError(f"bounds must be {world + 1} row edges from 0 to nx, got {bounds}")
     if world > 1 and exchange:
@@ -467,12 +485,15 @@ def project2d_rowslab(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: i
     if gather == "none" or world == 1:
         return o0, o1
     if gather == "dst":
+        # P2POp peers are GLOBAL ranks; dst and r are ranks of `group`
+        peer = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
         if rank != dst:
-            dist.batch_isend_irecv([dist.P2POp(dist.isend, o0.contiguous(), dst, group)])[0].wait()
+            dist.batch_isend_irecv([dist.P2POp(dist.isend, o0.contiguous(), peer(dst),
+                                               group)])[0].wait()
             return o0, None
         full = torch.empty((nx, ny), dtype=o0.dtype, device=o0.device)
         full[r0:r1] = o0
-        ops = [dist.P2POp(dist.irecv, full[bounds[r]:bounds[r + 1]], r, group)
+        ops = [dist.P2POp(dist.irecv, full[bounds[r]:bounds[r + 1]], peer(r), group)
                for r in range(world) if r != dst]
         for w in dist.batch_isend_irecv(ops):
             w.wait()

@@ -129,6 +129,13 @@ def create_weighted_image(positions, smoothing_lengths, weights, values, image_s
     """
     cs = _check_chunk_size(chunk_size)
     kid = kernel_id_of(kernel_func)
+    if deterministic and kid is not None:
+        # the native deterministic mode is an int64 fixed point per tile: a ratio of two
+        # such maps is imprecise where only kernel tails reach; the plug-in
+        # path's deterministic mode (fp64 sums in particle order) has no such limit
+        raise ValueError("deterministic=True cannot form a weighted (ratio) map with a native "
+                         "kernel: use deterministic=False, or pass the kernel as a plain "
+                         "Python callable (the kernel_func plug-in sums in fp64, in order)")
     _lengths(positions, smoothing_lengths, weights)
     w = np.asarray(weights, dtype=np.float64).reshape(-1)
     vals = np.asarray(values, dtype=np.float64).reshape(-1)

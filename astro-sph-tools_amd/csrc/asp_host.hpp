@@ -34,7 +34,7 @@ struct Buf {
     size_t cap = 0;
 };
 
-constexpr int kStages = 17;
+constexpr int kStages = 19;
 constexpr int kNStats = 13;  // asp_last_stats
 constexpr int kMarks = 8;  // launches of one stage timed per call
 enum Stage {
@@ -42,7 +42,8 @@ enum Stage {
     kSWide, kSRatio,
     // 3-D cube (asp_project3d)
     kS3Count = 10, kS3Colscan, kS3Tilescan, kS3Scatter, kS3Deposit, kS3Merge,
-    kSGather = 16  // 2-D gathered deposit of the large-record stream
+    kSGather = 16,  // 2-D gathered deposit of the large-record stream
+    kSKnnPrep = 17, kSKnnSearch = 18  // k-NN: keys / sort / tables; the search kernel
 };
 
 struct Workspace {

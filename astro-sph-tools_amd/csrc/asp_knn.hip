@@ -558,7 +558,7 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict
                                                         int k, const KGrid* __restrict__ g,
                                                         double* __restrict__ h, int diag,
                                                         int whalf, int fine, CellTab CT,
-                                                        int f32) {
+                                                        int f32, unsigned long long* evc) {
     __shared__ double sx[kKnnBlock / 64][64], sy[kKnnBlock / 64][64], sz[kKnnBlock / 64][64];
     __shared__ float fx[kKnnBlock / 64][64], fy[kKnnBlock / 64][64], fz[kKnnBlock / 64][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -597,6 +597,7 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict
         }
         long long pj1 = 0;           // the last lookup's end index ...
         unsigned long long pk1 = 1;  // ... and key (1: none yet -- no range ends there)
+        long long nscan = 0;         // ASP_KNN_COUNT: fp64 distances of the cell scans
         for (long long cx = ca[0]; cx <= cb[0]; ++cx)
             for (long long cy = ca[1]; cy <= cb[1]; ++cy)
                 for (long long cz = ca[2]; cz <= cb[2]; ++cz) {
@@ -622,7 +623,12 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict
                     pj1 = j1;
                     scan_range<K>(j0, min(j1, win0), xs, ys, zs, x, y, z, C.T);
                     scan_range<K>(max(j0, win1), j1, xs, ys, zs, x, y, z, C.T);
+                    if (evc) nscan += max(0LL, min(j1, win0) - j0) + max(0LL, j1 - max(j0, win1));
                 }
+        if (evc) {  // diagnostic: distances evaluated (window pass, cell scans)
+            atomicAdd(&evc[0], (unsigned long long)(win1 - win0));
+            atomicAdd(&evc[1], (unsigned long long)nscan);
+        }
     }
     if (act) h[idx[i]] = sqrt(C.T.mx);
 }
@@ -667,6 +673,8 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     double *ys = xs + n, *zs = ys + n;
     const unsigned nb = (unsigned)std::min<long long>(kRedBlocks, (n + kKnnBlock - 1) / kKnnBlock);
     const unsigned grid = (unsigned)((n + kKnnBlock - 1) / kKnnBlock);
+    if (ws.prof) ASP_TRY(prof_next(ws));
+    StageMark mprep(ws, kSKnnPrep, st);  // bounding box, keys, sort, gather, cell tables
     hipLaunchKernelGGL(k_bbox, dim3(nb), dim3(kKnnBlock), 0, st, dpos, (long long)n, part);
     ASP_LAUNCHED();
     hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(kKnnBlock), 0, st, (const double*)part, (int)nb, dg);
@@ -710,6 +718,7 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
                        (const int*)tab, (const int*)sub, subtab);
     ASP_LAUNCHED();
     const CellTab CT{tab, sub, subtab, 63 - 3 * L};
+    mprep.done();
     // diagnostics only: ASP_KNN_THREAD = one lane per particle throughout;
     // ASP_KNN_DIAG = 1: the window pass alone (wrong results, timing)
     const bool per_thread = getenv("ASP_KNN_THREAD") != nullptr;
@@ -717,6 +726,15 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     const int whalf = getenv("ASP_KNN_WINDOW") ? atoi(getenv("ASP_KNN_WINDOW")) : kWinHalf;
     const int fine = getenv("ASP_KNN_FINE") ? atoi(getenv("ASP_KNN_FINE")) : kCellFine;
     const int f32 = getenv("ASP_KNN_F32") ? atoi(getenv("ASP_KNN_F32")) : kWindowF32;
+    // ASP_KNN_COUNT: count the distances the search evaluates (bench.py's k-NN roofline;
+    // one atomic per lane, so off in timed runs) -> asp_last_stats [9] window, [10] cells
+    unsigned long long* evc = nullptr;
+    if (getenv("ASP_KNN_COUNT")) {
+        ASP_TRY(ensure(ws.knn[10], 2 * sizeof(unsigned long long)));
+        evc = (unsigned long long*)ws.knn[10].p;
+        ASP_HIP(hipMemsetAsync(evc, 0, 2 * sizeof(unsigned long long), st));
+    }
+    StageMark msearch(ws, kSKnnSearch, st);
 #define ASP_KNN(KN)                                                                               \
     do {                                                                                          \
         if (per_thread)                                                                           \
@@ -729,7 +747,7 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
                                dim3(kKnnBlock), 0, st, (const double*)xs, (const double*)ys,      \
                                (const double*)zs, (const unsigned long long*)kout,                \
                                (const int*)iout, (long long)n, k, (const KGrid*)dg, dh, diag, whalf,  \
-                               fine, CT, f32);\
+                               fine, CT, f32, evc);\
     } while (0)
     if (k <= 32)
         ASP_KNN(32);
@@ -737,6 +755,15 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
         ASP_KNN(64);
 #undef ASP_KNN
     ASP_LAUNCHED();
+    msearch.done();
+    for (int j = 9; j <= 12; ++j) ws.stats[j] = 0;
+    if (evc) {
+        unsigned long long e[2];
+        ASP_HIP(hipMemcpyAsync(e, evc, sizeof(e), hipMemcpyDeviceToHost, st));
+        ASP_HIP(hipStreamSynchronize(st));
+        ws.stats[9] = (long long)e[0];
+        ws.stats[10] = (long long)e[1];
+    }
     if (!dev) {
         ASP_HIP(hipMemcpyAsync(h, dh, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st));
         ASP_HIP(hipStreamSynchronize(st));

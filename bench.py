@@ -5,8 +5,9 @@ Workload (BASELINE.json configs[2], the metric's "10^8-particle 4096^2 projectio
 10^8 Plummer particles -> 4096^2 mass-weighted-temperature map (sum m T W / sum m W),
 Wendland-C2, fp32, pixel-scale smoothing lengths (h = 0.75 px, the HBM-bound case of
 SURVEY.md §8(d)).  Inputs are generated on the device and resident in HBM before the
-timed region.  With N ranks the particles are Z-slab sharded (equal counts) and one RCCL
-reduce sums the two component maps on rank 0 (strong scaling: total work fixed).
+timed region.  With N ranks (configs[3]) the particles are Z-slab sharded (equal modelled
+work) and one RCCL reduce sums the two component maps on rank 0 (strong scaling: total
+work fixed); ``--decomp rows`` is the image-row alternative of SURVEY H2 ("cfg4-rows").
 
 One "step" = one full map: binning + deposit + (N > 1) RCCL reduce + ratio.  With N > 1
 the component maps are double-buffered so the reduce of map i runs on RCCL's stream while
@@ -30,6 +31,11 @@ sys.path.insert(0, os.path.join(REPO, "astro-sph-tools_amd"))
 METRIC = "Mpixels/s + particles/s, 10^8-particle 4096² projection at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table: peak FP32 (vector), spec
+# FP64 vector: half the FP32 vector rate on gfx950 (78.6 TFLOPS, AMD's MI355X spec; the
+# guide's chip table lists only FP32 -- DESIGN.md §10 measures fp64 VALU at half rate)
+VALU_F64_PEAK_TFLOPS = 78.6
+# flops of one squared distance (dx, dy, dz: 3; dx dx: 1; two FMAs: 4)
+DIST_FLOPS = 8
 # Algorithmic fp32 flops per included (pixel, particle) pair, an FMA counted as 2
 # (DESIGN.md §4 "compute roofline"): dx, dy (2), r^2 = dx dx + dy dy (3), sqrt (1),
 # q = r / h (1), the shape, and a * W added into each map (2 per map).
@@ -55,17 +61,20 @@ def parse():
     ap.add_argument("--map", default="weighted", choices=["weighted", "surface"])
     ap.add_argument("--op", default="reduce",
                     choices=["reduce", "allreduce", "reduce_scatter", "reduce_scatter_gather"])
-    ap.add_argument("--decomp", default="rows", choices=["zslab", "rows"],
-                    help="N > 1: rows (default) = each rank owns image rows (particles "
-                         "routed by footprint before the timed region), projects only them "
-                         "with the ratio formed locally, and the ratio map's slabs go to "
-                         "rank 0 (--rows-gather) -- no grid reduction; zslab = each rank's "
-                         "Z-slab onto the full grid + one grid collective (--op).  One GPU, "
-                         "8 shares of the 10^8 map: rows max 0.50 ms vs zslab 0.59 ms + a "
-                         "2 x 64 MiB reduce (DESIGN.md §8)")
-    ap.add_argument("--rows-gather", default="dst", choices=["dst", "all"],
-                    help="--decomp rows: the ratio map's row slabs to rank 0 (point-to-point "
-                         "sends of the exact slabs) or all-gathered on every rank")
+    ap.add_argument("--decomp", default="zslab", choices=["zslab", "rows"],
+                    help="N > 1: zslab (default; north_star, BASELINE configs[3]) = each "
+                         "rank's Z-slab of the particles onto the FULL grid + one RCCL "
+                         "collective on the grid (--op) -- any reader split needs no "
+                         "exchange; rows = each rank owns image rows, the particles are "
+                         "routed to the row owners by one all-to-all from the reader's split "
+                         "(timed once, reported as partition_ms), each rank projects only "
+                         "its rows with the ratio formed locally, and the ratio map's slabs "
+                         "are gathered (--rows-gather); DESIGN.md §8")
+    ap.add_argument("--rows-gather", default="all", choices=["all", "dst"],
+                    help="--decomp rows: all-gather of the ratio map's (padded) row slabs on "
+                         "every rank (default), or point-to-point sends of the exact slabs to "
+                         "rank 0 (over gloo with CUDA tensors this path costs ~1.2-1.4 s per "
+                         "map whatever the size: a gloo artifact, DESIGN.md §8)")
     ap.add_argument("--slab-weight", default="cost", choices=["cost", "count"],
                     help="N > 1 Z-slab edges: equal modelled work (distributed.slab_cost) or "
                          "equal particle counts")
@@ -75,7 +84,9 @@ def parse():
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_latest.json"),
                     help="PMC summary (tools/pmc_summary.py) for roofline.traffic")
     ap.add_argument("--deterministic", action="store_true",
-                    help="int64 fixed-point accumulation (bitwise reproducible maps)")
+                    help="int64 fixed-point accumulation (bitwise reproducible maps); "
+                         "surface-density maps only (--map surface): the library refuses "
+                         "fixed-point ratio maps (DESIGN.md §4)")
     ap.add_argument("--workload", default="map", choices=["map", "cube", "stage", "knn", "ion"],
                     help="map: the headline 2-D projection; cube: BASELINE configs[4], "
                          "10^8 particles -> 512^3 density cube; stage: snapshot fp64 -> "
@@ -408,9 +419,17 @@ def run_knn(args, dev):
     """h = distance to the 32nd nearest neighbour (the reference's
     scipy KDTree query, io/SWIFT/_SnapshotSWIFT.py:62-83) for N Plummer particles, inputs
     in HBM.  CPU baseline: scipy KDTree build + query (one thread, as the reference calls
-    it) on a bounded random sample."""
+    it) on a bounded random sample.
+
+    Roofline (VALU): the search kernel evaluates squared distances -- fp32 ones in the
+    curve-window pass (the prefilter; exact fp64 only for the few candidates) and fp64
+    ones in the cell scans -- counted in one untimed diagnostic call (ASP_KNN_COUNT), 8
+    flops each; the time that work needs at the FP32 / FP64 vector peaks, over the search
+    kernel's HIP-event time in the timed steps, is the fraction."""
     import numpy as np
     import torch
+    from asp_amd import _lib
+    from asp_amd.device import stats
     from asp_amd.knn import knn_smoothing_lengths
     from asp_amd.plummer import plummer_torch
     d = plummer_torch(args.n, seed=0, h_law="pixel", extent=4.0, grid=64, device=dev)
@@ -420,12 +439,43 @@ def run_knn(args, dev):
     for _ in range(args.warmup):
         knn_smoothing_lengths(pos, 32)
     torch.cuda.synchronize()
+    local = dev.index or 0
+    _lib.profile(local, True)
     t = time.perf_counter()
     for _ in range(args.steps):
         h = knn_smoothing_lengths(pos, 32)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t) / args.steps * 1e3
+    prof = {k: v for k, v in _lib.profile_read(local).items() if v[1]}
+    _lib.profile(local, False)
     ok = bool(torch.isfinite(h).all().item()) and float(h.min().item()) > 0
+    # untimed: the distances the search evaluates (one atomic per lane while counting)
+    os.environ["ASP_KNN_COUNT"] = "1"
+    try:
+        h2 = knn_smoothing_lengths(pos, 32)
+        torch.cuda.synchronize()
+        st = stats(local)
+    finally:
+        del os.environ["ASP_KNN_COUNT"]
+    same = bool(torch.equal(h, h2))
+    e32, e64 = float(st["evals"]), float(st["evals_small"])  # window (fp32), cell scans (fp64)
+    s_ms = prof["knn_search"][0] / max(1, prof["knn_search"][1]) if "knn_search" in prof else None
+    roof = None
+    if s_ms:
+        t_peak = (e32 * DIST_FLOPS / (VALU_PEAK_TFLOPS * 1e12)
+                  + e64 * DIST_FLOPS / (VALU_F64_PEAK_TFLOPS * 1e12))
+        flops = (e32 + e64) * DIST_FLOPS
+        roof = {"bound": "valu", "kernel": "knn_search",
+                "achieved": round(flops / (s_ms * 1e-3) / 1e12, 3),
+                "peak": round(flops / t_peak / 1e12, 3), "unit": "TFLOP/s",
+                "frac": round(t_peak / (s_ms * 1e-3), 4),
+                "distances_fp32": int(e32), "distances_fp64": int(e64),
+                "distances_per_particle": round((e32 + e64) / args.n, 1),
+                "flops_per_distance": DIST_FLOPS,
+                "kernel_ms_per_step": round(s_ms, 4),
+                "peak_note": f"work-weighted peak: fp32 distances at {VALU_PEAK_TFLOPS}, fp64 "
+                             f"at {VALU_F64_PEAK_TFLOPS} TFLOP/s; frac = time at those peaks "
+                             f"/ the search kernel's event time"}
     res = {
         "metric": "k-NN smoothing lengths/s (k = 32, fp64, bit-exact vs scipy KDTree)",
         "value": args.n / ms * 1e3, "unit": "particles/s", "n_gpus": 1, "steps": args.steps,
@@ -433,8 +483,11 @@ def run_knn(args, dev):
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic Plummer sphere (a=1, seed 0) generated in HBM",
         "config": {"workload": f"knn: {args.n:.0e} particles, k = 32", "particles": args.n},
-        "output_ok": ok,
+        "stages": {k: {"ms_per_launch": a / b, "launches": b} for k, (a, b) in prof.items()},
+        "output_ok": ok and same,
     }
+    if roof is not None:
+        res["roofline"] = roof
     if args.cpu_baseline != "off":
         from scipy.spatial import KDTree
         m = min(args.n, 1 << 20)
@@ -573,6 +626,18 @@ def valu_roofline(valu, kernel, nout, dom, dom_ms, pm_stage):
     return r
 
 
+def workload_tag(n, grid, world, rows):
+    """BASELINE.json configs: [1] 10^7 -> 2048^2 surface density, [2] 10^8 -> 4096^2
+    weighted map (the metric's), [3] the same Z-slab-decomposed on N GPUs with one grid
+    collective; the image-row decomposition is NOT configs[3] ("cfg4-rows"); anything
+    else is a custom size."""
+    if n == 100_000_000 and grid == 4096:
+        return "cfg3" if world == 1 else ("cfg4-rows" if rows else "cfg4")
+    if n == 10_000_000 and grid == 2048:
+        return "cfg2"
+    return "custom"
+
+
 def output_check(out0, out1, a0, a1, ratio, world=1, gathered_ratio=False):
     """Size-independent sanity of the timed map (the parity proper is tests/): finite,
     non-negative component sums (W >= 0, m > 0), and for the mass-weighted map every pixel a
@@ -603,6 +668,10 @@ def output_check(out0, out1, a0, a1, ratio, world=1, gathered_ratio=False):
 
 def main():
     args = parse()
+    if args.deterministic and args.map == "weighted" and args.workload == "map":
+        log("bench: --deterministic needs --map surface (a ratio of fixed-point components "
+            "is imprecise in kernel-tail pixels; the library refuses it, DESIGN.md §4)")
+        sys.exit(2)
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -639,30 +708,51 @@ def main():
     t0 = time.time()
     d = plummer_torch(args.n, seed=0, h_law=args.h_law, extent=extent, grid=G, device=dev)
     R = None  # --decomp rows: the row-slab bounds
+    partition_ms = None  # --decomp rows: the timed all-to-all from the reader's split
+    rows_got = None
     if world > 1:
-        from asp_amd.distributed import route_rows, row_slabs, slab_cost
-        w = None if args.slab_weight == "count" else slab_cost(d["x"], d["y"], d["h"], ext, 2 * extent / G)
+        from asp_amd.distributed import exchange_rows, row_slabs, slab_cost
         if args.decomp == "rows":
-            # image-plane ownership: this rank's rows, the particles whose footprints reach
-            # them (the partition is untimed, as the Z-slab split is)
-            Rt = torch.tensor(row_slabs(G, world, d["x"], ext[:2], weights=w), dtype=torch.int64,
-                              device=dev)
-            dist.broadcast(Rt, src=0)
-            R = Rt.tolist()
-            r0, r1 = route_rows(d["x"], d["h"], ext[:2], G, R)
-            keep = (r0 <= rank) & (r1 >= rank)
-            del r0, r1
+            # The reader's split (_SnapshotEAGLE.py:120-130): a contiguous 1/W of the
+            # particles per rank, with no spatial order.  The row bounds balance the union
+            # of all ranks' particles (one all-reduce of a row histogram), then ONE
+            # all-to-all sends every particle to the ranks whose rows its 2h footprint
+            # reaches -- timed: the per-snapshot cost the row decomposition adds.
+            lo_, hi_ = args.n * rank // world, args.n * (rank + 1) // world
+            d = {k: v[lo_:hi_].contiguous() for k, v in d.items()}
+            w = None if args.slab_weight == "count" else slab_cost(d["x"], d["y"], d["h"], ext, 2 * extent / G)
+            R = row_slabs(G, world, d["x"], ext[:2], weights=w, group=dist.group.WORLD)
+            del w
+            cols = [d["x"], d["y"], d["h"]] + ([(d["m"] * d["T"]).contiguous(), d["m"]]
+                                               if args.map == "weighted" else [d["m"]])
+            torch.cuda.synchronize()
+            dist.barrier()
+            t_ex = time.perf_counter()
+            rows_got = exchange_rows(cols, d["x"], d["h"], u_extent=ext[:2], nx=G, bounds=R)
+            torch.cuda.synchronize()
+            pt = torch.tensor([time.perf_counter() - t_ex], dtype=torch.float64, device=dev)
+            dist.all_reduce(pt, op=dist.ReduceOp.MAX)
+            partition_ms = float(pt.item()) * 1e3
+            del cols, d
+            d = {"x": rows_got[0], "y": rows_got[1], "h": rows_got[2]}
         else:
+            # Z-slabs: any reader split sums to the same map, so no exchange is needed; the
+            # slabs (equal modelled work) only balance the ranks
+            w = None if args.slab_weight == "count" else slab_cost(d["x"], d["y"], d["h"], ext, 2 * extent / G)
             e = zslab_bounds(d["z"], world, weights=w)
             keep = (d["z"] >= e[rank]) & (d["z"] < e[rank + 1])
-        del w
-        d = {k: v[keep].contiguous() for k, v in d.items()}
+            del w
+            d = {k: v[keep].contiguous() for k, v in d.items()}
     u, v, h = d["x"], d["y"], d["h"]
-    if args.map == "weighted":
+    if rows_got is not None:  # the routed columns as exchanged
+        a0, a1 = rows_got[3], (rows_got[4] if args.map == "weighted" else None)
+        del rows_got
+    elif args.map == "weighted":
         a0, a1 = (d["m"] * d["T"]).contiguous(), d["m"]
+        del d["z"], d["T"]
     else:
         a0, a1 = d["m"], None
-    del d["z"], d["T"]
+        del d["z"], d["T"]
     n_local = u.shape[0]
     torch.cuda.synchronize()
     if not args.quiet:
@@ -856,14 +946,7 @@ def main():
             traffic_src = pm[key].get("source")
     except (OSError, ValueError, KeyError):
         pass
-    # BASELINE.json configs: [1] 10^7 -> 2048^2 surface density, [2] 10^8 -> 4096^2
-    # weighted map (the metric's), [3] the same on 8 GPUs; anything else is a custom size
-    if args.n == 100_000_000 and G == 4096:
-        cfg_tag = "cfg4" if world > 1 else "cfg3"
-    elif args.n == 10_000_000 and G == 2048:
-        cfg_tag = "cfg2"
-    else:
-        cfg_tag = "custom"
+    cfg_tag = workload_tag(args.n, G, world, R is not None)
     res = {
         "metric": METRIC, "value": round(mpix, 3), "unit": "Mpixels/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
@@ -891,13 +974,19 @@ def main():
                        "collective": args.op if R is None else
                        ("all_gather" if args.rows_gather == "all" else "p2p_gather"),
                        "partition": ("Z-slab split of the generated particles before the "
-                                     "timed region (untimed, as a reader-split snapshot "
-                                     "needs none)" if R is None else
-                                     "each rank keeps the generated particles whose 2h "
-                                     "footprint reaches its rows, before the timed region "
-                                     "(untimed; from a reader's arbitrary split this is "
-                                     "one all-to-all per snapshot, "
-                                     "distributed.exchange_rows)")} if world > 1 else {})},
+                                     "timed region (only balances the ranks: any reader "
+                                     "split sums to the same map, so none is needed)"
+                                     if R is None else
+                                     "from a reader split (a contiguous 1/W per rank), one "
+                                     "all-to-all routes every particle to the ranks whose "
+                                     "rows its 2h footprint reaches "
+                                     "(distributed.exchange_rows): once per snapshot, "
+                                     "before the timed region, timed as partition_ms")}
+                    if world > 1 else {})},
+        **({"partition_ms": round(partition_ms, 3),
+            "partition_note": "the rows decomposition's per-snapshot all-to-all (max over "
+                              "ranks); amortised over the maps made from one snapshot"}
+           if partition_ms is not None else {}),
         "particles_per_s": pps,
         **({"latency_ms_per_map": round(latency_ms, 4),
             "latency_note": "one map at a time, synchronised (no overlap of maps): binning + "

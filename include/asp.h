@@ -47,7 +47,9 @@ extern "C" {
 #define ASP_F_DETERMINISTIC 0x8 /* int64 fixed-point accumulation: bitwise reproducible and
                                  * input-order independent maps; relative precision degrades
                                  * for pixels below ~2^-37 n_t max|A W| of their 64x64 tile
-                                 * (DESIGN.md §4).  Default: fp64 accumulation.            */
+                                 * (DESIGN.md §4).  Default: fp64 accumulation.  Not with
+                                 * ASP_F_RATIO (ASP_ERR_INVALID): a ratio of fixed-point
+                                 * components is imprecise in kernel-tail pixels.           */
 #define ASP_F_DEVICE_OUTPUTS 0x10 /* host (pageable) inputs, device outputs: the reader's
                                    * arrays in, a device map out for the RCCL sum; the
                                    * inputs go through pinned bounce buffers (two 32 MiB

@@ -378,7 +378,9 @@ def _rows_worker(rank, world, port, q):
                                    kernel="cubic", ratio=True, gather="dst",
                                    projector=_oracle_rows)
         res["dst"] = got.numpy().copy()
-        R = row_slabs(GR, world, x, EXT[:2])
+        # the bounds project2d_rowslab balanced: the all-reduced row histogram of every
+        # rank's own particles (the same on both ranks)
+        R = row_slabs(GR, world, sl[0], EXT[:2], group=dist.group.WORLD)
         res["bounds"] = R
         r0, r1 = route_rows(x, h, EXT[:2], GR, R)
         res["routed"] = int(((r0 <= rank) & (r1 >= rank)).sum())

@@ -34,14 +34,25 @@ def _run(extra):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("decomp", ["rows", "zslab"])
+@pytest.mark.parametrize("decomp", ["default", "rows", "rows-dst"])
 def test_bench_two_ranks_one_gpu(gpu, decomp):
-    d = _run(["--decomp", decomp])
+    extra = {"default": [], "rows": ["--decomp", "rows"],
+             "rows-dst": ["--decomp", "rows", "--rows-gather", "dst", "--steps", "2"]}[decomp]
+    d = _run(extra)
     assert d["n_gpus"] == 2 and d["output_ok"] is True
     assert d["config"]["backend"].startswith("gloo")
-    assert d["config"]["decomp"] == decomp
+    # north_star / BASELINE configs[3]: Z-slabs + one grid collective are the N > 1 default
+    want = "zslab" if decomp == "default" else "rows"
+    assert d["config"]["decomp"] == want
+    assert d["config"]["parallelism"] == ("zslab2" if want == "zslab" else "rows2")
     assert 0.0 < d["roofline"]["frac"] <= 1.0
     assert d["value"] > 0 and d["ms_per_step"] > 0
-    if decomp == "rows":
+    if want == "zslab":
+        assert "Z-slab x2" in d["config"]["workload"] and d["config"]["collective"] == "reduce"
+        assert "partition_ms" not in d
+    else:
         R = d["config"]["row_bounds"]
         assert R[0] == 0 and R[-1] == 1024 and all(a < b for a, b in zip(R, R[1:]))
+        assert "image row slabs x2" in d["config"]["workload"]
+        assert d["partition_ms"] > 0  # the timed all-to-all from the reader's split
+        assert d["config"]["collective"] == ("p2p_gather" if decomp == "rows-dst" else "all_gather")

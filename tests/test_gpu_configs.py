@@ -12,7 +12,12 @@
   4096^2 mass-weighted map (``zslab_bounds(z, 8, weights=slab_cost(...))``, the edges
   ``bench.py --gpus 8`` uses), each projected by the HIP path alone and summed on the host
   as the RCCL reduce would: counts bit-exact against ``project_scatter`` over all
-  particles, both components and the ratio within the bar.
+  particles, both components and the ratio within the bar;
+* the image-row alternative (``bench.py --decomp rows``): the same map's eight
+  row slabs (``row_slabs``), each projected by ``asp_project2d_rows`` from only the
+  particles ``route_rows`` sends it, the ratio formed locally, the slabs concatenated as
+  the gather assembles them: counts bit-exact, components and ratio within the bar
+  against ``project_scatter`` over all particles.
 
 The reference has no cube and no multi-GPU path; the cube's parity
 is pinned by its CPU restatement (tests/test_cube_oracle.py), the map's by the goldens.
@@ -142,4 +147,56 @@ def test_cfg4_eight_zslab_shards_summed(gpu, oracle):
     assert_ratio_close(ratio, o0, o1)
     c_ref, _ = oracle.project_scatter(pos[:, 0], pos[:, 1], h, np.ones(n), None, (G, G), 64,
                                       *ext, kernel="indicator")
+    assert np.array_equal(cnt, c_ref)
+
+
+def test_cfg4_rows_eight_row_slabs_assembled(gpu, oracle):
+    """The row-slab decomposition (``bench.py --decomp rows``) on one GPU: 2 x 10^6 Plummer
+    particles at pixel-scale h, 4096^2 mass-weighted Wendland-C2 map, 8 row slabs; each
+    slab projected from ITS routed particles only (asp_project2d_rows), its ratio formed
+    locally, the slabs stitched as the reference stitches its chunks
+    (_projector.py:111-117): neighbour counts bit-exact, both components and the ratio
+    within the bar, against the oracle over ALL particles (not against the library's own
+    full map)."""
+    import torch
+    from asp_amd.device import project2d
+    from asp_amd.distributed import route_rows, row_slabs
+    from asp_amd.plummer import plummer
+    n, G, W = 2_000_000, 4096, 8
+    ext = (-4.0, 4.0, -4.0, 4.0)
+    p = plummer(n, seed=29, h_law="pixel", grid=G)
+    f32 = lambda a: np.ascontiguousarray(a, np.float32)  # noqa: E731
+    x, y, h = f32(p["pos"][:, 0]), f32(p["pos"][:, 1]), f32(p["h"])
+    a0, a1 = f32(p["m"] * p["T"]), f32(p["m"])
+    dev = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    u, v, hh, A0, A1 = (dev(a) for a in (x, y, h, a0, a1))
+    R = row_slabs(G, W, u, ext[:2])
+    assert len(R) == W + 1 and R[0] == 0 and R[-1] == G
+    r0, r1 = route_rows(u, hh, ext[:2], G, R)
+    s0, s1, rr, cnt = (np.zeros((G, G), np.float64) for _ in range(4))
+    routed = 0
+    for r in range(W):
+        k = (r0 <= r) & (r1 >= r)
+        routed += int(k.sum())
+        su, sv, sh, sa0, sa1 = (t[k].contiguous() for t in (u, v, hh, A0, A1))
+        rows = (R[r], R[r + 1])
+        kw = dict(image_size=(G, G), extent=ext, kernel="wendland_c2", rows=rows)
+        c0, c1 = project2d(su, sv, sh, sa0, sa1, **kw)
+        q0, q1 = project2d(su, sv, sh, sa0, sa1, ratio=True, **kw)
+        c, _ = project2d(su, sv, sh, torch.ones_like(sh), image_size=(G, G), extent=ext,
+                         kernel="indicator", rows=rows)
+        sl = slice(*rows)
+        s0[sl], s1[sl] = c0.cpu().numpy(), c1.cpu().numpy()
+        rr[sl], cnt[sl] = q0.cpu().numpy(), c.cpu().numpy()
+        # the weight map of the ratio call is the same sum (fp64 atomics: order may differ)
+        np.testing.assert_allclose(q1.cpu().numpy(), s1[sl], rtol=1e-6, atol=0)
+    assert n * 0.95 < routed < n * 1.05  # duplicates only where footprints cross a bound
+    xd, yd, hd = (a.astype(np.float64) for a in (x, y, h))
+    o0, o1 = oracle.project_scatter(xd, yd, hd, a0.astype(np.float64), a1.astype(np.float64),
+                                    (G, G), 64, *ext, kernel="wendland_c2")
+    assert_map_close(s0, o0)
+    assert_map_close(s1, o1)
+    assert_ratio_close(rr, o0, o1)
+    c_ref, _ = oracle.project_scatter(xd, yd, hd, np.ones(n), None, (G, G), 64, *ext,
+                                      kernel="indicator")
     assert np.array_equal(cnt, c_ref)

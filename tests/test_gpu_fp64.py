@@ -103,67 +103,56 @@ def test_baseline_cfg3_4096_weighted_wendland_pixel_h(gpu, oracle):
     assert cnt.sum() > 5 * n  # ~7 pairs per particle at pixel-scale h
 
 
-def assert_weighted_fixed_point(r, o0, o1):
-    """The deterministic (int64 fixed-point) weighted map against the reference components:
-    zero where the reference is zero, and within assert_ratio_close's propagated bound
-    wherever the reference weight is above the value bar (o1 > 2e-5 max o1).  Pixels whose
-    weight comes only from kernel-tail pairs hold a few fixed-point units of weight, so
-    their quotient carries no precision claim (a per-tile integer scale
-    cannot give tail terms relative precision; the fp64 default has no such pixels)."""
-    from test_gpu_parity import ABS_TOL
-    r = np.asarray(r, np.float64)
-    with np.errstate(divide="ignore", invalid="ignore"):
-        want = np.where(o1 != 0, o0 / o1, 0.0)
-    assert np.all(r[want == 0] == 0)
-    sel = o1 > ABS_TOL * np.abs(o1).max()
-    assert_ratio_close(np.where(sel, r, 0.0), np.where(sel, o0, 0.0), np.where(sel, o1, 0.0))
-    return int((~sel & (o1 != 0)).sum())
-
-
-def test_baseline_cfg3_4096_deterministic_weighted(gpu, oracle):
+def test_baseline_cfg3_4096_deterministic_components(gpu, oracle):
     """The int64 fixed-point accumulation (ASP_F_DETERMINISTIC) on BASELINE configs[2]'s map
-    (4096^2, weighted Wendland-C2, pixel h, 2 x 10^6 raw-fp64 Plummer particles): the two
-    components against the oracle within the value bar, the ratio against the oracle's
-    (assert_weighted_fixed_point), fused and host ratios agreeing, and the map bitwise
-    reproducible under a permutation of the particles."""
+    (4096^2, Wendland-C2, pixel h, 2 x 10^6 raw-fp64 Plummer particles): both component maps
+    (m T and m, two outputs, no ratio) against the oracle within the value bar, and bitwise
+    reproducible under a permutation of the particles.  A RATIO map of fixed-point
+    components is refused (ASP_ERR_INVALID / ValueError): pixels reached only by kernel
+    tails keep a few fixed-point units of weight."""
+    import torch
+    from asp_amd._lib import ASPError
+    from asp_amd.device import project2d, project2d_f64
     from asp_amd.tools.projections import create_weighted_image, wendland_c2_kernel
     n, G = 2_000_000, 4096
     p = _plummer(n, 41, "pixel", G)
     pos, h, m, T = p["pos"], p["h"], p["m"], p["T"]
     ext = (-4.0, 4.0, -4.0, 4.0)
-    kw = dict(kernel_func=wendland_c2_kernel, deterministic=True)
-    r, s0, s1 = create_weighted_image(pos, h, m, T, (G, G), 64, 2, *ext,
-                                      return_components=True, **kw)
+    kw = dict(image_size=(G, G), extent=ext, chunk_size=64, kernel="wendland_c2",
+              deterministic=True)
+    s0, s1 = project2d_f64(pos, h, m * T, m, **kw)
     o0, o1 = oracle.project_scatter(pos[:, 0], pos[:, 1], h, m * T, m, (G, G), 64, *ext,
                                     kernel="wendland_c2")
     assert_map_close(s0, o0)
     assert_map_close(s1, o1)
-    assert_weighted_fixed_point(r, o0, o1)
-    r2 = create_weighted_image(pos, h, m, T, (G, G), 64, 2, *ext, **kw)  # fused ratio
-    assert np.array_equal(r2, r.astype(np.float32).astype(np.float64)) or \
-        np.allclose(r2, r, rtol=2e-7, atol=0)
     perm = np.random.default_rng(3).permutation(n)
-    r3 = create_weighted_image(pos[perm], h[perm], m[perm], T[perm], (G, G), 64, 2, *ext, **kw)
-    assert np.array_equal(r2, r3)
+    q0, q1 = project2d_f64(pos[perm], h[perm], (m * T)[perm], m[perm], **kw)
+    assert np.array_equal(q0, s0) and np.array_equal(q1, s1)
+    with pytest.raises(ValueError):
+        create_weighted_image(pos, h, m, T, (G, G), 64, 2, *ext, kernel_func=wendland_c2_kernel,
+                              deterministic=True)
+    t = [torch.from_numpy(x.astype(np.float32)).cuda() for x in (pos[:1000, 0], pos[:1000, 1],
+                                                               h[:1000], m[:1000] * T[:1000], m[:1000])]
+    with pytest.raises(ASPError, match="DETERMINISTIC"):
+        project2d(*t, image_size=(64, 64), extent=ext, kernel="wendland_c2", ratio=True,
+                  deterministic=True)
 
 
-def test_deterministic_weighted_physical_h(gpu, oracle):
-    """The same at physical h (gathered large stream and split tiles: every fixed-point
-    deposit path)."""
-    from asp_amd.device import stats
-    from asp_amd.tools.projections import create_weighted_image
+def test_deterministic_components_physical_h(gpu, oracle):
+    """The same components at physical h (gathered large stream and split tiles: every
+    fixed-point deposit path)."""
+    from asp_amd.device import project2d_f64, stats
     n, G = 400_000, 1024
     p = _plummer(n, 43, "physical", G)
     pos, h, m, T = p["pos"], p["h"], p["m"], p["T"]
     ext = (-4.0, 4.0, -4.0, 4.0)
-    r, s0, s1 = create_weighted_image(pos, h, m, T, (G, G), 64, 2, *ext, deterministic=True,
-                                      return_components=True)
+    s0, s1 = project2d_f64(pos, h, m * T, m, image_size=(G, G), extent=ext, chunk_size=64,
+                           kernel="cubic", deterministic=True)
     st = stats(0)
     assert st["large"] > 0 and st["merges"] > 0
     o0, o1 = oracle.project_scatter(pos[:, 0], pos[:, 1], h, m * T, m, (G, G), 64, *ext)
     assert_map_close(s0, o0)
     assert_map_close(s1, o1)
-    assert_weighted_fixed_point(r, o0, o1)
 
 
 def test_baseline_cfg2_2048_cubic_physical_h(gpu, oracle):
@@ -251,8 +240,9 @@ def test_sharded_host_arrays_single_rank_hip_path(gpu):
     pos = rng.normal(0, 0.5, (n, 3))
     h = rng.uniform(0.003, 0.02, n)
     m, T = rng.uniform(0.5, 2.0, n), rng.uniform(1e3, 1e5, n)
+    # fp64 accumulation: a ratio map of fixed-point components is refused
     kw = dict(image_size=(256, 256), extent=(-2.0, 2.0, -2.0, 2.0), chunk_size=64,
-              kernel="wendland_c2", deterministic=True)
+              kernel="wendland_c2")
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -267,4 +257,6 @@ def test_sharded_host_arrays_single_rank_hip_path(gpu):
     want = np.where(c1 != 0, c0 / np.where(c1 != 0, c1, 1), 0).astype(np.float32)
     got = r.cpu().numpy()
     assert r.is_cuda
-    np.testing.assert_allclose(got, want, rtol=2e-7, atol=0)
+    # separate fp64-accumulated calls: LDS-atomic order moves the fp32 maps by an ulp or so
+    np.testing.assert_array_equal(got == 0, want == 0)
+    np.testing.assert_allclose(got, want, rtol=2e-6, atol=0)

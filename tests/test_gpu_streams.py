@@ -22,14 +22,14 @@ def test_two_stream_maps_equal_serial(gpu, oracle):
         d = plummer_torch(n, seed=seed, h_law=law, extent=4.0, grid=G, device=dev)
         sets.append((d["x"], d["y"], d["h"], (d["m"] * d["T"]).contiguous(), d["m"]))
     kw = dict(image_size=(G, G), extent=ext, kernel="wendland_c2", deterministic=True)
-    serial = [tuple(t.clone() for t in project2d(*s, ratio=True, **kw)) for s in sets]
+    serial = [tuple(t.clone() for t in project2d(*s, **kw)) for s in sets]
     torch.cuda.synchronize()
     streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
     outs = [None] * 12
     for k in range(12):
         s = sets[k % len(sets)]
         with torch.cuda.stream(streams[k % 2]):
-            outs[k] = project2d(*s, ratio=True, **kw)
+            outs[k] = project2d(*s, **kw)
     torch.cuda.synchronize()
     for k in range(12):
         want = serial[k % len(sets)]
@@ -46,6 +46,6 @@ def test_two_stream_maps_equal_serial(gpu, oracle):
     assert np.array_equal(cnt.double().cpu().numpy(), ref)
     _lib.check(_lib.lib().asp_release(0))
     with torch.cuda.stream(streams[0]):
-        again = project2d(*sets[0], ratio=True, **kw)
+        again = project2d(*sets[0], **kw)
     torch.cuda.synchronize()
     assert torch.equal(again[0], serial[0][0])

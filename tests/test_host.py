@@ -187,3 +187,29 @@ def test_cpu_baseline_chunk_counts():
             want[cx * nc + cy] = np.sum((u >= xl - r) & (u < xl + w + r) & (v >= yl - r) &
                                         (v < yl + w + r))
     assert np.abs(x - want).max() <= 0.001 * want.max()  # float edge cases at chunk bounds
+
+
+def test_bench_workload_tags():
+    """bench.py's config tag: configs[3] (cfg4) is the Z-slab decomposition only; a row-slab
+    line at the same size is tagged cfg4-rows (verdict r04: a row line labelled cfg4)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert b.workload_tag(100_000_000, 4096, 1, False) == "cfg3"
+    assert b.workload_tag(100_000_000, 4096, 8, False) == "cfg4"
+    assert b.workload_tag(100_000_000, 4096, 8, True) == "cfg4-rows"
+    assert b.workload_tag(10_000_000, 2048, 1, False) == "cfg2"
+    assert b.workload_tag(2_000_000, 1024, 2, True) == "custom"
+
+
+def test_bench_n_gt_1_defaults(monkeypatch):
+    """The N > 1 defaults: north_star's Z-slabs + one reduce; rows gather by all-gather."""
+    import importlib.util
+    import sys
+    spec = importlib.util.spec_from_file_location("bench_mod2", os.path.join(REPO, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
+    a = b.parse()
+    assert a.decomp == "zslab" and a.op == "reduce" and a.rows_gather == "all"

@@ -38,6 +38,7 @@ def run(k=5):
 
 
 settings = sys.argv[1:] or ["ASP_SCATTER_GROUP=4"]
+ref = None  # the first setting's maps: every other setting's maps must agree
 for rep in range(3):
     for s in settings:
         env = dict(kv.split("=") for kv in s.split(",") if kv)
@@ -49,4 +50,11 @@ for rep in range(3):
                 os.environ.pop(k)
             else:
                 os.environ[k] = val
-        print(rep, s, r, flush=True)
+        if ref is None:
+            ref = o.clone()
+            dev_ = 0.0
+        else:
+            dev_ = float(((o - ref).abs().max() / ref.abs().max()).item())
+        print(rep, s, r, f"maxdev {dev_:.2e}", flush=True)
+        if dev_ > 1e-5:
+            sys.exit(f"{s}: maps differ from {settings[0]} by {dev_:.2e} x max")
