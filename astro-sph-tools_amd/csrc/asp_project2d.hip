@@ -349,7 +349,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                 __syncthreads();
             }
             if (threadIdx.x == 0) {
-                if (wc_diag) wcd[0] = wcd[1] = wcd[2] = 0, wcd[3] = wci[0];
+                if (wc_diag & 1) wcd[0] = wcd[1] = wcd[2] = 0, wcd[3] = wci[0];
                 wci[1] = min(wci[1], nslots), wci[0] = 0;  // [0]: task count
             }
         }
@@ -487,21 +487,23 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                         atomicOr(&vmask[q], 1u << (slot & 3));
                         if ((slot & 3) == 3 || slot == rend[hs] - 1)  // the line's last slot
                             tasks[atomicAdd(&wci[0], 1)] = make_int2(line, q);
-                        if (wc_diag) atomicAdd(&wcd[0], 1);
+                        if (wc_diag & 1) atomicAdd(&wcd[0], 1);
                         return;
                     }
-                    if (wc_diag && hs >= 0) atomicAdd(&wcd[2], 1);
+                    if ((wc_diag & 1) && hs >= 0) atomicAdd(&wcd[2], 1);
                 }
                 if (first) {
                     first_slot[k] = slot;  // written by the paired store below
                     first_box[k] = bp;
                 } else {
+                    if (!(wc_diag & 2)) {  // (ablation 2: no direct stores; wrong maps)
                     rec_store(&recs[2 * (long long)slot],
                               make_float4((float)(U - corner_x(g, max(b.x0, tx * kTile))),
                                           (float)(V - corner_y(g, max(b.y0, ty * kTile))),
                                           ph[k], cf0));
                     rec_store(&recs[2 * (long long)slot + 1],
                               make_float4(cf1, __int_as_float(p), band, __uint_as_float(bp)));
+                    }
                 }
             };
             if (tx1 - tx0 <= 1 && ty1 - ty0 <= 1) {  // at most 2 x 2 tiles: straight-line
@@ -534,7 +536,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                 int src = half * 32 + (lane >> 1);
                 int slot = __shfl(first_slot[k], src);
                 float4 val = st[(lane & 1) * 72 + src];
-                if (slot >= 0) rec_store(&recs[2 * (long long)slot + (lane & 1)], val);
+                if (slot >= 0 && !(wc_diag & 2)) rec_store(&recs[2 * (long long)slot + (lane & 1)], val);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -544,11 +546,11 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             if (nslots > 0) {  // flush the lines finished in this batch: 8 lanes per line
                 __syncthreads();
                 const int nt = wci[0];
-                if (wc_diag && threadIdx.x == 0) wcd[1] += nt;
+                if ((wc_diag & 1) && threadIdx.x == 0) wcd[1] += nt;
                 for (int i = threadIdx.x >> 3; i < nt; i += kScatterBlock / 8) {
                     const int2 tk = tasks[i];
                     const int j = threadIdx.x & 7;
-                    if ((vmask[tk.y] >> (j >> 1)) & 1u)
+                    if (((vmask[tk.y] >> (j >> 1)) & 1u) && !(wc_diag & 4))
                         rec_store(&recs[8 * (long long)tk.x + j], ring[tk.y * 8 + j]);
                 }
                 __syncthreads();
@@ -576,7 +578,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     }
     __syncthreads();
     if constexpr (kWcOk)
-        if (wc_diag && nslots > 0 && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
+        if ((wc_diag & 1) && nslots > 0 && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
             printf("asp wc: block %d slots %d bmin %d parked %d flushed lines %d bypassed %d\n",
                    (int)blockIdx.x, wci[1], wcd[3], wcd[0], wcd[1], wcd[2]);
     if constexpr (ACC == kAccFix) {
@@ -2081,7 +2083,7 @@ static int scatter_variant(const Grid& g, const Src64& s, Workspace& ws, const P
                        a1, pl.n, pl.nblk, g, s, (const int*)ws.hist.p,
                        (const long long*)ws.tile_start.p, (const int*)ws.tile_total.p,
                        (float4*)ws.recs.p, (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc, pl.grp,
-                       rec_cap, wide_cap, xa, nslots, getenv("ASP_WC_DIAG") ? 1 : 0);
+                       rec_cap, wide_cap, xa, nslots, getenv("ASP_WC_DIAG") ? atoi(getenv("ASP_WC_DIAG")) : 0);
     ASP_LAUNCHED();
     return ASP_OK;
 }

@@ -1,0 +1,47 @@
+#!/bin/bash
+# One parameterised GPU step per call (chain calls with && inside one gpurun command).
+# Output under gpurun_out/$OUT/ (default r05).  Every GPU step runs under its own timeout.
+#   bash tools/gpu/run.sh suite                       pytest -m gpu (all) + smoke()
+#   bash tools/gpu/run.sh tests FILE...               pytest -m gpu on some files
+#   bash tools/gpu/run.sh bench NAME [bench args]     one bench.py line -> NAME.json
+#   bash tools/gpu/run.sh sweep VAR "V1 V2" NAME [bench args]
+#                                                     one line per VAR=Vi -> NAME_Vi.json
+#   bash tools/gpu/run.sh reps N NAME [bench args]    N fresh processes -> NAME_i.json
+#   bash tools/gpu/run.sh prof TAG [prof_driver args] kernel trace + PMC passes (prof_full.sh)
+# (round 4's one-off scripts tools/gpu/r04/*.sh are all instances of these modes)
+cd "$GRAFT_REPO_ROOT" || exit 9
+export TMPDIR=/tmp
+o=gpurun_out/${OUT:-r05}; mkdir -p $o
+mode=$1; shift
+summ() {  # name: ms, output check, dominant kernel, frac, per-stage ms
+  python3 -c "import json,sys;d=json.loads(open('$o/$1.json').read().strip().splitlines()[-1]);r=d.get('roofline',{});print('$1', d['ms_per_step'], d.get('output_ok'), r.get('kernel'), r.get('frac'), {k:round(v.get('ms_per_step', v.get('ms_per_launch', 0)),3) for k,v in d.get('stages',{}).items()})"
+}
+line() {  # name args...
+  local name=$1; shift
+  echo "== $(date +%T) $name: $*"
+  timeout -k 10 ${LIMIT:-300} python bench.py "$@" > $o/$name.json 2> $o/$name.err || { tail -5 $o/$name.err; return 1; }
+  summ $name
+}
+case $mode in
+  suite)
+    echo "== $(date +%T) gpu suite"
+    timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $o/gputest.log 2>&1 || { tail -40 $o/gputest.log; exit 1; }
+    tail -1 $o/gputest.log
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 || { tail -5 $o/smoke.log; exit 2; }
+    tail -1 $o/smoke.log ;;
+  tests)
+    echo "== $(date +%T) tests $*"
+    timeout -k 10 ${LIMIT:-900} python -u -m pytest "$@" -m gpu -x -q --timeout 300 --timeout-method thread > $o/tests.log 2>&1 || { tail -40 $o/tests.log; exit 1; }
+    tail -1 $o/tests.log ;;
+  bench)
+    line "$@" || exit 3 ;;
+  sweep)
+    var=$1; vals=$2; name=$3; shift 3
+    for v in $vals; do export "$var=$v"; line ${name}_$v "$@" || exit 3; done ;;
+  reps)
+    n=$1; name=$2; shift 2
+    for i in $(seq 1 $n); do line ${name}_$i "$@" || exit 3; done ;;
+  prof)
+    bash tools/gpu/prof_full.sh "$@" || exit 4 ;;
+  *) echo "unknown mode $mode"; exit 8 ;;
+esac

@@ -56,5 +56,5 @@ for rep in range(3):
         else:
             dev_ = float(((o - ref).abs().max() / ref.abs().max()).item())
         print(rep, s, r, f"maxdev {dev_:.2e}", flush=True)
-        if dev_ > 1e-5:
+        if dev_ > 1e-5 and not os.environ.get("AB_NOCHECK"):
             sys.exit(f"{s}: maps differ from {settings[0]} by {dev_:.2e} x max")
