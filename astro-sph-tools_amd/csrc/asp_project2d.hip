@@ -254,16 +254,9 @@ struct XArgs {
     float4* ext;
 };
 
-// Write-combining of the scatter's hottest runs (round 5).  A (workgroup, tile) run whose
-// records come often (the Plummer core's tiles) gets a two-line LDS ring (2 x 128 B = 8
-// records): its records are parked there by slot, and a 128-B line of the run is stored
-// only once all its slots are claimed -- by 8 lanes as ONE contiguous 128-B segment,
-// instead of 4 scattered 32-B records from 4 store instructions.  A record whose line is
-// more than one line past the run's first unfinished line is stored directly (the ring is
-// full); a flush writes only the slots its valid mask holds, so such a line stays correct.
-constexpr int kWcMinRun = 8;              // runs shorter than this are never buffered
-constexpr int kWcSlotBytes = 2 * 128 + 2 * 4 + 4 + 4 + 4 + 2 * 8;  // ring, masks, ls, rend, col, tasks
-constexpr int kStageF4 = 136;             // per-wave staging: halves 0 at [lane], 1 at [72 + lane]
+// Per-wave staging of the paired record stores: first halves at [lane], second halves at
+// [72 + lane] (8 float4 apart: neither the b128 writes nor the b128 reads conflict).
+constexpr int kStageF4 = 136;
 
 template <int KID, int NOUT, int ACC, bool CULL, int SRC, int PROBE, int NX = 0>
 __global__ __launch_bounds__(kScatterBlock) void k_scatter(
@@ -272,7 +265,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     Grid g, Src64 s, const int* __restrict__ hist, const long long* __restrict__ tile_start,
     const int* __restrict__ tile_total, float4* __restrict__ recs, unsigned* __restrict__ cmx,
     int* __restrict__ wide_list, int* __restrict__ ctr, int grp, long long rec_cap,
-    int wide_cap, XArgs xa, int nslots, int wc_diag) {
+    int wide_cap, XArgs xa) {
     // Speculative launch (enqueued before the host has read the counters): the record and
     // wide-list buffers were sized by an earlier call; if this call needs more, every
     // workgroup leaves at once and the host relaunches after growing them.
@@ -283,17 +276,6 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     // 8 float4 further on, so neither the b128 writes nor the b128 reads conflict)
     float4* stage = (float4*)(cur + 2 * g.ntiles);
     unsigned* cm = (unsigned*)(stage + (kScatterBlock / 64) * kStageF4);
-    // write-combining state (nslots > 0; f64 accumulation, no extra properties)
-    constexpr bool kWcOk = ACC == kAccF64 && NX == 0;
-    float4* ring = (float4*)cm;                              // [nslots][2 lines][8 halves]
-    unsigned* vmask = (unsigned*)(ring + (kWcOk ? nslots * 16 : 0));  // [nslots][2]
-    int* ls = (int*)(vmask + 2 * nslots);                    // first unfinished line of the run
-    int* rend = ls + nslots;                                 // the run's end (absolute slot)
-    int* hcol = rend + nslots;                               // the slot's column
-    int2* tasks = (int2*)(hcol + nslots);                    // lines to flush this batch
-    short* hs_of = (short*)(tasks + 2 * nslots);             // column -> slot, or -1
-    int* wci = (int*)(hs_of + ((g.ntiles + 1) & ~1));        // [0] tasks, [1] slots, [2..33] hist
-    int* wcd = wci + 34;  // ASP_WC_DIAG: parked records, flushed lines, bypassed hot records, threshold
     // this workgroup takes over count workgroups grp * sb ..: its cursors start at the
     // prefix row of the first of them
     const long long sb = blockIdx.x;
@@ -302,58 +284,6 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
         cur[t] = (int)tile_start[t] + row[t];  // n_recs < 2^31 (checked on the host)
     if constexpr (ACC == kAccFix)
         for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kScatterBlock) cm[t] = 0u;
-    // run end of small-stream column t (absolute slot one past this workgroup's last)
-    const bool last_wg = (sb + 1) * grp >= nblk;
-    const int* nrow = hist + (sb + 1) * grp * 2 * g.ntiles;
-    auto run_end = [&](int t) {
-        return (int)tile_start[t] + (last_wg ? tile_total[t] : nrow[t]);
-    };
-    if constexpr (kWcOk) {
-        if (nslots > 0) {
-            // the nslots longest runs (>= kWcMinRun records) get a ring: a log2 histogram of
-            // the run lengths, the threshold bucket, then slots by atomic claim
-            if (threadIdx.x < 34) wci[threadIdx.x] = 0;
-            __syncthreads();
-            for (int t = threadIdx.x; t < g.ntiles; t += kScatterBlock) {
-                const int len = run_end(t) - (int)tile_start[t] - row[t];
-                hs_of[t] = -1;
-                if (len >= kWcMinRun) atomicAdd(&wci[2 + 31 - __clz(len)], 1);
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) {  // lowest bucket whose runs and all longer ones fit
-                int acc = 0, b = 31;
-                for (; b >= 3; --b) {
-                    if (acc + wci[2 + b] > nslots) break;
-                    acc += wci[2 + b];
-                }
-                wci[0] = b + 1;  // runs with log2(len) >= wci[0] all get a slot
-            }
-            __syncthreads();
-            const int bmin = wci[0];
-            for (int pass = 0; pass < 2; ++pass) {  // the threshold buckets, then the next one
-                for (int t = threadIdx.x; t < g.ntiles; t += kScatterBlock) {
-                    const int len = run_end(t) - (int)tile_start[t] - row[t];
-                    if (len < kWcMinRun) continue;
-                    const int b = 31 - __clz(len);
-                    if (pass == 0 ? b >= bmin : b == bmin - 1) {
-                        const int k = atomicAdd(&wci[1], 1);
-                        if (k < nslots) {
-                            hs_of[t] = (short)k;
-                            ls[k] = cur[t] >> 2;
-                            rend[k] = run_end(t);
-                            hcol[k] = t;
-                            vmask[2 * k] = vmask[2 * k + 1] = 0u;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-            if (threadIdx.x == 0) {
-                if (wc_diag & 1) wcd[0] = wcd[1] = wcd[2] = 0, wcd[3] = wci[0];
-                wci[1] = min(wci[1], nslots), wci[0] = 0;  // [0]: task count
-            }
-        }
-    }
     __syncthreads();
     // the batches of count workgroups sb * grp .. (< nblk), in order:
     // batch it * nblk + sb * grp + j for j < gcnt, it = 0, 1, ...
@@ -471,39 +401,16 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                     atomicMax(&cm[t * NOUT], c0);
                     if (NOUT == 2) atomicMax(&cm[t * NOUT + 1], c1);
                 }
-                if constexpr (kWcOk) {
-                    const int hs = nslots > 0 && col == t ? (int)hs_of[t] : -1;
-                    if (hs >= 0 && (slot >> 2) - ls[hs] < 2) {  // park it in the run's ring
-                        const int line = slot >> 2, q = 2 * hs + (line & 1);
-                        float4* rl = ring + q * 8 + 2 * (slot & 3);
-                        if (first) {
-                            rl[0] = make_float4(first_lu[k], first_lv[k], ph[k], first_c0[k]);
-                        } else {
-                            rl[0] = make_float4((float)(U - corner_x(g, max(b.x0, tx * kTile))),
-                                                (float)(V - corner_y(g, max(b.y0, ty * kTile))),
-                                                ph[k], cf0);
-                        }
-                        rl[1] = make_float4(cf1, __int_as_float(p), band, __uint_as_float(bp));
-                        atomicOr(&vmask[q], 1u << (slot & 3));
-                        if ((slot & 3) == 3 || slot == rend[hs] - 1)  // the line's last slot
-                            tasks[atomicAdd(&wci[0], 1)] = make_int2(line, q);
-                        if (wc_diag & 1) atomicAdd(&wcd[0], 1);
-                        return;
-                    }
-                    if ((wc_diag & 1) && hs >= 0) atomicAdd(&wcd[2], 1);
-                }
                 if (first) {
                     first_slot[k] = slot;  // written by the paired store below
                     first_box[k] = bp;
                 } else {
-                    if (!(wc_diag & 2)) {  // (ablation 2: no direct stores; wrong maps)
                     rec_store(&recs[2 * (long long)slot],
                               make_float4((float)(U - corner_x(g, max(b.x0, tx * kTile))),
                                           (float)(V - corner_y(g, max(b.y0, ty * kTile))),
                                           ph[k], cf0));
                     rec_store(&recs[2 * (long long)slot + 1],
                               make_float4(cf1, __int_as_float(p), band, __uint_as_float(bp)));
-                    }
                 }
             };
             if (tx1 - tx0 <= 1 && ty1 - ty0 <= 1) {  // at most 2 x 2 tiles: straight-line
@@ -536,29 +443,11 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                 int src = half * 32 + (lane >> 1);
                 int slot = __shfl(first_slot[k], src);
                 float4 val = st[(lane & 1) * 72 + src];
-                if (slot >= 0 && !(wc_diag & 2)) rec_store(&recs[2 * (long long)slot + (lane & 1)], val);
+                if (slot >= 0) rec_store(&recs[2 * (long long)slot + (lane & 1)], val);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             first_slot[k] = -1;
-        }
-        if constexpr (kWcOk) {
-            if (nslots > 0) {  // flush the lines finished in this batch: 8 lanes per line
-                __syncthreads();
-                const int nt = wci[0];
-                if ((wc_diag & 1) && threadIdx.x == 0) wcd[1] += nt;
-                for (int i = threadIdx.x >> 3; i < nt; i += kScatterBlock / 8) {
-                    const int2 tk = tasks[i];
-                    const int j = threadIdx.x & 7;
-                    if (((vmask[tk.y] >> (j >> 1)) & 1u) && !(wc_diag & 4))
-                        rec_store(&recs[8 * (long long)tk.x + j], ring[tk.y * 8 + j]);
-                }
-                __syncthreads();
-                for (int i = threadIdx.x; i < nt; i += kScatterBlock) vmask[tasks[i].y] = 0u;
-                for (int k = threadIdx.x; k < wci[1]; k += kScatterBlock) ls[k] = cur[hcol[k]] >> 2;
-                if (threadIdx.x == 0) wci[0] = 0;  // every thread read nt before the barrier
-                __syncthreads();
-            }
         }
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
@@ -577,10 +466,6 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                 for (int k = 0; k < kUnroll; ++k) px[j][k] = nx_[j][k];
     }
     __syncthreads();
-    if constexpr (kWcOk)
-        if ((wc_diag & 1) && nslots > 0 && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
-            printf("asp wc: block %d slots %d bmin %d parked %d flushed lines %d bypassed %d\n",
-                   (int)blockIdx.x, wci[1], wcd[3], wcd[0], wcd[1], wcd[2]);
     if constexpr (ACC == kAccFix) {
         unsigned* out = cmx + (long long)blockIdx.x * g.ntiles * NOUT;  // per scatter block
         for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kScatterBlock) out[t] = cm[t];
@@ -2040,19 +1925,8 @@ static inline size_t merge_cap(const Grid& g) { return (size_t)g.ntiles + 16; }
 static inline size_t scatter_lds_base(const Grid& g) {
     return (size_t)2 * g.ntiles * sizeof(int) + (size_t)(kScatterBlock / 64) * kStageF4 * sizeof(float4);
 }
-// Write-combining slots of the scatter (two-line LDS rings of the longest runs): as many as
-// the CU's 160 KiB hold beside the cursors and staging; ASP_WC_SLOTS caps them (0 = off).
-static inline int scatter_wc_slots(const Grid& g) {
-    const char* e = getenv("ASP_WC_SLOTS");  // read per call: same-process A/Bs
-    const int cap = e ? std::max(0, atoi(e)) : 1 << 20;
-    const long long fixed = (long long)scatter_lds_base(g) + ((g.ntiles + 1) & ~1) * 2 + 38 * 4;
-    const long long room = 160LL * 1024 - fixed;
-    const int n = room > 0 ? (int)(room / kWcSlotBytes) & ~31 : 0;
-    return std::min(n, cap) >= 32 ? std::min(n, cap) : 0;
-}
-static inline size_t scatter_lds(const Grid& g, int nout, bool det, int nslots) {
-    return scatter_lds_base(g) + (det ? (size_t)g.ntiles * nout * sizeof(unsigned) : 0) +
-           (nslots > 0 ? (size_t)nslots * kWcSlotBytes + ((g.ntiles + 1) & ~1) * 2 + 38 * 4 : 0);
+static inline size_t scatter_lds(const Grid& g, int nout, bool det) {
+    return scatter_lds_base(g) + (det ? (size_t)g.ntiles * nout * sizeof(unsigned) : 0);
 }
 
 // Dynamic LDS above the 64 KiB default needs the kernel's attribute raised once.
@@ -2075,15 +1949,13 @@ static int scatter_variant(const Grid& g, const Src64& s, Workspace& ws, const P
                            const float* a1, long long rec_cap, int wide_cap, hipStream_t st,
                            const XArgs& xa) {
     int* dc = (int*)ws.counters.p;
-    const int nslots = (ACC == kAccF64 && NX == 0) ? scatter_wc_slots(g) : 0;
-    const size_t lds = scatter_lds(g, NOUT, ACC == kAccFix, nslots);
-    ASP_TRY(allow_lds(k_scatter<KID, NOUT, ACC, CULL, SRC, PROBE, NX>, (size_t)160 * 1024));
+    const size_t lds = scatter_lds(g, NOUT, ACC == kAccFix);
     hipLaunchKernelGGL((k_scatter<KID, NOUT, ACC, CULL, SRC, PROBE, NX>), dim3((unsigned)pl.nblk_s),
                        dim3(kScatterBlock), lds, st, u, v, h, a0,
                        a1, pl.n, pl.nblk, g, s, (const int*)ws.hist.p,
                        (const long long*)ws.tile_start.p, (const int*)ws.tile_total.p,
                        (float4*)ws.recs.p, (unsigned*)ws.cmx.p, (int*)ws.wide.p, dc, pl.grp,
-                       rec_cap, wide_cap, xa, nslots, getenv("ASP_WC_DIAG") ? atoi(getenv("ASP_WC_DIAG")) : 0);
+                       rec_cap, wide_cap, xa);
     ASP_LAUNCHED();
     return ASP_OK;
 }
