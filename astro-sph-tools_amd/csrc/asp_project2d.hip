@@ -293,18 +293,29 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     };
     long long c = 0;
     const long long p0 = batch_base(0);
+    // A lane's particles of the batch at base: base + k * kScatterBlock + threadIdx.x
+    // (coalesced dword loads).  Every load is unconditional -- index clamped to the last
+    // particle, h = 0 past the end (no footprint) -- so the compiler can count the loads in
+    // flight: with the vector-or-scalar load branches of load_vec it put s_waitcnt vmcnt(0)
+    // right after issuing the NEXT batch's loads, so each batch waited a full memory latency
+    // for its prefetch plus every store still pending (round 5).
+    auto pidx = [&](long long b, int k) { return b + (long long)k * kScatterBlock + threadIdx.x; };
+    auto ld = [&](const float* __restrict__ a, long long b, float* out) {
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k) out[k] = a[min(pidx(b, k), n - 1)];
+    };
     // Software pipeline: issue the next batch's loads BEFORE this batch's record stores,
     // so waiting for them (vmcnt counts loads and stores in issue order) never waits on
     // the scattered stores.
     float pu[kUnroll], pv[kUnroll], ph[kUnroll], pa0[kUnroll], pa1[kUnroll];
     double pU[kUnroll], pV[kUnroll];  // SRC 1: the exact coordinates
-    // SRC 1: the fp64 coordinates of U consecutive particles (index clamped to the array:
+    // SRC 1: the fp64 coordinates of the lane's particles (index clamped to the array:
     // unconditional loads; lanes past the end are never binned)
     auto load_src = [&](long long b, double* dU, double* dV) {
         if constexpr (SRC == 1) {
 #pragma unroll
             for (int k = 0; k < kUnroll; ++k) {
-                const long long q = min(b + (long long)threadIdx.x * kUnroll + k, n - 1) * s.stride;
+                const long long q = min(pidx(b, k), n - 1) * s.stride;
                 dU[k] = s.u64[q];
                 dV[k] = s.v64[q];
             }
@@ -312,6 +323,18 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
 #pragma unroll
             for (int k = 0; k < kUnroll; ++k) dU[k] = dV[k] = 0.0;
         }
+    };
+    auto load_all = [&](long long b, float* du, float* dv, float* dh, float* d0, float* d1) {
+        ld(u, b, du);
+        ld(v, b, dv);
+        ld(h, b, dh);
+        ld(a0, b, d0);
+        if constexpr (NOUT == 2) ld(a1, b, d1);
+        else
+#pragma unroll
+            for (int k = 0; k < kUnroll; ++k) d1[k] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k) dh[k] = pidx(b, k) < n ? dh[k] : 0.0f;
     };
     int first_slot[kUnroll];
     // the prepared fields of every particle's first record (the paired store's payload)
@@ -324,34 +347,28 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
         first_c0[k] = first_c1[k] = first_band[k] = first_lu[k] = first_lv[k] = 0.0f;
         first_box[k] = 0u;
     }
-    const bool al = aligned_vec<kUnroll>(u, v, h) && aligned_vec<kUnroll>(a0, NOUT == 2 ? a1 : a0, a0);
     // NX: properties 2..5, loaded with the batch (software-pipelined like the others)
     float px[NX ? 4 : 1][kUnroll];
-    const bool alx = NX && aligned_vec<kUnroll>(xa.a[0], xa.a[1], xa.a[2]) &&
-                     aligned_vec<kUnroll>(xa.a[3], xa.a[3], xa.a[3]);
     auto load_x = [&](long long b, float (&dst)[NX ? 4 : 1][kUnroll]) {
         if constexpr (NX) {
-            const long long q = b + (long long)threadIdx.x * kUnroll;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) load_vec<kUnroll>(xa.a[j], q, n, alx, dst[j]);
+            for (int j = 0; j < 4; ++j) ld(xa.a[j], b, dst[j]);
         }
     };
-    load_batch<kUnroll>(u, v, h, p0, n, al, pu, pv, ph);
-    load_props<NOUT>(a0, a1, p0, n, al, pa0, pa1);
+    load_all(p0, pu, pv, ph, pa0, pa1);
     load_src(p0, pU, pV);
     load_x(p0, px);
     for (long long base = p0, next; base < n; base = next) {
         next = batch_base(++c);
         float nu[kUnroll], nv[kUnroll], nh[kUnroll], na0[kUnroll], na1[kUnroll];
-        load_batch<kUnroll>(u, v, h, next, n, al, nu, nv, nh);
-        load_props<NOUT>(a0, a1, next, n, al, na0, na1);
+        load_all(next, nu, nv, nh, na0, na1);
         double nU[kUnroll], nV[kUnroll];
         load_src(next, nU, nV);
         float nx_[NX ? 4 : 1][kUnroll];
         load_x(next, nx_);
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
-            const int p = (int)(base + (long long)threadIdx.x * kUnroll + k);
+            const int p = (int)pidx(base, k);
             Box b;
             if (!footprint<CULL>(g, s, p, pu[k], pv[k], ph[k], b)) continue;
             // the fixed-point bound is taken over the same fp32 coefficients the deposit
@@ -432,7 +449,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
         const int lane = threadIdx.x & 63;
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
-            const int p = (int)(base + (long long)threadIdx.x * kUnroll + k);
+            const int p = (int)pidx(base, k);
             st[lane] = make_float4(first_lu[k], first_lv[k], ph[k], first_c0[k]);
             st[72 + lane] = make_float4(first_c1[k], __int_as_float(p), first_band[k],
                                         __uint_as_float(first_box[k]));

@@ -136,11 +136,15 @@ __device__ __forceinline__ void load3(const float* __restrict__ x, const float* 
                                       const float* __restrict__ z, const float* __restrict__ h,
                                       long long p, long long p1, float& px, float& py, float& pz,
                                       float& ph) {
-    bool in = p < p1;
-    px = in ? x[p] : 0.0f;
-    py = in ? y[p] : 0.0f;
-    pz = in ? z[p] : 0.0f;
-    ph = in ? h[p] : 0.0f;  // h = 0: no footprint
+    // unconditional loads, index clamped to the range (p1 >= 1): loads under a branch made
+    // the compiler wait (vmcnt(0)) for every load and store in flight at the top of each
+    // batch, the prefetched batch included
+    const long long q = p < p1 ? p : p1 - 1;
+    px = x[q];
+    py = y[q];
+    pz = z[q];
+    const float hq = h[q];
+    ph = p < p1 ? hq : 0.0f;  // h = 0: no footprint
 }
 
 // ----------------------------------------------------------------------------------
@@ -207,14 +211,7 @@ __global__ __launch_bounds__(k3Block) void k3_scatter(
     const long long p1 = inter ? n : min(n, p0 + per_block);
     const Grid3f gf = {(float)g.x_min, (float)g.y_min, (float)g.z_min,
                        (float)g.ipx, (float)g.ipy, (float)g.ipz};
-    float cx, cy, cz, ch, ca;
-    load3(x, y, z, h, p0 + threadIdx.x, p1, cx, cy, cz, ch);
-    ca = p0 + threadIdx.x < p1 ? a[p0 + threadIdx.x] : 0.0f;
-    for (long long base = p0; base < p1; base += stride) {
-        float nx_, ny_, nz_, nh_, na_;
-        long long q = base + stride + threadIdx.x;
-        load3(x, y, z, h, q, p1, nx_, ny_, nz_, nh_);
-        na_ = q < p1 ? a[q] : 0.0f;
+    auto bin = [&](float cx, float cy, float cz, float ch, float ca) {
         Box3 b;
         if (footprint3f(g, gf, cx, cy, cz, ch, b)) {
             float4 r0 = make_float4(cx, cy, cz, ch), r1 = make_float4(ca, 0.0f, 0.0f, 0.0f);
@@ -229,11 +226,23 @@ __global__ __launch_bounds__(k3Block) void k3_scatter(
                         recs[2 * (long long)slot + 1] = r1;
                     }
         }
-        cx = nx_;
-        cy = ny_;
-        cz = nz_;
-        ch = nh_;
-        ca = na_;
+    };
+    // Two particle buffers in ping-pong (no register copies at the loop's back edge, which
+    // made the compiler wait for every load and store in flight before it could issue the
+    // next batch's loads): batch j + 1 is loaded while batch j is binned.
+    float ax, ay, az, ah, aa, bx, by, bz, bh, ba;
+    load3(x, y, z, h, p0 + threadIdx.x, p1, ax, ay, az, ah);
+    aa = a[min(p0 + (long long)threadIdx.x, p1 - 1)];  // (unused where h = 0)
+    for (long long base = p0; base < p1; base += 2 * stride) {
+        long long q = base + stride + threadIdx.x;
+        load3(x, y, z, h, q, p1, bx, by, bz, bh);
+        ba = a[min(q, p1 - 1)];
+        bin(ax, ay, az, ah, aa);
+        if (base + stride >= p1) break;  // block-uniform
+        q = base + 2 * stride + threadIdx.x;
+        load3(x, y, z, h, q, p1, ax, ay, az, ah);
+        aa = a[min(q, p1 - 1)];
+        bin(bx, by, bz, bh, ba);
     }
 }
 
@@ -444,10 +453,17 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         }
         __syncthreads();
         unsigned cr[kRound / k3Block];  // class << 16 | rank, per record of this thread
+        // all of this thread's records of the round loaded first: loads interleaved with
+        // the class counters' LDS atomics were issued one at a time, each waiting a full
+        // memory latency (vmcnt(0)) before the next (round 5)
+        float4 qv[kRound / k3Block];
+#pragma unroll
+        for (int q = 0; q < kRound / k3Block; ++q)
+            qv[q] = recs[2 * (it.start + r0i + min(q * k3Block + (int)threadIdx.x, nr - 1))];
 #pragma unroll
         for (int q = 0; q < kRound / k3Block; ++q) {
             const int i = q * k3Block + (int)threadIdx.x;
-            const float4 q0 = recs[2 * (it.start + r0i + min(i, nr - 1))];
+            const float4 q0 = qv[q];
             Box3 b;
             int c = -1;
             if (i < nr && footprint3f(g, gf, q0.x, q0.y, q0.z, q0.w, b)) {

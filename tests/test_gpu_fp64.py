@@ -111,7 +111,6 @@ def test_baseline_cfg3_4096_deterministic_components(gpu, oracle):
     components is refused (ASP_ERR_INVALID / ValueError): pixels reached only by kernel
     tails keep a few fixed-point units of weight."""
     import torch
-    from asp_amd._lib import ASPError
     from asp_amd.device import project2d, project2d_f64
     from asp_amd.tools.projections import create_weighted_image, wendland_c2_kernel
     n, G = 2_000_000, 4096
@@ -133,7 +132,7 @@ def test_baseline_cfg3_4096_deterministic_components(gpu, oracle):
                               deterministic=True)
     t = [torch.from_numpy(x.astype(np.float32)).cuda() for x in (pos[:1000, 0], pos[:1000, 1],
                                                                h[:1000], m[:1000] * T[:1000], m[:1000])]
-    with pytest.raises(ASPError, match="DETERMINISTIC"):
+    with pytest.raises(ValueError, match="DETERMINISTIC"):  # ASP_ERR_INVALID
         project2d(*t, image_size=(64, 64), extent=ext, kernel="wendland_c2", ratio=True,
                   deterministic=True)
 

@@ -354,10 +354,16 @@ def test_bitwise_deterministic_and_permutation_invariant(gpu, oracle):
     perm = np.random.default_rng(1).permutation(p["h"].size)
     c = create_image(p["pos"][perm], p["h"][perm], p["m"][perm], (512, 512), 64, 2, *ext, **kw)
     assert np.array_equal(a, b) and np.array_equal(a, c)
-    w1 = create_weighted_image(p["pos"], p["h"], p["m"], p["T"], (512, 512), 64, 2, *ext, **kw)
-    w2 = create_weighted_image(p["pos"][perm], p["h"][perm], p["m"][perm], p["T"][perm],
-                               (512, 512), 64, 2, *ext, **kw)
-    assert np.array_equal(w1, w2)
+    # two fixed-point component maps (no ratio: DESIGN.md §4 -- the library refuses a
+    # fixed-point ratio map) are bitwise permutation invariant as well
+    from asp_amd.device import project2d_f64
+    mT = p["m"] * p["T"]
+    kw2 = dict(image_size=(512, 512), extent=ext, chunk_size=64, deterministic=True)
+    w1 = project2d_f64(p["pos"], p["h"], mT, p["m"], **kw2)
+    w2 = project2d_f64(p["pos"][perm], p["h"][perm], mT[perm], p["m"][perm], **kw2)
+    assert np.array_equal(w1[0], w2[0]) and np.array_equal(w1[1], w2[1])
+    with pytest.raises(ValueError):
+        create_weighted_image(p["pos"], p["h"], p["m"], p["T"], (512, 512), 64, 2, *ext, **kw)
     ref, _ = oracle.project_scatter(p["pos"][:, 0], p["pos"][:, 1], p["h"], p["m"], None,
                                     (512, 512), 64, *ext)
     assert_map_close(a, ref)
@@ -373,15 +379,17 @@ def test_record_placement_trials(gpu, oracle, monkeypatch):
     from asp_amd.tools.projections import indicator_kernel
     p = plummer_f32(300_000, seed=21, h_law="physical")
     ext = (-4.0, 4.0, -4.0, 4.0)
-    kw = dict(deterministic=True)
+    from asp_amd.device import project2d_f64
+    mT = p["m"] * p["T"]
+    kw = dict(image_size=(512, 512), extent=ext, chunk_size=64, deterministic=True)
     monkeypatch.setenv("ASP_PLACEMENT_TRIALS", "0")
     _lib.check(_lib.lib().asp_release(0))
-    a = create_weighted_image(p["pos"], p["h"], p["m"], p["T"], (512, 512), 64, 2, *ext, **kw)
+    a = project2d_f64(p["pos"], p["h"], mT, p["m"], **kw)
     monkeypatch.setenv("ASP_PLACEMENT_TRIALS", "4")
     monkeypatch.setenv("ASP_PLACEMENT_MIN_MB", "0")
     _lib.check(_lib.lib().asp_release(0))
-    b = create_weighted_image(p["pos"], p["h"], p["m"], p["T"], (512, 512), 64, 2, *ext, **kw)
-    assert np.array_equal(a, b)
+    b = project2d_f64(p["pos"], p["h"], mT, p["m"], **kw)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
     _lib.check(_lib.lib().asp_release(0))
     cnt = create_image(p["pos"], p["h"], np.ones_like(p["h"]), (512, 512), 64, 2, *ext,
                        kernel_func=indicator_kernel)
@@ -432,8 +440,9 @@ def test_large_stream_threshold(gpu, oracle, gmin, area, monkeypatch):
     w0, w1 = oracle.project_scatter(pos[:, 0], pos[:, 1], h, A * T, A, (G, G), 64, *ext)
     assert_map_close(s0, w0)
     assert_map_close(s1, w1)
-    dr, d0, d1 = create_weighted_image(pos, h, A, T, (G, G), 64, 2, *ext, return_components=True,
-                                       deterministic=True)
+    from asp_amd.device import project2d_f64
+    d0, d1 = project2d_f64(pos, h, A * T, A, image_size=(G, G), extent=(-1.0, 1.0, -1.0, 1.0),
+                           chunk_size=64, deterministic=True)
     assert_map_close(d0, w0)
     assert_map_close(d1, w1)
 
