@@ -69,6 +69,11 @@ constexpr int kCountUnroll = ASP_COUNT_UNROLL;  // particles per lane and batch 
 constexpr int kScatterBlock = ASP_SCATTER_BLOCK;
 constexpr int kScatterGroup = ASP_SCATTER_GROUP_DEF;
 constexpr int kUnroll = (int)(kCountBlock * kCountUnroll / kScatterBlock);  // particles per lane and batch in scatter
+// batches a scatter loop iteration takes at once (ASP_SCATTER_BATCHES)
+#ifndef ASP_SCATTER_BATCHES
+#define ASP_SCATTER_BATCHES 2
+#endif
+constexpr int kSB = ASP_SCATTER_BATCHES;
 // Particles per loop iteration of a count / scatter workgroup (a "batch").  Batches are
 // dealt to the count workgroups round-robin (batch j to workgroup j % nblk; the scatter
 // workgroup of count workgroups sb*grp.. takes their batches in order), so at any moment
@@ -291,84 +296,87 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     auto batch_base = [&](long long c) {
         return ((c / gcnt) * nblk + sb * grp + c % gcnt) * kBatch;
     };
-    long long c = 0;
-    const long long p0 = batch_base(0);
-    // A lane's particles of the batch at base: base + k * kScatterBlock + threadIdx.x
-    // (coalesced dword loads).  Every load is unconditional -- index clamped to the last
-    // particle, h = 0 past the end (no footprint) -- so the compiler can count the loads in
-    // flight: with the vector-or-scalar load branches of load_vec it put s_waitcnt vmcnt(0)
-    // right after issuing the NEXT batch's loads, so each batch waited a full memory latency
-    // for its prefetch plus every store still pending (round 5).
-    auto pidx = [&](long long b, int k) { return b + (long long)k * kScatterBlock + threadIdx.x; };
-    auto ld = [&](const float* __restrict__ a, long long b, float* out) {
-#pragma unroll
-        for (int k = 0; k < kUnroll; ++k) out[k] = a[min(pidx(b, k), n - 1)];
+    // A loop iteration takes kSB consecutive batches of this workgroup (kLane particles per
+    // lane): twice the bytes in flight per wave of one batch, and half as many waits for
+    // the previous iteration's stores (gfx950 counts loads and stores in one vmcnt) -- the
+    // scatter runs one 8-wave workgroup per CU, so its loads are latency-bound otherwise
+    // (round 5).  Lane particle k of iteration c: batch c * kSB + k / kUnroll,
+    // base + (k % kUnroll) * kScatterBlock + threadIdx.x (coalesced dword loads).  Every load
+    // is unconditional -- index clamped to the last particle, h = 0 past the end (no
+    // footprint) -- so the compiler can count the loads in flight: with load_vec's
+    // vector-or-scalar branches it put s_waitcnt vmcnt(0) right after issuing the NEXT
+    // batch's loads.
+    constexpr int kLane = kUnroll * kSB;
+    auto pidx = [&](long long c, int k) {
+        return batch_base(c * kSB + k / kUnroll) + (long long)(k % kUnroll) * kScatterBlock +
+               threadIdx.x;
     };
-    // Software pipeline: issue the next batch's loads BEFORE this batch's record stores,
-    // so waiting for them (vmcnt counts loads and stores in issue order) never waits on
-    // the scattered stores.
-    float pu[kUnroll], pv[kUnroll], ph[kUnroll], pa0[kUnroll], pa1[kUnroll];
-    double pU[kUnroll], pV[kUnroll];  // SRC 1: the exact coordinates
+    auto ld = [&](const float* __restrict__ a, long long c, float* out) {
+#pragma unroll
+        for (int k = 0; k < kLane; ++k) out[k] = a[min(pidx(c, k), n - 1)];
+    };
+    // Software pipeline: issue the next iteration's loads BEFORE this one's record stores.
+    float pu[kLane], pv[kLane], ph[kLane], pa0[kLane], pa1[kLane];
+    double pU[kLane], pV[kLane];  // SRC 1: the exact coordinates
     // SRC 1: the fp64 coordinates of the lane's particles (index clamped to the array:
     // unconditional loads; lanes past the end are never binned)
-    auto load_src = [&](long long b, double* dU, double* dV) {
+    auto load_src = [&](long long c, double* dU, double* dV) {
         if constexpr (SRC == 1) {
 #pragma unroll
-            for (int k = 0; k < kUnroll; ++k) {
-                const long long q = min(pidx(b, k), n - 1) * s.stride;
+            for (int k = 0; k < kLane; ++k) {
+                const long long q = min(pidx(c, k), n - 1) * s.stride;
                 dU[k] = s.u64[q];
                 dV[k] = s.v64[q];
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < kUnroll; ++k) dU[k] = dV[k] = 0.0;
+            for (int k = 0; k < kLane; ++k) dU[k] = dV[k] = 0.0;
         }
     };
-    auto load_all = [&](long long b, float* du, float* dv, float* dh, float* d0, float* d1) {
-        ld(u, b, du);
-        ld(v, b, dv);
-        ld(h, b, dh);
-        ld(a0, b, d0);
-        if constexpr (NOUT == 2) ld(a1, b, d1);
+    auto load_all = [&](long long c, float* du, float* dv, float* dh, float* d0, float* d1) {
+        ld(u, c, du);
+        ld(v, c, dv);
+        ld(h, c, dh);
+        ld(a0, c, d0);
+        if constexpr (NOUT == 2) ld(a1, c, d1);
         else
 #pragma unroll
-            for (int k = 0; k < kUnroll; ++k) d1[k] = 0.0f;
+            for (int k = 0; k < kLane; ++k) d1[k] = 0.0f;
 #pragma unroll
-        for (int k = 0; k < kUnroll; ++k) dh[k] = pidx(b, k) < n ? dh[k] : 0.0f;
+        for (int k = 0; k < kLane; ++k) dh[k] = pidx(c, k) < n ? dh[k] : 0.0f;
     };
-    int first_slot[kUnroll];
+    int first_slot[kLane];
     // the prepared fields of every particle's first record (the paired store's payload)
-    float first_c0[kUnroll], first_c1[kUnroll], first_band[kUnroll], first_lu[kUnroll],
-        first_lv[kUnroll];
-    unsigned first_box[kUnroll];
+    float first_c0[kLane], first_c1[kLane], first_band[kLane], first_lu[kLane],
+        first_lv[kLane];
+    unsigned first_box[kLane];
 #pragma unroll
-    for (int k = 0; k < kUnroll; ++k) {
+    for (int k = 0; k < kLane; ++k) {
         first_slot[k] = -1;
         first_c0[k] = first_c1[k] = first_band[k] = first_lu[k] = first_lv[k] = 0.0f;
         first_box[k] = 0u;
     }
     // NX: properties 2..5, loaded with the batch (software-pipelined like the others)
-    float px[NX ? 4 : 1][kUnroll];
-    auto load_x = [&](long long b, float (&dst)[NX ? 4 : 1][kUnroll]) {
+    float px[NX ? 4 : 1][kLane];
+    auto load_x = [&](long long c, float (&dst)[NX ? 4 : 1][kLane]) {
         if constexpr (NX) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) ld(xa.a[j], b, dst[j]);
+            for (int j = 0; j < 4; ++j) ld(xa.a[j], c, dst[j]);
         }
     };
-    load_all(p0, pu, pv, ph, pa0, pa1);
-    load_src(p0, pU, pV);
-    load_x(p0, px);
-    for (long long base = p0, next; base < n; base = next) {
-        next = batch_base(++c);
-        float nu[kUnroll], nv[kUnroll], nh[kUnroll], na0[kUnroll], na1[kUnroll];
-        load_all(next, nu, nv, nh, na0, na1);
-        double nU[kUnroll], nV[kUnroll];
-        load_src(next, nU, nV);
-        float nx_[NX ? 4 : 1][kUnroll];
-        load_x(next, nx_);
+    load_all(0, pu, pv, ph, pa0, pa1);
+    load_src(0, pU, pV);
+    load_x(0, px);
+    for (long long c = 0; batch_base(c * kSB) < n; ++c) {
+        float nu[kLane], nv[kLane], nh[kLane], na0[kLane], na1[kLane];
+        load_all(c + 1, nu, nv, nh, na0, na1);
+        double nU[kLane], nV[kLane];
+        load_src(c + 1, nU, nV);
+        float nx_[NX ? 4 : 1][kLane];
+        load_x(c + 1, nx_);
 #pragma unroll
-        for (int k = 0; k < kUnroll; ++k) {
-            const int p = (int)pidx(base, k);
+        for (int k = 0; k < kLane; ++k) {
+            const int p = (int)pidx(c, k);
             Box b;
             if (!footprint<CULL>(g, s, p, pu[k], pv[k], ph[k], b)) continue;
             // the fixed-point bound is taken over the same fp32 coefficients the deposit
@@ -448,8 +456,8 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
         float4* st = stage + (threadIdx.x >> 6) * kStageF4;
         const int lane = threadIdx.x & 63;
 #pragma unroll
-        for (int k = 0; k < kUnroll; ++k) {
-            const int p = (int)pidx(base, k);
+        for (int k = 0; k < kLane; ++k) {
+            const int p = (int)pidx(c, k);
             st[lane] = make_float4(first_lu[k], first_lv[k], ph[k], first_c0[k]);
             st[72 + lane] = make_float4(first_c1[k], __int_as_float(p), first_band[k],
                                         __uint_as_float(first_box[k]));
@@ -467,7 +475,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             first_slot[k] = -1;
         }
 #pragma unroll
-        for (int k = 0; k < kUnroll; ++k) {
+        for (int k = 0; k < kLane; ++k) {
             pu[k] = nu[k];
             pv[k] = nv[k];
             ph[k] = nh[k];
@@ -480,7 +488,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int k = 0; k < kUnroll; ++k) px[j][k] = nx_[j][k];
+                for (int k = 0; k < kLane; ++k) px[j][k] = nx_[j][k];
     }
     __syncthreads();
     if constexpr (ACC == kAccFix) {
