@@ -69,9 +69,10 @@ constexpr int kCountUnroll = ASP_COUNT_UNROLL;  // particles per lane and batch 
 constexpr int kScatterBlock = ASP_SCATTER_BLOCK;
 constexpr int kScatterGroup = ASP_SCATTER_GROUP_DEF;
 constexpr int kUnroll = (int)(kCountBlock * kCountUnroll / kScatterBlock);  // particles per lane and batch in scatter
-// batches a scatter loop iteration takes at once (ASP_SCATTER_BATCHES)
+// batches a scatter loop iteration takes at once (ASP_SCATTER_BATCHES, an A/B build switch;
+// 1 measured best)
 #ifndef ASP_SCATTER_BATCHES
-#define ASP_SCATTER_BATCHES 2
+#define ASP_SCATTER_BATCHES 1
 #endif
 constexpr int kSB = ASP_SCATTER_BATCHES;
 // Particles per loop iteration of a count / scatter workgroup (a "batch").  Batches are
@@ -297,10 +298,11 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
         return ((c / gcnt) * nblk + sb * grp + c % gcnt) * kBatch;
     };
     // A loop iteration takes kSB consecutive batches of this workgroup (kLane particles per
-    // lane): twice the bytes in flight per wave of one batch, and half as many waits for
-    // the previous iteration's stores (gfx950 counts loads and stores in one vmcnt) -- the
-    // scatter runs one 8-wave workgroup per CU, so its loads are latency-bound otherwise
-    // (round 5).  Lane particle k of iteration c: batch c * kSB + k / kUnroll,
+    // lane).  More batches per iteration put more loads in flight per wave and wait less
+    // often for the previous iteration's stores (gfx950 counts loads and stores in one
+    // vmcnt), but measured slower: 1 / 2 / 4 batches 1.756 / 1.794 / 1.918 ms (same box,
+    // round 5) -- the scatter is bound by its stores, not by load latency.
+    // Lane particle k of iteration c: batch c * kSB + k / kUnroll,
     // base + (k % kUnroll) * kScatterBlock + threadIdx.x (coalesced dword loads).  Every load
     // is unconditional -- index clamped to the last particle, h = 0 past the end (no
     // footprint) -- so the compiler can count the loads in flight: with load_vec's
