@@ -425,3 +425,79 @@ def test_rowslab_world2():
     assert out[1]["dst"].shape == (R[2] - R[1], GR)  # rank 1 keeps its own slab
     # every particle reaches some rank; the wide physical-h halo is duplicated, not all of it
     assert x.numel() <= out[0]["routed"] + out[1]["routed"] < 2 * x.numel()
+
+
+def _rows_subgroup_worker(rank, world, port, q):
+    """World 3; the row-slab map runs on the SUBGROUP {1, 2} (group ranks 0, 1 = global 1,
+    2), each member holding one spatial half of the particles in x (a skewed reader split)."""
+    import sys
+    sys.path.insert(0, PKG_ROOT)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from asp_amd.distributed import project2d_rowslab, row_slabs
+        grp = dist.new_group([1, 2])  # every rank creates it
+        res = {}
+        if rank in (1, 2):
+            x, y, z, h, m, T = _data()
+            # skewed split: group rank 0 gets x < 0, group rank 1 x >= 0
+            keep = (x < 0) if rank == 1 else (x >= 0)
+            sl = [t[keep].contiguous() for t in (x, y, h, m, T)]
+            try:  # two maps but one gather: refused (ADVICE r04)
+                project2d_rowslab(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3], image_size=(GR, GR),
+                                  extent=EXT, chunk_size=16, kernel="cubic", gather="all",
+                                  group=grp, projector=_oracle_rows)
+                res["refused"] = False
+            except ValueError:
+                res["refused"] = True
+            res["bounds"] = row_slabs(GR, 2, sl[0], EXT[:2], group=grp)
+            got, _ = project2d_rowslab(sl[0], sl[1], sl[2], sl[3] * sl[4], sl[3],
+                                       image_size=(GR, GR), extent=EXT, chunk_size=16,
+                                       kernel="cubic", ratio=True, gather="dst", dst=0,
+                                       group=grp, projector=_oracle_rows)
+            res["dst"] = got.numpy().copy()
+        dist.barrier()
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rowslab_subgroup_global_peers_and_skewed_split():
+    """The row-slab gather on a process subgroup sends to / receives from the members'
+    GLOBAL ranks (world 3, group {1, 2}, dst = group rank 0 = global rank 1); the row bounds
+    balance the UNION of the members' particles although each holds one spatial half (one
+    rank's sample alone would put the bound at an edge of its own half); and two component
+    maps with one gather are refused."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rows_subgroup_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0] == {}
+    assert out[1]["refused"] and out[2]["refused"]
+    R = out[1]["bounds"]
+    assert R == out[2]["bounds"]
+    x, y, z, h, m, T = _data()
+    # the union's median row: the bound must sit near it (equal counts per slab)
+    rows = np.floor((x.numpy().astype(np.float64) - EXT[0]) / ((EXT[1] - EXT[0]) / GR))
+    rows = np.clip(rows, 0, GR - 1)
+    frac_below = float(np.mean(rows < R[1]))
+    assert 0.45 < frac_below < 0.55, (R, frac_below)
+    full0, full1 = pyoracle.project_scatter(x.numpy(), y.numpy(), h.numpy(), (m * T).numpy(),
+                                            m.numpy(), (GR, GR), 16, *EXT, kernel="cubic")
+    cov = full1 > 1e-3 * full1.max()
+    want = np.where(full1 != 0, full0 / np.where(full1 != 0, full1, 1), 0.0)
+    np.testing.assert_allclose(out[1]["dst"][cov], want[cov], rtol=1e-4)  # the full map
+    assert out[2]["dst"].shape == (R[2] - R[1], GR)                       # its own slab
