@@ -184,6 +184,36 @@ inline int map_slot(int device, hipStream_t st) {
     return s;
 }
 
+// Scatter gate (ASP_SCATTER_GATE=1, read per call): with maps on two streams (two slots),
+// a map's count and scans may run beside the previous map's deposit, but its scatter
+// waits for that deposit -- the scatter and the deposit both stream GBs through the memory
+// system and slowed each other when fully overlapped.  The event of
+// the most recent map's deposit end, per device, with the stream that recorded it.
+struct DepositGate {
+    std::mutex mu;
+    hipEvent_t ev = nullptr;
+    hipStream_t st = nullptr;
+};
+inline DepositGate g_gate[64];
+inline bool scatter_gate_on() {
+    const char* e = getenv("ASP_SCATTER_GATE");
+    return e && atoi(e) != 0;
+}
+inline int gate_wait(int device, hipStream_t st) {  // before a map's scatter
+    DepositGate& G = g_gate[device];
+    std::lock_guard<std::mutex> lock(G.mu);
+    if (G.ev && G.st != st) ASP_HIP(hipStreamWaitEvent(st, G.ev, 0));
+    return ASP_OK;
+}
+inline int gate_record(int device, hipStream_t st) {  // after a map's deposit
+    DepositGate& G = g_gate[device];
+    std::lock_guard<std::mutex> lock(G.mu);
+    if (!G.ev) ASP_HIP(hipEventCreateWithFlags(&G.ev, hipEventDisableTiming));
+    ASP_HIP(hipEventRecord(G.ev, st));
+    G.st = st;
+    return ASP_OK;
+}
+
 inline int set_device(int device) {
     int ndev = 0;
     ASP_HIP(hipGetDeviceCount(&ndev));

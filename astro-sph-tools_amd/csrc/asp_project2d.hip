@@ -2238,6 +2238,8 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     // the scatter behind it on st need not wait for the copy's own latency.
     ASP_TRY(ensure_side(ws));
     ASP_HIP(hipEventRecord(ws.scan_ev, st));
+    int gate_dev = -1;  // ASP_SCATTER_GATE: this map's scatter after the last map's deposit
+    if (scatter_gate_on() && hipGetDevice(&gate_dev) == hipSuccess) ASP_TRY(gate_wait(gate_dev, st));
     ASP_HIP(hipStreamWaitEvent(ws.side, ws.scan_ev, 0));
     ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, (size_t)cNum * sizeof(int), hipMemcpyDeviceToHost,
                            ws.side));
@@ -2328,6 +2330,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
 #undef ASP_XP
         if (rc != ASP_OK) return rc;
     }
+    if (gate_dev >= 0) ASP_TRY(gate_record(gate_dev, st));
     for (int k = 9; k <= 12; ++k) ws.stats[k] = 0;  // the evals diagnostic of THIS pass only
     if (getenv("ASP_COUNT_EVALS")) {  // diagnostic: the deposit kernels' lane-slots
         ASP_TRY(ensure(ws.aux[5], 3 * sizeof(unsigned long long)));

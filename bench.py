@@ -95,11 +95,13 @@ def parse():
     ap.add_argument("--cube", type=int, default=512, help="cube edge (voxels), --workload cube")
     ap.add_argument("--streams", type=int, default=0,
                     help="HIP streams consecutive maps alternate between (each its own "
-                         "workspace slot in the library), so map i + 1's launches overlap "
-                         "map i's tail; 1 = one stream, maps strictly in sequence; 0 (auto) "
-                         "= 2 for a rank's share of <= 3e7 particles (the N >= 4 shards: "
-                         "0.561 -> 0.518 ms at 1.25e7), else 1 (10^8: 3.28 vs 3.43 ms, the "
-                         "kernels already fill the GPU; DESIGN.md §9)")
+                         "workspace slot in the library), so map i + 1's binning and scatter "
+                         "run beside map i's deposit (store-bound and LDS-bound kernels "
+                         "sharing the CUs); 1 = one stream, maps strictly in sequence; 0 "
+                         "(auto) = 2, with the scatter gated behind the previous map's "
+                         "deposit (ASP_SCATTER_GATE) for a rank's share of <= 2e7 particles.  "
+                         "Same box, round 5: 10^8 3.25 -> 3.11 ms, 5e7 1.69 -> 1.59, 2.5e7 "
+                         "0.94 -> 0.86, 1.25e7 (gated) 0.58 -> 0.57 (DESIGN.md §7, §18)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="N > 1: wait for each map's collective before the next map")
     ap.add_argument("--no-stage-events", dest="stage_events", action="store_false",
@@ -766,7 +768,10 @@ def main():
     # Consecutive maps alternate between --streams HIP streams (each with its own output
     # buffer; the library gives each stream its own workspace slot): the binning of map
     # i + 1 runs beside the deposit of map i.  --streams 1: one stream.
-    ns = args.streams if args.streams > 0 else (2 if n_local <= 30_000_000 else 1)
+    ns = args.streams if args.streams > 0 else 2
+    if args.streams == 0 and n_local <= 20_000_000:
+        os.environ["ASP_SCATTER_GATE"] = "1"  # small shares: scatter after the last deposit
+    gated = ns > 1 and os.environ.get("ASP_SCATTER_GATE", "0") not in ("", "0")
     streams = ([torch.cuda.current_stream(dev)] if ns == 1 else
                [torch.cuda.Stream(device=dev) for _ in range(ns)])
     nbuf = max(ns, 2 if (world > 1 and args.pipeline) else 1)
@@ -969,7 +974,7 @@ def main():
                        **({"row_bounds": R} if R is not None else {})} if world > 1 else {}),
                    "accumulation": "int64 fixed point" if args.deterministic else "fp64",
                    "collective_overlap": world > 1 and args.pipeline,
-                   "streams": ns,
+                   "streams": ns, "scatter_gate": gated,
                    **({"slab_weight": args.slab_weight,
                        "collective": args.op if R is None else
                        ("all_gather" if args.rows_gather == "all" else "p2p_gather"),
@@ -998,7 +1003,12 @@ def main():
                      "bytes_alg_per_launch": bytes_alg,
                      "kernel_ms_per_step": round(dom_ms, 4),
                      "kernel_launches_timed": launched[dom][1],
-                     "pipeline_frac": round(bytes_alg / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                     "pipeline_frac": round(bytes_alg / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     **({"concurrency_note": f"maps alternate between {ns} HIP streams: this "
+                         "kernel's launches run beside the other stream's kernels (the "
+                         "previous map's deposit), so its per-launch time includes sharing "
+                         "the CUs and HBM; pipeline_frac (the whole map per step) is the "
+                         "measure of the overlapped pipeline"} if ns > 1 else {})},
         "stages": stages,
         "records_per_particle": round(st["records"] / max(1, n_local), 4),
         "work_items": st["items"], "wide_particles": st["wide"], "large_records": st["large"],

@@ -9,7 +9,10 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_two_stream_maps_equal_serial(gpu, oracle):
+@pytest.mark.parametrize("gate", ["0", "1"])
+def test_two_stream_maps_equal_serial(gpu, oracle, gate, monkeypatch):
+    # gate "1": each map's scatter waits for the previous map's deposit (ASP_SCATTER_GATE)
+    monkeypatch.setenv("ASP_SCATTER_GATE", gate)
     import torch
     from asp_amd import _lib
     from asp_amd.device import project2d
