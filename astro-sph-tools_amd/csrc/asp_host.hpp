@@ -155,7 +155,10 @@ inline Workspace g_ws[64];
 // stream takes the least recently used slot.  Within a slot calls stay ordered (ws_begin
 // waits for the slot's previous call); across slots the caller's streams order the work,
 // as for any two HIP streams.  ASP_MAP_SLOTS=1: one slot (every call ordered).
-constexpr int kMapSlots = 2;
+#ifndef ASP_MAP_SLOTS_MAX  // (an A/B build switch: 3 slots measured in round 5)
+#define ASP_MAP_SLOTS_MAX 2
+#endif
+constexpr int kMapSlots = ASP_MAP_SLOTS_MAX;
 inline Workspace g_ws_alt[64][kMapSlots - 1];
 struct SlotTable {
     std::mutex mu;
