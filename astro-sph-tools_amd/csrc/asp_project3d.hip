@@ -849,9 +849,12 @@ static int project3d(const float* x, const float* y, const float* z, const float
     ASP_HIP(hipGetDeviceCount(&ndev));
     if (device >= ndev) return fail(ASP_ERR_INVALID, "device index out of range");
     ASP_HIP(hipSetDevice(device));
-    Workspace& ws = g_ws[device];
-    std::lock_guard<std::mutex> lock(ws.mu);
     hipStream_t st = (hipStream_t)stream;
+    // a workspace slot per stream, as the 2-D maps have (asp_host.hpp map_slot): cubes on
+    // two streams overlap -- one cube's store-bound scatter beside the other's VALU-bound
+    // deposit (round 5)
+    Workspace& ws = slot_ws(device, map_slot(device, st));
+    std::lock_guard<std::mutex> lock(ws.mu);
     ASP_TRY(ws_begin(ws, st));
     WsEnd ws_end_(ws, st);
     const bool dev = flags & ASP_F_DEVICE_PTRS;
@@ -934,6 +937,10 @@ static int project3d(const float* x, const float* y, const float* z, const float
     ws.stats[6] = agg[2];
     ws.stats[7] = agg[3];
     ws.stats[8] = n > 0 ? 1 : 0;
+    if (&ws != &g_ws[device]) {  // asp_last_stats reads slot 0 (under its lock, as in 2-D)
+        std::lock_guard<std::mutex> lk(g_ws[device].mu);
+        std::copy(ws.stats, ws.stats + kNStats, g_ws[device].stats);
+    }
     return ws_end_.finish();
 }
 

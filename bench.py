@@ -271,14 +271,26 @@ def run_cube(args, world, rank, local, dev):
         d = {k: v[keep].contiguous() for k, v in d.items()}
     x, y, z, h, m = d["x"], d["y"], d["z"], d["h"], d["m"]
     n_local = x.shape[0]
-    out = torch.empty((C, C, K[rank + 1] - K[rank]), dtype=torch.float32, device=dev)
+    # consecutive cubes alternate between --streams HIP streams (0 = auto = 2), each with
+    # its own output and library workspace slot: one cube's store-bound scatter runs beside
+    # the previous cube's VALU-bound deposit
+    ns = args.streams if args.streams > 0 else 2
+    streams = ([torch.cuda.current_stream(dev)] if ns == 1 else
+               [torch.cuda.Stream(device=dev) for _ in range(ns)])
+    outs = [torch.empty((C, C, K[rank + 1] - K[rank]), dtype=torch.float32, device=dev)
+            for _ in range(ns)]
     torch.cuda.synchronize()
     if not args.quiet:
         log(f"[rank {rank}] cube data ready: {n_local} particles in {time.time() - t0:.1f}s")
+    it = [0]
 
     def step():
-        project3d(x, y, z, h, m, cube_size=(C, C, C), extent=ext, kernel=kernel,
-                  planes=(K[rank], K[rank + 1]), out=out)
+        k = it[0]
+        it[0] += 1
+        with torch.cuda.stream(streams[k % ns]):
+            project3d(x, y, z, h, m, cube_size=(C, C, C), extent=ext, kernel=kernel,
+                      planes=(K[rank], K[rank + 1]), out=outs[k % ns])
+        return outs[k % ns]
 
     for _ in range(args.warmup):
         step()
@@ -289,7 +301,7 @@ def run_cube(args, world, rank, local, dev):
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        out = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -325,7 +337,7 @@ def run_cube(args, world, rank, local, dev):
         "data": "synthetic Plummer sphere (a=1, M=1, seed 0, physical h) generated in HBM",
         "config": {"workload": f"cfg5: {args.n:.0e} particles -> {C}^3 density cube, {kernel}, "
                                f"physical h, fp32" + (f", voxel Z-slabs x{world}" if world > 1 else ""),
-                   "particles": args.n, "cube": C, "kernel": kernel,
+                   "particles": args.n, "cube": C, "kernel": kernel, "streams": ns,
                    "parallelism": f"planes{world}" if world > 1 else "single"},
         "particles_per_s": args.n * args.steps / elapsed,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(bytes_alg / (dom_ms * 1e-3) / 1e9, 2),

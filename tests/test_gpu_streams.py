@@ -52,3 +52,36 @@ def test_two_stream_maps_equal_serial(gpu, oracle, gate, monkeypatch):
         again = project2d(*sets[0], **kw)
     torch.cuda.synchronize()
     assert torch.equal(again[0], serial[0][0])
+
+
+def test_two_stream_cubes_equal_serial(gpu):
+    """Cubes on two HIP streams (each its own workspace slot, round 5): every cube equals
+    the one-stream cube -- voxel neighbour counts bit-exact, densities to fp32 rounding (fp64
+    LDS atomics sum in any order) -- for alternating calls of different sizes."""
+    import torch
+    from asp_amd.device import project3d
+    from asp_amd.plummer import plummer_torch
+    dev = torch.device("cuda:0")
+    C, ext = 128, (-4.0, 4.0) * 3
+    sets = []
+    for n, seed in ((200_000, 5), (60_000, 6), (300_000, 7)):
+        d = plummer_torch(n, seed=seed, h_law="physical", extent=4.0, grid=C, device=dev)
+        sets.append((d["x"], d["y"], d["z"], d["h"], d["m"]))
+    kw = dict(cube_size=(C, C, C), extent=ext, kernel="wendland_c2")
+    serial = [project3d(*s, **kw).clone() for s in sets]
+    cnt = [project3d(*s[:4], torch.ones_like(s[3]), cube_size=(C, C, C), extent=ext,
+                     kernel="indicator").clone() for s in sets]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    outs, couts = [None] * 6, [None] * 6
+    for k in range(6):
+        s = sets[k % len(sets)]
+        with torch.cuda.stream(streams[k % 2]):
+            outs[k] = project3d(*s, **kw)
+            couts[k] = project3d(*s[:4], torch.ones_like(s[3]), cube_size=(C, C, C),
+                                 extent=ext, kernel="indicator")
+    torch.cuda.synchronize()
+    for k in range(6):
+        want = serial[k % len(sets)]
+        assert torch.equal(couts[k], cnt[k % len(sets)]), k
+        torch.testing.assert_close(outs[k], want, rtol=1e-6, atol=1e-6 * float(want.abs().max()))
