@@ -94,14 +94,20 @@ def parse():
                          "driver's line")
     ap.add_argument("--cube", type=int, default=512, help="cube edge (voxels), --workload cube")
     ap.add_argument("--streams", type=int, default=0,
-                    help="HIP streams consecutive maps alternate between (each its own "
-                         "workspace slot in the library), so map i + 1's binning and scatter "
-                         "run beside map i's deposit (store-bound and LDS-bound kernels "
-                         "sharing the CUs); 1 = one stream, maps strictly in sequence; 0 "
-                         "(auto) = 2, with the scatter gated behind the previous map's "
-                         "deposit (ASP_SCATTER_GATE) for a rank's share of <= 2e7 particles.  "
-                         "Same box, round 5: 10^8 3.25 -> 3.11 ms, 5e7 1.69 -> 1.59, 2.5e7 "
-                         "0.94 -> 0.86, 1.25e7 (gated) 0.58 -> 0.57 (DESIGN.md §7, §18)")
+                    help="HIP streams the TIMED region's consecutive maps (cubes) alternate "
+                         "between (each its own workspace slot in the library).  0 (auto): 1 "
+                         "for maps -- strictly in sequence, so every kernel's event-timed "
+                         "duration (the roofline) is its own, not shared with another map's "
+                         "kernels -- and 2 for cubes (the deposit dominates either way)")
+    ap.add_argument("--overlap-streams", type=int, default=2,
+                    help="after the timed region, a second timed region of --steps maps "
+                         "alternating between this many streams (0/1: none), reported as "
+                         "'overlapped': map i + 1's binning and scatter run beside map i's "
+                         "deposit (store-bound and LDS-bound kernels sharing the CUs), the "
+                         "scatter gated behind the previous map's deposit (ASP_SCATTER_GATE) "
+                         "for a rank's share of <= 2e7 particles unless the environment sets "
+                         "it.  Same box, round 5: 10^8 3.25 -> 3.11 ms, 5e7 1.69 -> 1.59, "
+                         "2.5e7 0.94 -> 0.86, 1.25e7 (gated) 0.58 -> 0.57 (DESIGN.md §7, §18)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="N > 1: wait for each map's collective before the next map")
     ap.add_argument("--no-stage-events", dest="stage_events", action="store_false",
@@ -779,14 +785,29 @@ def main():
     # only after its collective (stream-ordered wait).
     # Consecutive maps alternate between --streams HIP streams (each with its own output
     # buffer; the library gives each stream its own workspace slot): the binning of map
-    # i + 1 runs beside the deposit of map i.  --streams 1: one stream.
-    ns = args.streams if args.streams > 0 else 2
-    if args.streams == 0 and n_local <= 20_000_000:
-        os.environ["ASP_SCATTER_GATE"] = "1"  # small shares: scatter after the last deposit
-    gated = ns > 1 and os.environ.get("ASP_SCATTER_GATE", "0") not in ("", "0")
-    streams = ([torch.cuda.current_stream(dev)] if ns == 1 else
-               [torch.cuda.Stream(device=dev) for _ in range(ns)])
-    nbuf = max(ns, 2 if (world > 1 and args.pipeline) else 1)
+    # i + 1 runs beside the deposit of map i.  The timed region uses
+    # --streams (default 1); a second timed region uses --overlap-streams (default 2).
+    gate_env = os.environ.get("ASP_SCATTER_GATE")  # set by the caller: kept as is
+
+    def set_gate(n):
+        """ASP_SCATTER_GATE for a region on n streams (auto: small shares only)."""
+        if gate_env is None:
+            os.environ["ASP_SCATTER_GATE"] = "1" if (n > 1 and n_local <= 20_000_000) else "0"
+        return n > 1 and os.environ.get("ASP_SCATTER_GATE", "0") not in ("", "0")
+
+    stream_sets = {}
+
+    def stream_set(n):
+        if n not in stream_sets:
+            stream_sets[n] = ([torch.cuda.current_stream(dev)] if n == 1 else
+                              [torch.cuda.Stream(device=dev) for _ in range(n)])
+        return stream_sets[n]
+
+    ns = args.streams if args.streams > 0 else 1
+    nso = args.overlap_streams if args.overlap_streams > 1 else 0
+    mode = {"ns": ns, "streams": stream_set(ns)}
+    gated = set_gate(ns)
+    nbuf = max(ns, nso, 2 if (world > 1 and args.pipeline) else 1)
     bufs = [torch.empty((2 if a1 is not None else 1, G, G), dtype=torch.float32, device=dev)
             for _ in range(nbuf)]
     pending = [None]
@@ -829,7 +850,7 @@ def main():
         it[0] += 1
         maps = bufs[k % nbuf]
         o0, o1 = maps[0], (maps[1] if a1 is not None else None)
-        with torch.cuda.stream(streams[k % ns]):
+        with torch.cuda.stream(mode["streams"][k % mode["ns"]]):
             if R is not None:
                 # this rank's rows (ratio formed locally: its rows' sums are complete), then
                 # ONE all-gather of the single map -- no grid reduction
@@ -855,7 +876,7 @@ def main():
                 if pending[0] is not None:
                     # map k - 1's collective: the stream that next writes its buffer (map
                     # k - 1 + nbuf) waits for it -- stream-ordered, no host block
-                    with torch.cuda.stream(streams[(k - 1 + nbuf) % ns]):
+                    with torch.cuda.stream(mode["streams"][(k - 1 + nbuf) % mode["ns"]]):
                         last[0] = pending[0].wait()
                 pending[0] = p
             else:
@@ -863,7 +884,7 @@ def main():
 
     def drain():
         if pending[0] is not None:
-            with torch.cuda.stream(streams[(it[0] - 1) % ns]):
+            with torch.cuda.stream(mode["streams"][(it[0] - 1) % mode["ns"]]):
                 last[0] = pending[0].wait()
             pending[0] = None
 
@@ -931,6 +952,54 @@ def main():
     ok = output_check(out0, out1, a0, a1, ratio, world,
                       gathered_ratio=world > 1 and (args.op == "reduce_scatter_gather"
                                                     or R is not None))
+    overlapped = None
+    if nso:
+        # Second timed region: the same maps alternating between nso streams (throughput of
+        # the overlapped pipeline; no stage events, so the kernels run undisturbed).  Its
+        # kernels share the CUs with the other stream's, so their durations say nothing
+        # about any one kernel: the roofline above is the sequential region's.
+        drain()
+        torch.cuda.synchronize()
+        mode["ns"], mode["streams"] = nso, stream_set(nso)
+        gated_o = set_gate(nso)
+        for _ in range(args.warmup):
+            step()
+        drain()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        to = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        drain()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tt = torch.tensor([time.perf_counter() - to], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el_o = float(tt.item())
+        o0, o1 = last[0]
+        if R is not None:
+            if args.rows_gather == "all":
+                o0 = torch.cat([o0[r * rmax:r * rmax + R[r + 1] - R[r]] for r in range(world)])
+            elif rank != 0:
+                o0 = o0[R[rank]:R[rank + 1]]
+            o1 = None
+        ok_o = output_check(o0, o1, a0, a1, ratio, world,
+                            gathered_ratio=world > 1 and (args.op == "reduce_scatter_gather"
+                                                          or R is not None))
+        overlapped = {"streams": nso, "scatter_gate": gated_o,
+                      "ms_per_step": round(el_o / args.steps * 1e3, 4),
+                      "value": round(G * G * args.steps / el_o / 1e6, 3), "unit": "Mpixels/s",
+                      "output_ok": ok_o,
+                      "note": f"a second timed region of {args.steps} maps (after {args.warmup} "
+                              f"warm-up maps) alternating between {nso} HIP streams, each with "
+                              "its own workspace slot and output buffer: map i + 1's binning "
+                              "and scatter run beside map i's deposit.  Throughput of the "
+                              "overlapped pipeline; 'value' and the roofline are the "
+                              "sequential region's"}
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -1021,6 +1090,7 @@ def main():
                          "previous map's deposit), so its per-launch time includes sharing "
                          "the CUs and HBM; pipeline_frac (the whole map per step) is the "
                          "measure of the overlapped pipeline"} if ns > 1 else {})},
+        **({"overlapped": overlapped} if overlapped else {}),
         "stages": stages,
         "records_per_particle": round(st["records"] / max(1, n_local), 4),
         "work_items": st["items"], "wide_particles": st["wide"], "large_records": st["large"],

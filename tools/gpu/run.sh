@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 o=gpurun_out/${OUT:-r05}; mkdir -p $o
 mode=$1; shift
 summ() {  # name: ms, output check, dominant kernel, frac, per-stage ms
-  python3 -c "import json,sys;d=json.loads(open('$o/$1.json').read().strip().splitlines()[-1]);r=d.get('roofline',{});print('$1', d['ms_per_step'], d.get('output_ok'), r.get('kernel'), r.get('frac'), {k:round(v.get('ms_per_step', v.get('ms_per_launch', 0)),3) for k,v in d.get('stages',{}).items()})"
+  python3 -c "import json,sys;d=json.loads(open('$o/$1.json').read().strip().splitlines()[-1]);r=d.get('roofline',{});print('$1', d['ms_per_step'], d.get('output_ok'), r.get('kernel'), r.get('frac'), 'ovl', (d.get('overlapped') or {}).get('ms_per_step'), (d.get('overlapped') or {}).get('output_ok'), {k:round(v.get('ms_per_step', v.get('ms_per_launch', 0)),3) for k,v in d.get('stages',{}).items()})"
 }
 line() {  # name args...
   local name=$1; shift
