@@ -195,36 +195,78 @@ __global__ __launch_bounds__(k3Block) void k3_count(const float* __restrict__ x,
 // ----------------------------------------------------------------------------------
 // C3: scatter 32-byte records {x, y, z, h}, {a, 0, 0, 0} into the bricks' runs
 // ----------------------------------------------------------------------------------
-template <int PROBE>  // 1: the placement trials' launches (asp_project2d.hip k_scatter)
-__global__ __launch_bounds__(k3Block) void k3_scatter(
+// TB = GRP x k3Block threads: scatter workgroup b takes the batches of count workgroups
+// GRP b .. GRP b + GRP - 1 (interleaved: batch r nblk + GRP b + g, g < GRP, is one
+// contiguous range of TB particles; contiguous: their adjacent ranges), so its runs are
+// the union of theirs -- GRP x fewer (workgroup, brick) runs open at once (the scatter's
+// record stores cost with the number of open runs; 512 workgroups of 512
+// -> 256 of 1024: scatter 3.91 -> 3.62 ms at 10^8 / 512^3, count unchanged).
+template <int PROBE, int TB>  // PROBE 1: the placement trials' launches (asp_project2d.hip k_scatter)
+__global__ __launch_bounds__(TB) void k3_scatter(
     const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
     const float* __restrict__ h, const float* __restrict__ a, long long n, long long per_block,
     Grid3 g, const int* __restrict__ hist, const long long* __restrict__ brick_start,
     float4* __restrict__ recs, int inter) {
     extern __shared__ __attribute__((aligned(16))) int cur[];
-    const int* row = hist + (long long)blockIdx.x * g.nb;
-    for (int t = threadIdx.x; t < g.nb; t += k3Block) cur[t] = (int)brick_start[t] + row[t];
+    constexpr int GRP = TB / k3Block;
+    const int* row = hist + (long long)blockIdx.x * GRP * g.nb;
+    for (int t = threadIdx.x; t < g.nb; t += TB) cur[t] = (int)brick_start[t] + row[t];
     __syncthreads();
-    // the count's batch assignment (k3_count)
-    const long long stride = inter ? (long long)gridDim.x * k3Block : k3Block;
-    const long long p0 = inter ? (long long)blockIdx.x * k3Block : (long long)blockIdx.x * per_block;
-    const long long p1 = inter ? n : min(n, p0 + per_block);
+    // the count's batch assignment (k3_count), GRP count workgroups at a time
+    const long long stride = inter ? (long long)gridDim.x * TB : TB;
+    const long long p0 = inter ? (long long)blockIdx.x * TB : (long long)blockIdx.x * GRP * per_block;
+    const long long p1 = inter ? n : min(n, p0 + GRP * per_block);
     const Grid3f gf = {(float)g.x_min, (float)g.y_min, (float)g.z_min,
                        (float)g.ipx, (float)g.ipy, (float)g.ipz};
+    // A wave's (particle, brick) pairs are dealt 64 per round, one per lane, so every
+    // store instruction is full.  Nested brick loops per lane ran max-over-lanes
+    // iterations with few lanes active (1.39 records per particle, ~6 iterations per wave
+    // at 10^8 / 512^3: 23 % of the store lanes busy).  Round 5: scatter 3.96 -> 3.91 ms,
+    // 3.83 -> 3.62 with the grouped workgroups.
+    const int lane = threadIdx.x & 63;
     auto bin = [&](float cx, float cy, float cz, float ch, float ca) {
         Box3 b;
+        int nbr = 0, bi0 = 0, bj0 = 0, bk0 = 0, nj = 1, nk = 1;
         if (footprint3f(g, gf, cx, cy, cz, ch, b)) {
-            float4 r0 = make_float4(cx, cy, cz, ch), r1 = make_float4(ca, 0.0f, 0.0f, 0.0f);
-            int bi0 = (b.i0 - g.i_lo) >> kBXs, bi1 = (b.i1 - g.i_lo) >> kBXs;
-            int bj0 = b.j0 >> kBYs, bj1 = b.j1 >> kBYs;
-            int bk0 = (b.k0 - g.k_lo) >> kBZs, bk1 = (b.k1 - g.k_lo) >> kBZs;
-            for (int bi = bi0; bi <= bi1; ++bi)
-                for (int bj = bj0; bj <= bj1; ++bj)
-                    for (int bk = bk0; bk <= bk1; ++bk) {
-                        int slot = atomicAdd(&cur[(bi * g.nby + bj) * g.nbz + bk], 1);
-                        recs[2 * (long long)slot] = r0;
-                        recs[2 * (long long)slot + 1] = r1;
-                    }
+            bi0 = (b.i0 - g.i_lo) >> kBXs;
+            bj0 = b.j0 >> kBYs;
+            bk0 = (b.k0 - g.k_lo) >> kBZs;
+            nj = (b.j1 >> kBYs) - bj0 + 1;
+            nk = ((b.k1 - g.k_lo) >> kBZs) - bk0 + 1;
+            nbr = (((b.i1 - g.i_lo) >> kBXs) - bi0 + 1) * nj * nk;
+        }
+        if (__ballot(nbr > 1) == 0) {  // one brick at most per lane: store in place
+            if (nbr) {
+                const int slot = atomicAdd(&cur[(bi0 * g.nby + bj0) * g.nbz + bk0], 1);
+                recs[2 * (long long)slot] = make_float4(cx, cy, cz, ch);
+                recs[2 * (long long)slot + 1] = make_float4(ca, 0.0f, 0.0f, 0.0f);
+            }
+            return;
+        }
+        int incl = nbr;  // inclusive scan of the pair counts over the wave
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(incl, d);
+            if (lane >= d) incl += v;
+        }
+        const int total = __shfl(incl, 63), excl = incl - nbr;
+        for (int r = 0; r < total; r += 64) {
+            const int p = r + lane;
+            int s = 0;  // the pair's source lane: the number of lanes with incl <= p
+#pragma unroll
+            for (int st = 32; st >= 1; st >>= 1)
+                if (__shfl(incl, s + st - 1) <= p) s += st;
+            const float fx = __shfl(cx, s), fy = __shfl(cy, s), fz = __shfl(cz, s);
+            const float fh = __shfl(ch, s), fa = __shfl(ca, s);
+            const int sj = __shfl(nj, s), sk = __shfl(nk, s);
+            const int q = p - __shfl(excl, s);
+            const int t = q / sk, dk = q - t * sk, di = t / sj, dj = t - di * sj;
+            const int bi = __shfl(bi0, s) + di, bj = __shfl(bj0, s) + dj, bk = __shfl(bk0, s) + dk;
+            if (p < total) {
+                const int slot = atomicAdd(&cur[(bi * g.nby + bj) * g.nbz + bk], 1);
+                recs[2 * (long long)slot] = make_float4(fx, fy, fz, fh);
+                recs[2 * (long long)slot + 1] = make_float4(fa, 0.0f, 0.0f, 0.0f);
+            }
         }
     };
     // Two particle buffers in ping-pong (no register copies at the loop's back edge, which
@@ -788,8 +830,14 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
     ASP_TRY(ensure(ws.slabs, (size_t)n_slabs * kBrickVox * sizeof(double)));
     auto scatter = [&](bool probe) -> int {
         StageMark m(ws, kS3Scatter, st);
-        hipLaunchKernelGGL(probe ? k3_scatter<1> : k3_scatter<0>, dim3((unsigned)nblk),
-                           dim3(k3Block), lds_bins, st, dx,
+        // grouped workgroups (GRP 2) need an even count grid; ASP_CUBE_SGRP=1: one count
+        // workgroup per scatter workgroup (A/B switch, read per call)
+        const char* ge = getenv("ASP_CUBE_SGRP");
+        const bool g2 = (ge ? atoi(ge) != 1 : true) && nblk % 2 == 0;
+        auto kern = g2 ? (probe ? k3_scatter<1, 2 * k3Block> : k3_scatter<0, 2 * k3Block>)
+                       : (probe ? k3_scatter<1, k3Block> : k3_scatter<0, k3Block>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)(g2 ? nblk / 2 : nblk)),
+                           dim3(g2 ? 2 * k3Block : k3Block), lds_bins, st, dx,
                            dy, dz, dh, da, n, per_block, g, (const int*)ws.hist.p,
                            (const long long*)ws.tile_start.p, (float4*)ws.recs.p, inter);
         ASP_LAUNCHED();
