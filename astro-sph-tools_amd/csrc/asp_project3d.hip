@@ -51,9 +51,11 @@ constexpr int kBrickVox = kBX * kBY * kBZ;   // 8192 -> 64 KiB of fp64 accumulat
 // padded to kBZP doubles (a 32-double row stride put the same k of adjacent columns in
 // one bank), the bank then shifting with each lane's first plane.
 constexpr int kBZP = kBZ + ASP_CUBE_PAD;
+static_assert(ASP_CUBE_PLANES || ASP_CUBE_PAD >= 1, "column-major: the pad word takes plane kBZ");
 constexpr int kPlane = kBX * kBY;
 constexpr int kKStride = ASP_CUBE_PLANES ? kPlane : 1;  // LDS step from plane k to k + 1
-constexpr int kBrickLds = ASP_CUBE_PLANES ? kBZ * kPlane : kBX * kBY * kBZP;
+// (plane-major: one spare plane kBZ after the brick, the odd-length columns' last pair)
+constexpr int kBrickLds = ASP_CUBE_PLANES ? (kBZ + 1) * kPlane : kBX * kBY * kBZP;
 __device__ __forceinline__ int lds_at(int li, int lj, int lk) {
     return ASP_CUBE_PLANES ? lk * kPlane + li * kBY + lj : (li * kBY + lj) * kBZP + lk;
 }
@@ -347,6 +349,84 @@ __device__ __forceinline__ void voxel3(const Rec3& R, double s, int li, int lj, 
     }
 }
 
+// The plane walk of one column, planes [a, b] (brick-local), edge-continuous kernels: in
+// units of h, q = sqrt(dz'^2 + s') with dz' = (zr - k pz) / h and s' = s / h^2 formed once
+// per column, and the term's coefficient folded into the shape's last factor (Wendland:
+// t^4 (c + 2c q)) -- two packed operations fewer per plane pair than q = sqrt(r2) / h and
+// f(q) * c.  col: the column's plane-0 word; sfh = s'; zh = (z - Z[0]) / h; pzh = -pz / h;
+// sc = the term coefficient x kShapeScale.
+template <int KID>
+__device__ __forceinline__ void plane_walk(double* col, float fa, float fb, float sfh, float zh,
+                                           float pzh, float sc) {
+    const f2 zr2 = {zh, zh}, npz = {pzh, pzh}, sf2 = {sfh, sfh};
+    const f2 sc2 = {sc, sc}, sc22 = {2.0f * sc, 2.0f * sc};
+    auto planes2 = [&](f2 pl) {
+        const f2 dz = __builtin_elementwise_fma(pl, npz, zr2);
+        const f2 r2 = __builtin_elementwise_fma(dz, dz, sf2);
+        const f2 q = f2{__builtin_amdgcn_sqrtf(r2.x), __builtin_amdgcn_sqrtf(r2.y)};
+        if constexpr (KID == 1) {  // Wendland C2: c t^4 (1 + 2q) = t^4 (c + 2c q)
+            const f2 t = pk_one_minus_half_clamp(q);
+            const f2 t2 = t * t;
+            return (t2 * t2) * __builtin_elementwise_fma(sc22, q, sc2);
+        } else {
+            return edge_shape2<KID>(q) * sc2;
+        }
+    };
+    // whole plane pairs, no odd last plane: a column of odd length also adds plane fb + 1,
+    // where the term is 0 (beyond the sphere: the range is a superset of its planes and the
+    // box's last plane is the sphere's, the brick's or the slab's) or lands in the brick's
+    // spare plane kBZ / a plane past the slab, neither ever read out.  The plane numbers are
+    // small integers in fp32 (exact), so the packed pair doubles as the loop counter.
+    f2 lk2 = {fa, fa + 1.0f};
+    double* p = col + (int)fa * kKStride;
+    for (; lk2.x <= fb; lk2 += (f2){2.0f, 2.0f}, p += 2 * kKStride) {
+        const f2 w = planes2(lk2);
+        atomicAdd(p, (double)w.x);
+        atomicAdd(p + kKStride, (double)w.y);
+    }
+}
+
+// Per-record constants of the edge-continuous column walk, formed once per record (the
+// walk's loops then hold them in registers).  k0f / k1f are canonical (a clamp by fmaxf
+// would otherwise re-canonicalise them in every column).
+struct ColE {
+    float tin;       // fl32(thr) (1 + 2^-20): columns with s below can meet the sphere
+    float tpe;       // fl32(thr) (1 + 2^-19)
+    float rzs;       // 1 / pz (1 + 2^-18)
+    float kc, k0f, k1f;
+    float h2, zh, pzh, sc;
+};
+template <int KID>
+__device__ __forceinline__ ColE col_consts(const Grid3& g, const Rec3& R) {
+    ColE K;
+    K.tin = R.thrf * (1.0f + 0x1p-20f);
+    K.tpe = R.thrf * (1.0f + 0x1p-19f);
+    K.rzs = (float)g.ipz * (1.0f + 0x1p-18f);
+    K.kc = R.kc;
+    K.k0f = __builtin_canonicalizef((float)R.b.k0);
+    K.k1f = __builtin_canonicalizef((float)R.b.k1);
+    K.h2 = R.hinv * R.hinv;
+    K.zh = R.zr * R.hinv;
+    K.pzh = -(float)g.pz * R.hinv;
+    K.sc = R.s * kShapeScale<KID>;
+    return K;
+}
+
+// One column of an edge-continuous kernel: s = dx^2 + dy^2 in fp32 (offsets from the box's
+// first column, column3), its plane range, the walk.  column3's half-width argument
+// max(thr - s, 0) + thr 2^-20 is replaced by thr (1 + 2^-19) - s, never smaller for the
+// columns that pass (s < thr (1 + 2^-20)), so the range stays a superset; the scale and the
+// margin are one fma.
+template <int KID>
+__device__ __forceinline__ void column_e(const ColE& K, double* col, float sf) {
+    if (!(sf < K.tin)) return;  // the column misses the sphere
+    const float rz = fmaf(__builtin_amdgcn_sqrtf(K.tpe - sf), K.rzs, 0x1p-10f);
+    const float fa = fmaxf(ceilf(K.kc - rz), K.k0f);
+    const float fb = fminf(floorf(K.kc + rz), K.k1f);
+    if (!(fa <= fb)) return;
+    plane_walk<KID>(col, fa, fb, sf * K.h2, K.zh, K.pzh, K.sc);
+}
+
 template <int KID>
 __device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, int lj, int K0,
                                         const double* xt, const double* yt, const double* zt,
@@ -357,55 +437,11 @@ __device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, i
         if (!column_range(g, R, li, lj, xt, yt, s, a, b)) return;
         for (int lk = a; lk <= b; ++lk) voxel3<KID>(R, s, li, lj, lk, zt, acc);
     } else {  // fp32 throughout: the column's plane range and dz, no decision
-        // the record's fp32 fields as scalars (reading them through the struct inside the
-        // loop nest made the compiler keep it in scratch memory)
-        const float hinv = R.hinv, rs = R.s, kc = R.kc;
         // offsets from the box's first column in fp32 (no LDS corner reads per column):
         // within 2^-24 (|lx| + 16 pitches) of the exact ones, ~2^-20 of h for these boxes
         const float dx = fmaf(-(float)(li - R.b.i0), (float)g.px, R.lx);
         const float dy = fmaf(-(float)(lj - R.b.j0), (float)g.py, R.ly);
-        const float sf = fmaf(dx, dx, dy * dy);
-        const float thr = R.thrf;
-        if (!(sf < thr * (1.0f + 0x1p-20f))) return;  // the column misses the sphere
-        // the planes of q < 2 (W > 0): |dz| < sqrt(thr - s), widened well past the roundings
-        float rz = __builtin_amdgcn_sqrtf(fmaxf(thr - sf, 0.0f) + thr * 0x1p-20f) * (float)g.ipz;
-        rz = rz * (1.0f + 0x1p-18f) + 0x1p-10f;
-        const float fa = fmaxf(ceilf(kc - rz), (float)R.b.k0);
-        const float fb = fminf(floorf(kc + rz), (float)R.b.k1);
-        if (!(fa <= fb)) return;
-        const int a = (int)fa, b = (int)fb;
-        // the plane walk in units of h: q = sqrt(dz'^2 + s') with dz' = (zr - k pz) / h and
-        // s' = s / h^2 formed once per column, and the term's coefficient folded into the
-        // shape's last factor (Wendland: t^4 (c + 2c q)) -- two packed operations fewer
-        // per plane pair than q = sqrt(r2) / h and f(q) * c
-        const float zh = R.zr * hinv;  // z relative to the brick's first plane, in h
-        const float pzh = -(float)g.pz * hinv;
-        const f2 zr2 = {zh, zh}, npz = {pzh, pzh}, sf2 = {sf * (hinv * hinv), sf * (hinv * hinv)};
-        const float sc = rs * kShapeScale<KID>;  // edge_shape2 returns f / kShapeScale
-        const f2 sc2 = {sc, sc}, sc22 = {2.0f * sc, 2.0f * sc};
-        double* col = acc + lds_at(li, lj, 0);
-        f2 lk2 = {(float)a, (float)(a + 1)};
-        auto planes2 = [&](f2 pl) {
-            const f2 dz = __builtin_elementwise_fma(pl, npz, zr2);
-            const f2 r2 = __builtin_elementwise_fma(dz, dz, sf2);
-            const f2 q = f2{__builtin_amdgcn_sqrtf(r2.x), __builtin_amdgcn_sqrtf(r2.y)};
-            if constexpr (KID == 1) {  // Wendland C2: c t^4 (1 + 2q) = t^4 (c + 2c q)
-                const f2 t = pk_one_minus_half_clamp(q);
-                const f2 t2 = t * t;
-                return (t2 * t2) * __builtin_elementwise_fma(sc22, q, sc2);
-            } else {
-                return edge_shape2<KID>(q) * sc2;
-            }
-        };
-        // whole plane pairs without a per-pair branch, then the odd last plane
-        int lk = a;
-        for (; lk < b; lk += 2) {
-            const f2 w = planes2(lk2);
-            atomicAdd(&col[lk * kKStride], (double)w.x);
-            atomicAdd(&col[(lk + 1) * kKStride], (double)w.y);
-            lk2 += (f2){2.0f, 2.0f};
-        }
-        if (lk == b) atomicAdd(&col[lk * kKStride], (double)planes2(lk2).x);
+        column_e<KID>(col_consts<KID>(g, R), acc + lds_at(li, lj, 0), fmaf(dx, dx, dy * dy));
     }
 }
 
@@ -539,10 +575,13 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         // whole wave), the lane classes 64 at a time (one per lane).  The next chunk is
         // claimed and its records loaded before the current one is walked.
         int ccls = 0;  // claim cursor: the class being claimed from (wave-uniform)
+        // records claimed at a time: the wave class kWaveTake (each walked by the whole
+        // wave), the lane classes 64 (one per lane)
+        auto take = [](int c) { return c == 0 ? kWaveTake : 64; };
         auto claim = [&](int& cls, int& base) {
             while (ccls < kQCls) {
                 int b0 = 0;
-                if (lane == 0) b0 = atomicAdd(&qhead[ccls], ccls == 0 ? kWaveTake : 64);
+                if (lane == 0) b0 = atomicAdd(&qhead[ccls], take(ccls));
                 b0 = __shfl(b0, 0);
                 if (b0 < qcnt[ccls]) {
                     cls = ccls;
@@ -555,7 +594,7 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
             base = 0;
         };
         auto fetch = [&](int cls, int base, int& i, float4& q0, float4& q1) {
-            const bool have = cls < kQCls && lane < (cls == 0 ? kWaveTake : 64) &&
+            const bool have = cls < kQCls && lane < take(cls) &&
                               base + lane < qcnt[min(cls, kQCls - 1)];
             i = have ? (int)qlist[qoff[cls] + base + lane] : -1;
             const long long ri = it.start + r0i + max(i, 0);  // unconditional load
@@ -580,11 +619,31 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
                 if (live) {
                     const int nc = bw * bh;
                     int li = R.b.i0, lj = R.b.j0;
-                    for (int c = 0; c < nc; ++c) {
-                        column3<KID>(g, R, li, lj, K0, xt, yt, zt, acc);
-                        if (++lj > R.b.j1) {
-                            lj = R.b.j0;
-                            ++li;
+                    if constexpr (KID == 2) {
+                        for (int c = 0; c < nc; ++c) {
+                            column3<KID>(g, R, li, lj, K0, xt, yt, zt, acc);
+                            if (++lj > R.b.j1) {
+                                lj = R.b.j0;
+                                ++li;
+                            }
+                        }
+                    } else {
+                        // the record's constants once; the column offsets stepped (one
+                        // subtraction per column instead of two conversions and two fma:
+                        // <= 16 roundings of ~2^-24 |d|, a value effect only)
+                        const ColE K = col_consts<KID>(g, R);
+                        const float px = (float)g.px, py = (float)g.py;
+                        float dx = R.lx, dy = R.ly;
+                        for (int c = 0; c < nc; ++c) {
+                            column_e<KID>(K, acc + lds_at(li, lj, 0), fmaf(dx, dx, dy * dy));
+                            if (++lj > R.b.j1) {
+                                lj = R.b.j0;
+                                ++li;
+                                dy = R.ly;
+                                dx -= px;
+                            } else {
+                                dy -= py;
+                            }
                         }
                     }
                 }
@@ -614,8 +673,17 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
                     // next one of a lane 64 further on (one division per record, not per column)
                     const int di = 64 / qh, dj = 64 - di * qh;
                     int ci = lane / qh, cj = lane - ci * qh;
+                    ColE K = {};
+                    if constexpr (KID != 2) K = col_consts<KID>(g, Q);
+                    const float px = (float)g.px, py = (float)g.py;
                     for (int cc = lane; cc < qw * qh; cc += 64) {
-                        column3<KID>(g, Q, Q.b.i0 + ci, Q.b.j0 + cj, K0, xt, yt, zt, acc);
+                        if constexpr (KID == 2) {
+                            column3<KID>(g, Q, Q.b.i0 + ci, Q.b.j0 + cj, K0, xt, yt, zt, acc);
+                        } else {
+                            const float dx = fmaf(-(float)ci, px, Q.lx), dy = fmaf(-(float)cj, py, Q.ly);
+                            column_e<KID>(K, acc + lds_at(Q.b.i0 + ci, Q.b.j0 + cj, 0),
+                                          fmaf(dx, dx, dy * dy));
+                        }
                         ci += di;
                         cj += dj;
                         if (cj >= qh) {
