@@ -72,18 +72,24 @@ constexpr int kLaneCols = ASP_CUBE_LANE_COLS;  // boxes up to this many (i, j) c
                                                // lane-per-record, wider: a wave per record
 
 // Deposit rounds: records classified per round (LDS list of 2-byte indices) and the
-// classes (0: boxes of more than lane_cols columns, 1-4: lane-per-record boxes by volume)
+// classes (0: boxes of more than lane_cols columns, 1..kNCCls + 1: lane-per-record boxes by
+// column count, large to small)
 constexpr int kRound = 4096;
-constexpr int kQCls = 5;
+// Lane classes by the box's column count (round 5): a lane-per-record wave runs
+// max-over-lanes column steps, so records of similar column counts go together.  The box
+// volume classes before (80 / 32 / 12) mixed column counts within a class: deposit 11.84
+// -> 11.07 ms (same process; thresholds 36 / 25 / 16 / 9 / 4 against 10 or 13 finer ones
+// and 40 / 30 / 20 / 12 / 6: 11.07-11.30 ms).
+#ifndef ASP_CUBE_CCLS
+#define ASP_CUBE_CCLS 36, 25, 16, 9, 4
+#endif
+constexpr int kCCls[] = {ASP_CUBE_CCLS};  // descending: class 1 + #{t : cols <= t}
+constexpr int kNCCls = sizeof(kCCls) / sizeof(int);
+constexpr int kQCls = 2 + kNCCls;  // the wave class, then the lane classes large to small
 #ifndef ASP_CUBE_WAVE_TAKE
 #define ASP_CUBE_WAVE_TAKE 32
 #endif
 constexpr int kWaveTake = ASP_CUBE_WAVE_TAKE;  // wave-class records claimed at a time
-#ifndef ASP_CUBE_VOL
-#define ASP_CUBE_VOL 80, 32, 12
-#endif
-constexpr int kVol[3] = {ASP_CUBE_VOL};  // lane classes: box volume above kV1, kV2, kV3, rest
-constexpr int kV1 = kVol[0], kV2 = kVol[1], kV3 = kVol[2];
 static_assert(kRound % k3Block == 0 && kRound <= 65536, "round of whole blocks, 16-bit index");
 
 struct Grid3 {
@@ -513,8 +519,8 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         return ok;
     };
     // The item's records are taken in rounds of kRound.  Each round is first CLASSIFIED:
-    // boxes of more than lane_cols columns (a wave walks each) and four classes of the
-    // lane-per-record boxes by box volume; the record indices are counting-sorted by class
+    // boxes of more than lane_cols columns (a wave walks each) and kNCCls + 1 classes of
+    // the lane-per-record boxes by column count; the record indices are counting-sorted by class
     // into an LDS list.  Then every wave repeatedly claims a chunk of one class (the wave
     // class first, then the lane classes from large to small boxes) until the round is
     // exhausted: a wave's 64 lanes walk boxes of similar size, where records in arrival
@@ -549,8 +555,11 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
                 const int bh = min(b.j1, J0 + TH - 1) - max(b.j0, J0) + 1;
                 const int bd = min(b.k1, K0 + TD - 1) - max(b.k0, K0) + 1;
                 if (bw > 0 && bh > 0 && bd > 0) {
-                    const int cols = bw * bh, vol = cols * bd;
-                    c = cols > g.lane_cols ? 0 : vol > kV1 ? 1 : vol > kV2 ? 2 : vol > kV3 ? 3 : 4;
+                    const int cols = bw * bh;
+                    c = 1;
+#pragma unroll
+                    for (int t = 0; t < kNCCls; ++t) c += cols <= kCCls[t];
+                    if (cols > g.lane_cols) c = 0;
                     if ((g.diag == 1 && c == 0) || (g.diag == 2 && c > 0)) c = -1;
                 }
             }
@@ -826,7 +835,6 @@ static bool make_grid3(const double* ext, int nx, int ny, int nz, int k_lo, int 
     g.lane_cols = kLaneCols;
     if (const char* e = getenv("ASP_CUBE_LANE_COLS")) g.lane_cols = std::max(0, atoi(e));
     g.diag = getenv("ASP_CUBE_DIAG") ? atoi(getenv("ASP_CUBE_DIAG")) : 0;
-
     return true;
 }
 
