@@ -77,8 +77,8 @@ constexpr int kLaneCols = ASP_CUBE_LANE_COLS;  // boxes up to this many (i, j) c
 constexpr int kRound = 4096;
 // Lane classes by the box's column count (round 5): a lane-per-record wave runs
 // max-over-lanes column steps, so records of similar column counts go together.  The box
-// volume classes before (80 / 32 / 12) mixed column counts within a class: deposit 11.84
-// -> 11.07 ms (same process; thresholds 36 / 25 / 16 / 9 / 4 against 10 or 13 finer ones
+// volume classes before (80 / 32 / 12) mixed column counts within a class (CPU model:
+// tools/sim/cube_classes.py): deposit 11.84 -> 11.07 ms (same process; thresholds 36 / 25 / 16 / 9 / 4 against 10 or 13 finer ones
 // and 40 / 30 / 20 / 12 / 6: 11.07-11.30 ms).
 #ifndef ASP_CUBE_CCLS
 #define ASP_CUBE_CCLS 36, 25, 16, 9, 4

@@ -1,3 +1,11 @@
+"""Lane-class model of the cube deposit's lane-per-record path (CPU, numpy; round 5).
+
+Samples the cfg-5 particle set (10^8 Plummer, physical h, 512^3), forms every (particle,
+brick) record of <= 48 columns with its per-column plane counts, and prices a wave of 64
+records of one class as prep + sum over column steps (max over its lanes) of the column
+set-up and the packed plane pairs.  Compares the box-volume classes (80 / 32 / 12) with
+classes by column count; the deposit went 11.84 -> 11.07 ms on the GPU.
+"""
 import numpy as np, itertools
 N_REAL, C, EXT, SAMPLE = 10**8, 512, 4.0, 150_000
 rng = np.random.default_rng(1)
