@@ -201,8 +201,33 @@ __global__ __launch_bounds__(k3Block) void k3_count(const float* __restrict__ x,
 }
 
 // ----------------------------------------------------------------------------------
-// C3: scatter 32-byte records {x, y, z, h}, {a, 0, 0, 0} into the bricks' runs
+// C3: scatter 32-byte records {x, y, z, h}, {a, box, lx, ly} into the bricks' runs
 // ----------------------------------------------------------------------------------
+// The record's second half: a, the particle's box clipped to brick (bi, bj, bk) in
+// brick-local voxels (5 bits per bound: i0 i1 j0 j1 k0 k1), and the fp32 offsets of the
+// particle from the box's first column, fl32(x - X[I0 + i0]), fl32(y - Y[J0 + j0]) -- formed
+// here, where the brick is known, by the expressions the deposit used to evaluate from the
+// particle (same fp64 operations, so identical bits): the deposit's classification and
+// record set-up no longer recompute the footprint (round 5).  The box's
+// clip to the cube (TW / TH / TD) is implied: footprint3f already clips to the slab.
+__device__ __forceinline__ float4 rec_half1(const Grid3& g, int bi0, int bi1, int bj0, int bj1,
+                                            int bk0, int bk1, int bi, int bj, int bk, float x,
+                                            float y, float a) {
+    const int I0 = g.i_lo + bi * kBX, J0 = bj * kBY, K0 = g.k_lo + bk * kBZ;
+    const int i0 = max(bi0 - I0, 0), i1 = min(bi1 - I0, kBX - 1);
+    const int j0 = max(bj0 - J0, 0), j1 = min(bj1 - J0, kBY - 1);
+    const int k0 = max(bk0 - K0, 0), k1 = min(bk1 - K0, kBZ - 1);
+    const unsigned bits = (unsigned)i0 | (unsigned)i1 << 5 | (unsigned)j0 << 10 |
+                          (unsigned)j1 << 15 | (unsigned)k0 << 20 | (unsigned)k1 << 25;
+    const float lx = (float)((double)x - (g.x_min + (double)(I0 + i0) * g.px));
+    const float ly = (float)((double)y - (g.y_min + (double)(J0 + j0) * g.py));
+    return make_float4(a, __uint_as_float(bits), lx, ly);
+}
+__device__ __forceinline__ Box3 rec_box(float bits_f) {
+    const unsigned v = __float_as_uint(bits_f);
+    return Box3{(int)(v & 31), (int)(v >> 5 & 31), (int)(v >> 10 & 31),
+                (int)(v >> 15 & 31), (int)(v >> 20 & 31), (int)(v >> 25 & 31)};
+}
 // TB = GRP x k3Block threads: scatter workgroup b takes the batches of count workgroups
 // GRP b .. GRP b + GRP - 1 (interleaved: batch r nblk + GRP b + g, g < GRP, is one
 // contiguous range of TB particles; contiguous: their adjacent ranges), so its runs are
@@ -233,7 +258,7 @@ __global__ __launch_bounds__(TB) void k3_scatter(
     // 3.83 -> 3.62 with the grouped workgroups.
     const int lane = threadIdx.x & 63;
     auto bin = [&](float cx, float cy, float cz, float ch, float ca) {
-        Box3 b;
+        Box3 b = {};
         int nbr = 0, bi0 = 0, bj0 = 0, bk0 = 0, nj = 1, nk = 1;
         if (footprint3f(g, gf, cx, cy, cz, ch, b)) {
             bi0 = (b.i0 - g.i_lo) >> kBXs;
@@ -247,10 +272,13 @@ __global__ __launch_bounds__(TB) void k3_scatter(
             if (nbr) {
                 const int slot = atomicAdd(&cur[(bi0 * g.nby + bj0) * g.nbz + bk0], 1);
                 recs[2 * (long long)slot] = make_float4(cx, cy, cz, ch);
-                recs[2 * (long long)slot + 1] = make_float4(ca, 0.0f, 0.0f, 0.0f);
+                recs[2 * (long long)slot + 1] =
+                    rec_half1(g, b.i0, b.i1, b.j0, b.j1, b.k0, b.k1, bi0, bj0, bk0, cx, cy, ca);
             }
             return;
         }
+        // the box, packed for the deal (16 bits per bound: cube edges < 65536)
+        const int pi = b.i0 | b.i1 << 16, pj = b.j0 | b.j1 << 16, pk = b.k0 | b.k1 << 16;
         int incl = nbr;  // inclusive scan of the pair counts over the wave
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -270,10 +298,13 @@ __global__ __launch_bounds__(TB) void k3_scatter(
             const int q = p - __shfl(excl, s);
             const int t = q / sk, dk = q - t * sk, di = t / sj, dj = t - di * sj;
             const int bi = __shfl(bi0, s) + di, bj = __shfl(bj0, s) + dj, bk = __shfl(bk0, s) + dk;
+            const int si = __shfl(pi, s), sjj = __shfl(pj, s), skk = __shfl(pk, s);
             if (p < total) {
                 const int slot = atomicAdd(&cur[(bi * g.nby + bj) * g.nbz + bk], 1);
                 recs[2 * (long long)slot] = make_float4(fx, fy, fz, fh);
-                recs[2 * (long long)slot + 1] = make_float4(fa, 0.0f, 0.0f, 0.0f);
+                recs[2 * (long long)slot + 1] =
+                    rec_half1(g, si & 0xffff, si >> 16, sjj & 0xffff, sjj >> 16, skk & 0xffff,
+                              skk >> 16, bi, bj, bk, fx, fy, fa);
             }
         }
     };
@@ -489,18 +520,10 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         zt[threadIdx.x - kBX - kBY] = g.z_min + (double)(K0 + (int)threadIdx.x - kBX - kBY) * g.pz;
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const Grid3f gf = {(float)g.x_min, (float)g.y_min, (float)g.z_min,
-                       (float)g.ipx, (float)g.ipy, (float)g.ipz};
     // A record's state for the walk: its box clipped to the brick (brick-local), the fp64
     // centre and threshold, 1/h, the term coefficient and the brick-local plane of z.
     auto prep = [&](const float4& q0, const float4& q1, Rec3& R) -> bool {
-        if (!footprint3f(g, gf, q0.x, q0.y, q0.z, q0.w, R.b)) return false;
-        R.b.i0 = max(R.b.i0, I0) - I0;
-        R.b.i1 = min(R.b.i1, I0 + TW - 1) - I0;
-        R.b.j0 = max(R.b.j0, J0) - J0;
-        R.b.j1 = min(R.b.j1, J0 + TH - 1) - J0;
-        R.b.k0 = max(R.b.k0, K0) - K0;
-        R.b.k1 = min(R.b.k1, K0 + TD - 1) - K0;
+        R.b = rec_box(q1.y);  // clipped to the brick by the scatter (rec_half1)
         R.x = q0.x;
         R.y = q0.y;
         R.z = q0.z;
@@ -509,14 +532,11 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         R.hinv = 1.0f / q0.w;
         R.s = (float)term_coef<KID>(q1.x, q0.w);
         R.kc = (float)((R.z - g.z_min) * g.ipz - (double)K0);
-        const bool ok = R.b.i0 <= R.b.i1 && R.b.j0 <= R.b.j1 && R.b.k0 <= R.b.k1;
-        // the corner coordinates by the tables' own fp64 expressions (identical values): an
-        // LDS table read here would wait (lgkmcnt) behind the wave's in-flight atomics
-        R.lx = ok ? (float)(R.x - (g.x_min + (double)(I0 + R.b.i0) * g.px)) : 0.0f;
-        R.ly = ok ? (float)(R.y - (g.y_min + (double)(J0 + R.b.j0) * g.py)) : 0.0f;
+        R.lx = q1.z;
+        R.ly = q1.w;
         R.zr = (float)(R.z - (g.z_min + (double)K0 * g.pz));
         R.thrf = (float)R.thr;
-        return ok;
+        return true;
     };
     // The item's records are taken in rounds of kRound.  Each round is first CLASSIFIED:
     // boxes of more than lane_cols columns (a wave walks each) and kNCCls + 1 classes of
@@ -540,28 +560,23 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         // all of this thread's records of the round loaded first: loads interleaved with
         // the class counters' LDS atomics were issued one at a time, each waiting a full
         // memory latency (vmcnt(0)) before the next (round 5)
-        float4 qv[kRound / k3Block];
+        // the class from the box the scatter stored in the record's second half
+        float qv[kRound / k3Block];
 #pragma unroll
         for (int q = 0; q < kRound / k3Block; ++q)
-            qv[q] = recs[2 * (it.start + r0i + min(q * k3Block + (int)threadIdx.x, nr - 1))];
+            qv[q] = recs[2 * (it.start + r0i + min(q * k3Block + (int)threadIdx.x, nr - 1)) + 1].y;
 #pragma unroll
         for (int q = 0; q < kRound / k3Block; ++q) {
             const int i = q * k3Block + (int)threadIdx.x;
-            const float4 q0 = qv[q];
-            Box3 b;
             int c = -1;
-            if (i < nr && footprint3f(g, gf, q0.x, q0.y, q0.z, q0.w, b)) {
-                const int bw = min(b.i1, I0 + TW - 1) - max(b.i0, I0) + 1;
-                const int bh = min(b.j1, J0 + TH - 1) - max(b.j0, J0) + 1;
-                const int bd = min(b.k1, K0 + TD - 1) - max(b.k0, K0) + 1;
-                if (bw > 0 && bh > 0 && bd > 0) {
-                    const int cols = bw * bh;
-                    c = 1;
+            if (i < nr) {
+                const Box3 b = rec_box(qv[q]);
+                const int cols = (b.i1 - b.i0 + 1) * (b.j1 - b.j0 + 1);
+                c = 1;
 #pragma unroll
-                    for (int t = 0; t < kNCCls; ++t) c += cols <= kCCls[t];
-                    if (cols > g.lane_cols) c = 0;
-                    if ((g.diag == 1 && c == 0) || (g.diag == 2 && c > 0)) c = -1;
-                }
+                for (int t = 0; t < kNCCls; ++t) c += cols <= kCCls[t];
+                if (cols > g.lane_cols) c = 0;
+                if ((g.diag == 1 && c == 0) || (g.diag == 2 && c > 0)) c = -1;
             }
             cr[q] = c < 0 ? 0xffffffffu : ((unsigned)c << 16) | (unsigned)atomicAdd(&qcnt[c], 1);
         }
