@@ -424,8 +424,7 @@ __device__ __forceinline__ void plane_walk(double* col, float fa, float fb, floa
 }
 
 // Per-record constants of the edge-continuous column walk, formed once per record (the
-// walk's loops then hold them in registers).  k0f / k1f are canonical (a clamp by fmaxf
-// would otherwise re-canonicalise them in every column).
+// walk's loops then hold them in registers).
 struct ColE {
     float tin;       // fl32(thr) (1 + 2^-20): columns with s below can meet the sphere
     float tpe;       // fl32(thr) (1 + 2^-19)
@@ -440,8 +439,8 @@ __device__ __forceinline__ ColE col_consts(const Grid3& g, const Rec3& R) {
     K.tpe = R.thrf * (1.0f + 0x1p-19f);
     K.rzs = (float)g.ipz * (1.0f + 0x1p-18f);
     K.kc = R.kc;
-    K.k0f = __builtin_canonicalizef((float)R.b.k0);
-    K.k1f = __builtin_canonicalizef((float)R.b.k1);
+    K.k0f = (float)R.b.k0;
+    K.k1f = (float)R.b.k1;
     K.h2 = R.hinv * R.hinv;
     K.zh = R.zr * R.hinv;
     K.pzh = -(float)g.pz * R.hinv;
@@ -458,8 +457,10 @@ template <int KID>
 __device__ __forceinline__ void column_e(const ColE& K, double* col, float sf) {
     if (!(sf < K.tin)) return;  // the column misses the sphere
     const float rz = fmaf(__builtin_amdgcn_sqrtf(K.tpe - sf), K.rzs, 0x1p-10f);
-    const float fa = fmaxf(ceilf(K.kc - rz), K.k0f);
-    const float fb = fminf(floorf(K.kc + rz), K.k1f);
+    // clamps by v_med3 (an fmaxf / fminf re-canonicalised the per-record bound in every
+    // column: one instruction each)
+    const float fa = __builtin_amdgcn_fmed3f(ceilf(K.kc - rz), K.k0f, 0x1p30f);
+    const float fb = __builtin_amdgcn_fmed3f(floorf(K.kc + rz), -0x1p30f, K.k1f);
     if (!(fa <= fb)) return;
     plane_walk<KID>(col, fa, fb, sf * K.h2, K.zh, K.pzh, K.sc);
 }

@@ -96,9 +96,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=0,
                     help="HIP streams the TIMED region's consecutive maps (cubes) alternate "
                          "between (each its own workspace slot in the library).  0 (auto): 1 "
-                         "for maps -- strictly in sequence, so every kernel's event-timed "
-                         "duration (the roofline) is its own, not shared with another map's "
-                         "kernels -- and 2 for cubes (the deposit dominates either way)")
+                         "-- strictly in sequence, so every kernel's event-timed duration (the "
+                         "roofline) is its own, not shared with another map's kernels")
     ap.add_argument("--overlap-streams", type=int, default=2,
                     help="after the timed region, a second timed region of --steps maps "
                          "alternating between this many streams (0/1: none), reported as "
@@ -277,10 +276,12 @@ def run_cube(args, world, rank, local, dev):
         d = {k: v[keep].contiguous() for k, v in d.items()}
     x, y, z, h, m = d["x"], d["y"], d["z"], d["h"], d["m"]
     n_local = x.shape[0]
-    # consecutive cubes alternate between --streams HIP streams (0 = auto = 2), each with
-    # its own output and library workspace slot: one cube's store-bound scatter runs beside
-    # the previous cube's VALU-bound deposit
-    ns = args.streams if args.streams > 0 else 2
+    # consecutive cubes may alternate between --streams HIP streams, each with its own
+    # output and library workspace slot (one cube's scatter beside the previous cube's
+    # deposit).  Default 1: the deposit's LDS brick leaves no room for a scatter workgroup
+    # beside it, and on the round-5 build two streams measure no faster (14.38-14.45 vs
+    # 14.35 ms)
+    ns = args.streams if args.streams > 0 else 1
     streams = ([torch.cuda.current_stream(dev)] if ns == 1 else
                [torch.cuda.Stream(device=dev) for _ in range(ns)])
     outs = [torch.empty((C, C, K[rank + 1] - K[rank]), dtype=torch.float32, device=dev)
