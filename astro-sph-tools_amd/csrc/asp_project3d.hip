@@ -35,8 +35,17 @@
 
 namespace asp {
 
-constexpr int kBX = 16, kBY = 16, kBZ = 32;  // brick edge (voxels); z fastest
-constexpr int kBXs = 4, kBYs = 4, kBZs = 5;
+// Brick edge (voxels); z fastest.  16 x 16 x 32: two 512-thread deposit workgroups per
+// CU.  32 x 16 x 32 (build switch ASP_CUBE_BX=32; one 1024-thread workgroup per CU, the
+// 128-KiB brick) cuts the records to 1.28 per particle (1.39) and halves the scatter's
+// open brick runs -- scatter 3.76 -> 3.21 ms -- but the deposit ran 9.94 -> 11.15 ms and
+// the merge 0.07 -> 0.25 ms (round 5)
+#ifndef ASP_CUBE_BX
+#define ASP_CUBE_BX 16
+#endif
+constexpr int kBX = ASP_CUBE_BX, kBY = 16, kBZ = 32;
+constexpr int kBXs = kBX == 32 ? 5 : 4, kBYs = 4, kBZs = 5;
+static_assert(kBX == 1 << kBXs, "brick edge in x: 16 or 32");
 constexpr int kBrickVox = kBX * kBY * kBZ;   // 8192 -> 64 KiB of fp64 accumulators
 #ifndef ASP_CUBE_PAD
 #define ASP_CUBE_PAD 1
@@ -64,7 +73,8 @@ __device__ __forceinline__ int lds_vox(int v) {  // dense brick index -> padded 
 }
 constexpr int kMaxBricks = 16384;            // C1/C3 LDS: one int per brick (64 KiB)
 static_assert(kMaxBricks <= kScanThreads * kScanPer, "k_tilescan holds <= kScanPer bricks per thread");
-constexpr int k3Block = 512;                 // count / scatter / deposit workgroup
+constexpr int k3Block = 512;                 // count / scatter / merge workgroup
+constexpr int kDBlock = 2 * kBX * kBY;       // deposit workgroup: two threads per brick column
 #ifndef ASP_CUBE_LANE_COLS
 #define ASP_CUBE_LANE_COLS 48
 #endif
@@ -90,7 +100,7 @@ constexpr int kQCls = 2 + kNCCls;  // the wave class, then the lane classes larg
 #define ASP_CUBE_WAVE_TAKE 32
 #endif
 constexpr int kWaveTake = ASP_CUBE_WAVE_TAKE;  // wave-class records claimed at a time
-static_assert(kRound % k3Block == 0 && kRound <= 65536, "round of whole blocks, 16-bit index");
+static_assert(kRound % kDBlock == 0 && kRound <= 65536, "round of whole blocks, 16-bit index");
 
 struct Grid3 {
     double x_min, y_min, z_min;
@@ -484,7 +494,7 @@ __device__ __forceinline__ void column3(const Grid3& g, const Rec3& R, int li, i
 }
 
 template <int KID>
-__global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __restrict__ recs,
+__global__ __launch_bounds__(kDBlock) void k3_deposit(Grid3 g, const float4* __restrict__ recs,
                                                       const Item* __restrict__ items,
                                                       double* __restrict__ slabs,
                                                       float* __restrict__ out, int accumulate) {
@@ -507,13 +517,13 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
     };
     if (it.count == 0) {  // empty brick
         if (accumulate) return;
-        for (int v = threadIdx.x; v < kBrickVox; v += k3Block) {
+        for (int v = threadIdx.x; v < kBrickVox; v += kDBlock) {
             long long o = out_index(v);
             if (o >= 0) out[o] = 0.0f;
         }
         return;
     }
-    for (int v = threadIdx.x; v < kBrickLds; v += k3Block) acc[v] = 0.0;
+    for (int v = threadIdx.x; v < kBrickLds; v += kDBlock) acc[v] = 0.0;
     if (threadIdx.x < kBX) xt[threadIdx.x] = g.x_min + (double)(I0 + (int)threadIdx.x) * g.px;
     else if (threadIdx.x < kBX + kBY)
         yt[threadIdx.x - kBX] = g.y_min + (double)(J0 + (int)threadIdx.x - kBX) * g.py;
@@ -557,18 +567,18 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
             qhead[threadIdx.x] = 0;
         }
         __syncthreads();
-        unsigned cr[kRound / k3Block];  // class << 16 | rank, per record of this thread
+        unsigned cr[kRound / kDBlock];  // class << 16 | rank, per record of this thread
         // all of this thread's records of the round loaded first: loads interleaved with
         // the class counters' LDS atomics were issued one at a time, each waiting a full
         // memory latency (vmcnt(0)) before the next (round 5)
         // the class from the box the scatter stored in the record's second half
-        float qv[kRound / k3Block];
+        float qv[kRound / kDBlock];
 #pragma unroll
-        for (int q = 0; q < kRound / k3Block; ++q)
-            qv[q] = recs[2 * (it.start + r0i + min(q * k3Block + (int)threadIdx.x, nr - 1)) + 1].y;
+        for (int q = 0; q < kRound / kDBlock; ++q)
+            qv[q] = recs[2 * (it.start + r0i + min(q * kDBlock + (int)threadIdx.x, nr - 1)) + 1].y;
 #pragma unroll
-        for (int q = 0; q < kRound / k3Block; ++q) {
-            const int i = q * k3Block + (int)threadIdx.x;
+        for (int q = 0; q < kRound / kDBlock; ++q) {
+            const int i = q * kDBlock + (int)threadIdx.x;
             int c = -1;
             if (i < nr) {
                 const Box3 b = rec_box(qv[q]);
@@ -591,10 +601,10 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
         }
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < kRound / k3Block; ++q)
+        for (int q = 0; q < kRound / kDBlock; ++q)
             if (cr[q] != 0xffffffffu)
                 qlist[qoff[cr[q] >> 16] + (cr[q] & 0xffffu)] =
-                    (unsigned short)(q * k3Block + (int)threadIdx.x);
+                    (unsigned short)(q * kDBlock + (int)threadIdx.x);
         __syncthreads();
         // claim chunks: the wave class kWaveTake records at a time (each is walked by the
         // whole wave), the lane classes 64 at a time (one per lane).  The next chunk is
@@ -729,7 +739,7 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
     if constexpr (ASP_CUBE_PLANES) {
         // thread t: column c = t mod 256, planes [kh, kh + 16) -- conflict-free LDS reads
         // (adjacent lanes, adjacent columns), 16 consecutive outputs per thread
-        static_assert(k3Block == 2 * kPlane && kBZ == 32, "two half-columns per thread pair");
+        static_assert(kDBlock == 2 * kPlane && kBZ == 32, "two half-columns per thread pair");
         const int c = (int)threadIdx.x & (kPlane - 1), kh = ((int)threadIdx.x / kPlane) * (kBZ / 2);
         if (it.slab >= 0) {  // dense brick order (c * kBZ + k), as k3_merge reads it
             double* dst = slabs + (long long)it.slab * kBrickVox + c * kBZ + kh;
@@ -749,10 +759,10 @@ __global__ __launch_bounds__(k3Block) void k3_deposit(Grid3 g, const float4* __r
     }
     if (it.slab >= 0) {
         double* dst = slabs + (long long)it.slab * kBrickVox;
-        for (int v = threadIdx.x; v < kBrickVox; v += k3Block) dst[v] = acc[lds_vox(v)];
+        for (int v = threadIdx.x; v < kBrickVox; v += kDBlock) dst[v] = acc[lds_vox(v)];
         return;
     }
-    for (int v = threadIdx.x; v < kBrickVox; v += k3Block) {
+    for (int v = threadIdx.x; v < kBrickVox; v += kDBlock) {
         long long o = out_index(v);
         if (o < 0) continue;
         float val = (float)acc[lds_vox(v)];
@@ -945,7 +955,13 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
         StageMark m(ws, kS3Deposit, st);
         size_t lds = (size_t)kBrickLds * sizeof(double) + (kBX + kBY + kBZ) * sizeof(double);
         auto kern = kid == 0 ? k3_deposit<0> : kid == 1 ? k3_deposit<1> : k3_deposit<2>;
-        hipLaunchKernelGGL(kern, dim3(n_items), dim3(k3Block), lds, st, g,
+        static bool lds_set[3] = {false, false, false};  // (per process; idempotent)
+        if (!lds_set[kid]) {
+            ASP_HIP(hipFuncSetAttribute((const void*)kern,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            lds_set[kid] = true;
+        }
+        hipLaunchKernelGGL(kern, dim3(n_items), dim3(kDBlock), lds, st, g,
                            (const float4*)ws.recs.p, (const Item*)ws.items.p,
                            (double*)ws.slabs.p, dout, acc);
         ASP_LAUNCHED();
