@@ -96,10 +96,12 @@ def parse():
     ap.add_argument("--streams", type=int, default=0,
                     help="HIP streams the TIMED region's consecutive maps (cubes) alternate "
                          "between (each its own workspace slot in the library).  0 (auto): 1 "
-                         "-- strictly in sequence, so every kernel's event-timed duration (the "
-                         "roofline) is its own, not shared with another map's kernels")
+                         "on one GPU -- strictly in sequence, so every kernel's event-timed "
+                         "duration (the roofline) is its own, not shared with another map's "
+                         "kernels; 2 for maps on N > 1 GPUs (a rank's share is small, the "
+                         "scatter gated behind the previous deposit for shares <= 2e7)")
     ap.add_argument("--overlap-streams", type=int, default=2,
-                    help="after the timed region, a second timed region of --steps maps "
+                    help="N = 1: after the timed region, a second timed region of --steps maps "
                          "alternating between this many streams (0/1: none), reported as "
                          "'overlapped': map i + 1's binning and scatter run beside map i's "
                          "deposit (store-bound and LDS-bound kernels sharing the CUs), the "
@@ -804,8 +806,12 @@ def main():
                               [torch.cuda.Stream(device=dev) for _ in range(n)])
         return stream_sets[n]
 
-    ns = args.streams if args.streams > 0 else 1
-    nso = args.overlap_streams if args.overlap_streams > 1 else 0
+    # auto: one stream on one GPU (the roofline's kernel durations are then the kernels'
+    # own); two on N > 1, where the line is a scaling point and a rank's share is small
+    # (1.25e7: 0.618 -> 0.538 ms gated, profiles/r05/seq_main/).  The second, overlapped
+    # region runs on one GPU only: at N > 1 the timed region itself already overlaps maps.
+    ns = args.streams if args.streams > 0 else (1 if world == 1 else 2)
+    nso = args.overlap_streams if (args.overlap_streams > 1 and world == 1) else 0
     mode = {"ns": ns, "streams": stream_set(ns)}
     gated = set_gate(ns)
     nbuf = max(ns, nso, 2 if (world > 1 and args.pipeline) else 1)
