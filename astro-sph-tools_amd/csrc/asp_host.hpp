@@ -61,7 +61,7 @@ struct Workspace {
     int pset = 0;                  // the set the current call records into
     double stage_ms[kStages] = {};
     long long stage_n[kStages] = {};
-    Buf knn[10];  // asp_knn_smoothing_lengths (knn[7]: the level-L cell table, knn[8..9]: sub-tables)
+    Buf knn[11];  // asp_knn_smoothing_lengths (knn[7]: the level-L cell table, knn[8..9]: sub-tables, knn[10]: its scan)
     Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
         wide, slabs, morton, aux[6], iorder;
     Buf in64[4];     // asp_project2d_f64: the caller's fp64 arrays, resident for exact decisions
