@@ -684,7 +684,48 @@ __global__ __launch_bounds__(kDBlock) void k3_deposit(Grid3 g, const float4* __r
                 }
             } else {
                 unsigned long long big = __ballot(live);
-                while (big) {
+                if constexpr (KID != 2) {
+                    // each record's column constants formed by its own lane (all 64 at
+                    // once), then broadcast: the whole wave forming them per record cost
+                    // ~10 VALU per wave-class record, as did the first column's division
+                    const ColE Kl = col_consts<KID>(g, R);
+                    const float px = (float)g.px, py = (float)g.py;
+                    while (big) {
+                        const int l = __builtin_ctzll(big);
+                        big &= big - 1;
+                        ColE K;
+                        K.tin = bcast(Kl.tin, l);
+                        K.tpe = bcast(Kl.tpe, l);
+                        K.rzs = Kl.rzs;  // (the same for every record)
+                        K.kc = bcast(Kl.kc, l);
+                        K.k0f = bcast(Kl.k0f, l);
+                        K.k1f = bcast(Kl.k1f, l);
+                        K.h2 = bcast(Kl.h2, l);
+                        K.zh = bcast(Kl.zh, l);
+                        K.pzh = bcast(Kl.pzh, l);
+                        K.sc = bcast(Kl.sc, l);
+                        const float lx = bcast(R.lx, l), ly = bcast(R.ly, l);
+                        const int i0 = bcast(R.b.i0, l), j0 = bcast(R.b.j0, l);
+                        const int qw = bcast(bw, l), qh = bcast(bh, l);
+                        // column cc = ci * qh + cj; a lane's first (ci, cj) by fp32 (exact:
+                        // (lane + 1/2) / qh is never within 1/32 of an integer), its next 64
+                        // columns on by increments
+                        const int di = 64 / qh, dj = 64 - di * qh;
+                        int ci = (int)(((float)lane + 0.5f) * __builtin_amdgcn_rcpf((float)qh));
+                        int cj = lane - ci * qh;
+                        for (int cc = lane; cc < qw * qh; cc += 64) {
+                            const float dx = fmaf(-(float)ci, px, lx), dy = fmaf(-(float)cj, py, ly);
+                            column_e<KID>(K, acc + lds_at(i0 + ci, j0 + cj, 0), fmaf(dx, dx, dy * dy));
+                            ci += di;
+                            cj += dj;
+                            if (cj >= qh) {
+                                cj -= qh;
+                                ++ci;
+                            }
+                        }
+                    }
+                }
+                while (KID == 2 && big) {
                     int l = __builtin_ctzll(big);
                     big &= big - 1;
                     Rec3 Q = {};
@@ -708,17 +749,8 @@ __global__ __launch_bounds__(kDBlock) void k3_deposit(Grid3 g, const float4* __r
                     // next one of a lane 64 further on (one division per record, not per column)
                     const int di = 64 / qh, dj = 64 - di * qh;
                     int ci = lane / qh, cj = lane - ci * qh;
-                    ColE K = {};
-                    if constexpr (KID != 2) K = col_consts<KID>(g, Q);
-                    const float px = (float)g.px, py = (float)g.py;
                     for (int cc = lane; cc < qw * qh; cc += 64) {
-                        if constexpr (KID == 2) {
-                            column3<KID>(g, Q, Q.b.i0 + ci, Q.b.j0 + cj, K0, xt, yt, zt, acc);
-                        } else {
-                            const float dx = fmaf(-(float)ci, px, Q.lx), dy = fmaf(-(float)cj, py, Q.ly);
-                            column_e<KID>(K, acc + lds_at(Q.b.i0 + ci, Q.b.j0 + cj, 0),
-                                          fmaf(dx, dx, dy * dy));
-                        }
+                        column3<KID>(g, Q, Q.b.i0 + ci, Q.b.j0 + cj, K0, xt, yt, zt, acc);
                         ci += di;
                         cj += dj;
                         if (cj >= qh) {
