@@ -74,6 +74,7 @@ __device__ __forceinline__ int lds_vox(int v) {  // dense brick index -> padded 
 constexpr int kMaxBricks = 16384;            // C1/C3 LDS: one int per brick (64 KiB)
 static_assert(kMaxBricks <= kScanThreads * kScanPer, "k_tilescan holds <= kScanPer bricks per thread");
 constexpr int k3Block = 512;                 // count / scatter / merge workgroup
+constexpr int kStage3 = 136;                 // scatter: float4 staging per wave (paired stores)
 constexpr int kDBlock = 2 * kBX * kBY;       // deposit workgroup: two threads per brick column
 #ifndef ASP_CUBE_LANE_COLS
 #define ASP_CUBE_LANE_COLS 48
@@ -251,6 +252,7 @@ __global__ __launch_bounds__(TB) void k3_scatter(
     Grid3 g, const int* __restrict__ hist, const long long* __restrict__ brick_start,
     float4* __restrict__ recs, int inter) {
     extern __shared__ __attribute__((aligned(16))) int cur[];
+    float4* stage = (float4*)(cur + ((g.nb + 3) & ~3)) + (threadIdx.x >> 6) * kStage3;
     constexpr int GRP = TB / k3Block;
     const int* row = hist + (long long)blockIdx.x * GRP * g.nb;
     for (int t = threadIdx.x; t < g.nb; t += TB) cur[t] = (int)brick_start[t] + row[t];
@@ -267,6 +269,29 @@ __global__ __launch_bounds__(TB) void k3_scatter(
     // at 10^8 / 512^3: 23 % of the store lanes busy).  Round 5: scatter 3.96 -> 3.91 ms,
     // 3.83 -> 3.62 with the grouped workgroups.
     const int lane = threadIdx.x & 63;
+    // Paired store (as the 2-D scatter): the wave's records staged in LDS (first halves at
+    // [lane], second halves at [72 + lane]: no bank conflicts either way), then lanes 2j and
+    // 2j + 1 write the two 16-B halves of record j, so one store instruction covers 32
+    // whole 32-B records instead of 64 half records.  slot < 0: no record.  Called by the
+    // whole wave.
+    auto pstore = [&](int slot, const float4& r0, const float4& r1) {
+        stage[lane] = r0;
+        stage[72 + lane] = r1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int src = half * 32 + (lane >> 1);
+            const int sl = __shfl(slot, src);
+            const float4 v = stage[(lane & 1) * 72 + src];
+            if (sl >= 0) {
+                recs[2 * (long long)sl + (lane & 1)] = v;
+                asm volatile("" ::: "memory");  // one dwordx4 store per half record
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    };
     auto bin = [&](float cx, float cy, float cz, float ch, float ca) {
         Box3 b = {};
         int nbr = 0, bi0 = 0, bj0 = 0, bk0 = 0, nj = 1, nk = 1;
@@ -278,13 +303,10 @@ __global__ __launch_bounds__(TB) void k3_scatter(
             nk = ((b.k1 - g.k_lo) >> kBZs) - bk0 + 1;
             nbr = (((b.i1 - g.i_lo) >> kBXs) - bi0 + 1) * nj * nk;
         }
-        if (__ballot(nbr > 1) == 0) {  // one brick at most per lane: store in place
-            if (nbr) {
-                const int slot = atomicAdd(&cur[(bi0 * g.nby + bj0) * g.nbz + bk0], 1);
-                recs[2 * (long long)slot] = make_float4(cx, cy, cz, ch);
-                recs[2 * (long long)slot + 1] =
-                    rec_half1(g, b.i0, b.i1, b.j0, b.j1, b.k0, b.k1, bi0, bj0, bk0, cx, cy, ca);
-            }
+        if (__ballot(nbr > 1) == 0) {  // one brick at most per lane: one record each
+            const int slot = nbr ? atomicAdd(&cur[(bi0 * g.nby + bj0) * g.nbz + bk0], 1) : -1;
+            pstore(slot, make_float4(cx, cy, cz, ch),
+                   rec_half1(g, b.i0, b.i1, b.j0, b.j1, b.k0, b.k1, bi0, bj0, bk0, cx, cy, ca));
             return;
         }
         // the box, packed for the deal (16 bits per bound: cube edges < 65536)
@@ -309,13 +331,10 @@ __global__ __launch_bounds__(TB) void k3_scatter(
             const int t = q / sk, dk = q - t * sk, di = t / sj, dj = t - di * sj;
             const int bi = __shfl(bi0, s) + di, bj = __shfl(bj0, s) + dj, bk = __shfl(bk0, s) + dk;
             const int si = __shfl(pi, s), sjj = __shfl(pj, s), skk = __shfl(pk, s);
-            if (p < total) {
-                const int slot = atomicAdd(&cur[(bi * g.nby + bj) * g.nbz + bk], 1);
-                recs[2 * (long long)slot] = make_float4(fx, fy, fz, fh);
-                recs[2 * (long long)slot + 1] =
-                    rec_half1(g, si & 0xffff, si >> 16, sjj & 0xffff, sjj >> 16, skk & 0xffff,
-                              skk >> 16, bi, bj, bk, fx, fy, fa);
-            }
+            const int slot = p < total ? atomicAdd(&cur[(bi * g.nby + bj) * g.nbz + bk], 1) : -1;
+            pstore(slot, make_float4(fx, fy, fz, fh),
+                   rec_half1(g, si & 0xffff, si >> 16, sjj & 0xffff, sjj >> 16, skk & 0xffff,
+                             skk >> 16, bi, bj, bk, fx, fy, fa));
         }
     };
     // Two particle buffers in ping-pong (no register copies at the loop's back edge, which
@@ -970,8 +989,17 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
         const bool g2 = (ge ? atoi(ge) != 1 : true) && nblk % 2 == 0;
         auto kern = g2 ? (probe ? k3_scatter<1, 2 * k3Block> : k3_scatter<0, 2 * k3Block>)
                        : (probe ? k3_scatter<1, k3Block> : k3_scatter<0, k3Block>);
-        hipLaunchKernelGGL(kern, dim3((unsigned)(g2 ? nblk / 2 : nblk)),
-                           dim3(g2 ? 2 * k3Block : k3Block), lds_bins, st, dx,
+        const int tb = g2 ? 2 * k3Block : k3Block;
+        const size_t lds_sc = (size_t)((g.nb + 3) & ~3) * sizeof(int) +
+                              (size_t)(tb / 64) * kStage3 * sizeof(float4);
+        static bool lds_sc_set[2][2] = {{false, false}, {false, false}};  // [probe][g2]
+        if (!lds_sc_set[probe][g2]) {  // (the largest: 16384 bricks + 16 waves' staging)
+            const size_t mx = (size_t)kMaxBricks * sizeof(int) + (size_t)(tb / 64) * kStage3 * sizeof(float4);
+            ASP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)mx));
+            lds_sc_set[probe][g2] = true;
+        }
+        hipLaunchKernelGGL(kern, dim3((unsigned)(g2 ? nblk / 2 : nblk)), dim3(tb), lds_sc, st, dx,
                            dy, dz, dh, da, n, per_block, g, (const int*)ws.hist.p,
                            (const long long*)ws.tile_start.p, (float4*)ws.recs.p, inter);
         ASP_LAUNCHED();
