@@ -186,11 +186,7 @@ __global__ __launch_bounds__(k3Block) void k3_count(const float* __restrict__ x,
     const long long p1 = inter ? n : min(n, p0 + per_block);
     const Grid3f gf = {(float)g.x_min, (float)g.y_min, (float)g.z_min,
                        (float)g.ipx, (float)g.ipy, (float)g.ipz};
-    float cx, cy, cz, ch;
-    load3(x, y, z, h, p0 + threadIdx.x, p1, cx, cy, cz, ch);
-    for (long long base = p0; base < p1; base += stride) {
-        float nx_, ny_, nz_, nh_;
-        load3(x, y, z, h, base + stride + threadIdx.x, p1, nx_, ny_, nz_, nh_);
+    auto bin = [&](float cx, float cy, float cz, float ch) {
         Box3 b;
         if (footprint3f(g, gf, cx, cy, cz, ch, b)) {
             int bi0 = (b.i0 - g.i_lo) >> kBXs, bi1 = (b.i1 - g.i_lo) >> kBXs;
@@ -201,10 +197,18 @@ __global__ __launch_bounds__(k3Block) void k3_count(const float* __restrict__ x,
                     for (int bk = bk0; bk <= bk1; ++bk)
                         atomicAdd(&lh[(bi * g.nby + bj) * g.nbz + bk], 1);
         }
-        cx = nx_;
-        cy = ny_;
-        cz = nz_;
-        ch = nh_;
+    };
+    // two particle buffers in ping-pong, as the scatter: a copy of the next batch into the
+    // current one at the loop's back edge made the compiler wait for its loads there, so
+    // one batch was in flight at a time (round 5)
+    float ax, ay, az, ah, bx, by, bz, bh;
+    load3(x, y, z, h, p0 + threadIdx.x, p1, ax, ay, az, ah);
+    for (long long base = p0; base < p1; base += 2 * stride) {
+        load3(x, y, z, h, base + stride + threadIdx.x, p1, bx, by, bz, bh);
+        bin(ax, ay, az, ah);
+        if (base + stride >= p1) break;  // block-uniform
+        load3(x, y, z, h, base + 2 * stride + threadIdx.x, p1, ax, ay, az, ah);
+        bin(bx, by, bz, bh);
     }
     __syncthreads();
     int* row = hist + (long long)blockIdx.x * g.nb;
@@ -250,7 +254,10 @@ __global__ __launch_bounds__(TB) void k3_scatter(
     const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
     const float* __restrict__ h, const float* __restrict__ a, long long n, long long per_block,
     Grid3 g, const int* __restrict__ hist, const long long* __restrict__ brick_start,
-    float4* __restrict__ recs, int inter) {
+    float4* __restrict__ recs, int inter, const int* __restrict__ ctr, long long rec_cap) {
+    // speculative launch (enqueued before the host has read the record count): a no-op
+    // when the records would not fit the buffer it was given
+    if ((long long)ctr[cRecs] > rec_cap) return;
     extern __shared__ __attribute__((aligned(16))) int cur[];
     float4* stage = (float4*)(cur + ((g.nb + 3) & ~3)) + (threadIdx.x >> 6) * kStage3;
     constexpr int GRP = TB / k3Block;
@@ -969,19 +976,7 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
         ASP_LAUNCHED();
         m.done();
     }
-    ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, cNum * sizeof(int), hipMemcpyDeviceToHost, st));
-    ASP_HIP(hipStreamSynchronize(st));
-    n_items = ws.h_counters[cItems];
-    n_recs = ws.h_counters[cRecs];
-    n_slabs = ws.h_counters[cSlabs];
-    n_merges = ws.h_counters[cMerges];
-    long long rec_limit = 0x7fffffffLL;  // 32-bit record cursors (ASP_MAX_RECORDS: tests)
-    if (const char* e = getenv("ASP_MAX_RECORDS")) rec_limit = std::max(1LL, atoll(e));
-    if (n_recs >= rec_limit) return kRetSplit3;  // nothing written: the caller splits
-    const void* recs_before = ws.recs.p;
-    ASP_TRY(ensure(ws.recs, (size_t)n_recs * 2 * sizeof(float4)));
-    ASP_TRY(ensure(ws.slabs, (size_t)n_slabs * kBrickVox * sizeof(double)));
-    auto scatter = [&](bool probe) -> int {
+    auto scatter_launch = [&](bool probe, long long cap) -> int {
         StageMark m(ws, kS3Scatter, st);
         // grouped workgroups (GRP 2) need an even count grid; ASP_CUBE_SGRP=1: one count
         // workgroup per scatter workgroup (A/B switch, read per call)
@@ -1001,13 +996,42 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
         }
         hipLaunchKernelGGL(kern, dim3((unsigned)(g2 ? nblk / 2 : nblk)), dim3(tb), lds_sc, st, dx,
                            dy, dz, dh, da, n, per_block, g, (const int*)ws.hist.p,
-                           (const long long*)ws.tile_start.p, (float4*)ws.recs.p, inter);
+                           (const long long*)ws.tile_start.p, (float4*)ws.recs.p, inter,
+                           (const int*)dc, cap);
         ASP_LAUNCHED();
         m.done();
         return ASP_OK;
     };
-    bool placed = false;  // a fresh record buffer: placement trials (asp_host.hpp)
-    if (ws.recs.p != recs_before)
+    auto scatter = [&](bool probe) { return scatter_launch(probe, 0x7ffffffeLL); };
+    // One small read-back sizes the buffers.  With a record buffer left by an earlier call,
+    // the scatter is enqueued BEFORE the host waits for the counters (it checks them against
+    // that buffer's capacity itself), so the GPU does not idle across the host round trip
+    // (as the 2-D path, asp_project2d.hip).
+    ASP_TRY(ensure_side(ws));  // (its events)
+    ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, cNum * sizeof(int), hipMemcpyDeviceToHost, st));
+    ASP_HIP(hipEventRecord(ws.cnt_ev, st));
+    const long long rec_cap =
+        (long long)std::min<size_t>(ws.recs.cap / (2 * sizeof(float4)), 0x7ffffffe);
+    const bool spec = ws.recs.p != nullptr && getenv("ASP_NO_SPECULATE") == nullptr;
+    if (spec) ASP_TRY(scatter_launch(false, rec_cap));
+    ASP_HIP(hipEventSynchronize(ws.cnt_ev));
+    n_items = ws.h_counters[cItems];
+    n_recs = ws.h_counters[cRecs];
+    n_slabs = ws.h_counters[cSlabs];
+    n_merges = ws.h_counters[cMerges];
+    long long rec_limit = 0x7fffffffLL;  // 32-bit record cursors (ASP_MAX_RECORDS: tests)
+    if (const char* e = getenv("ASP_MAX_RECORDS")) rec_limit = std::max(1LL, atoll(e));
+    if (n_recs >= rec_limit) {  // the caller splits (a speculative scatter wrote into spare room)
+        if (spec) ASP_HIP(hipStreamSynchronize(st));
+        return kRetSplit3;
+    }
+    const bool pre = spec && n_recs <= rec_cap;  // the speculative scatter did the work
+    if (spec && !pre) ASP_HIP(hipStreamSynchronize(st));  // its no-op is done: buffer free
+    const void* recs_before = ws.recs.p;
+    ASP_TRY(ensure(ws.recs, (size_t)n_recs * 2 * sizeof(float4)));
+    ASP_TRY(ensure(ws.slabs, (size_t)n_slabs * kBrickVox * sizeof(double)));
+    bool placed = pre;  // a fresh record buffer: placement trials (asp_host.hpp)
+    if (!pre && ws.recs.p != recs_before)
         ASP_TRY(place_records(ws, (size_t)n_recs * 2 * sizeof(float4), st,
                               [&]() { return scatter(true); }, placed));
     if (!placed) ASP_TRY(scatter(false));
