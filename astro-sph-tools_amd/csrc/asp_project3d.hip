@@ -940,7 +940,12 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
     ASP_TRY(ensure(ws.hist, (size_t)nblk * g.nb * sizeof(int)));
     ASP_TRY(ensure(ws.tile_total, (size_t)g.nb * sizeof(int)));
     ASP_TRY(ensure(ws.tile_start, (size_t)g.nb * sizeof(long long)));
-    ASP_TRY(ensure(ws.items, (size_t)(g.nb + kTargetItems + 16) * sizeof(Item)));
+    // target item count: 1024 (round 5; 512 / 1024 / 2048 / 4096: deposit + merge 10.45 /
+    // 9.99-10.04 / 10.06 / 10.15 ms, same process -- fewer split bricks, fewer fp64 slabs
+    // to write and merge); ASP_CUBE_ITEMS overrides (read per call)
+    int target = 1024;
+    if (const char* e = getenv("ASP_CUBE_ITEMS")) target = std::max(64, atoi(e));
+    ASP_TRY(ensure(ws.items, (size_t)(g.nb + target + 16) * sizeof(Item)));
     ASP_TRY(ensure(ws.merges, (size_t)(g.nb + 16) * sizeof(Merge)));
     ASP_TRY(ensure(ws.counters, cNum * sizeof(int)));
     if (!ws.h_counters) ASP_HIP(hipHostMalloc((void**)&ws.h_counters, kMarks * cNum * sizeof(int)));
@@ -967,12 +972,12 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
             hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
                            (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1,
                            (long long*)ws.tile_start.p, (Item*)ws.items.p,
-                           (Merge*)ws.merges.p, dc, (int*)nullptr, 0, kTargetItems);
+                           (Merge*)ws.merges.p, dc, (int*)nullptr, 0, target);
         else
             hipLaunchKernelGGL(k_tilescan<kScanPer>, dim3(1), dim3(kScanThreads), 0, st,
                            (const int*)ws.tile_total.p, (const int*)ws.morton3.p, g.nb, 1,
                            (long long*)ws.tile_start.p, (Item*)ws.items.p,
-                           (Merge*)ws.merges.p, dc, (int*)nullptr, 0, kTargetItems);
+                           (Merge*)ws.merges.p, dc, (int*)nullptr, 0, target);
         ASP_LAUNCHED();
         m.done();
     }
