@@ -198,17 +198,21 @@ __global__ __launch_bounds__(k3Block) void k3_count(const float* __restrict__ x,
                         atomicAdd(&lh[(bi * g.nby + bj) * g.nbz + bk], 1);
         }
     };
-    // two particle buffers in ping-pong, as the scatter: a copy of the next batch into the
-    // current one at the loop's back edge made the compiler wait for its loads there, so
-    // one batch was in flight at a time (round 5)
-    float ax, ay, az, ah, bx, by, bz, bh;
+    // three particle buffers in rotation, two batches ahead: a copy of the next batch into
+    // the current one at the loop's back edge made the compiler wait for its loads there,
+    // so one batch was in flight at a time (round 5)
+    float ax, ay, az, ah, bx, by, bz, bh, cx, cy, cz, ch;
     load3(x, y, z, h, p0 + threadIdx.x, p1, ax, ay, az, ah);
-    for (long long base = p0; base < p1; base += 2 * stride) {
-        load3(x, y, z, h, base + stride + threadIdx.x, p1, bx, by, bz, bh);
+    load3(x, y, z, h, p0 + stride + threadIdx.x, p1, bx, by, bz, bh);
+    for (long long base = p0; base < p1; base += 3 * stride) {
+        load3(x, y, z, h, base + 2 * stride + threadIdx.x, p1, cx, cy, cz, ch);
         bin(ax, ay, az, ah);
         if (base + stride >= p1) break;  // block-uniform
-        load3(x, y, z, h, base + 2 * stride + threadIdx.x, p1, ax, ay, az, ah);
+        load3(x, y, z, h, base + 3 * stride + threadIdx.x, p1, ax, ay, az, ah);
         bin(bx, by, bz, bh);
+        if (base + 2 * stride >= p1) break;
+        load3(x, y, z, h, base + 4 * stride + threadIdx.x, p1, bx, by, bz, bh);
+        bin(cx, cy, cz, ch);
     }
     __syncthreads();
     int* row = hist + (long long)blockIdx.x * g.nb;
