@@ -179,3 +179,21 @@ def test_cube_particle_batches(gpu, oracle, monkeypatch, knob):
     monkeypatch.delenv(knob[0])
     assert np.array_equal(g, oracle.project3d(x, y, z, h, ones, size, EXT, kernel="indicator"))
     assert_map_close(d, oracle.project3d(x, y, z, h, m, size, EXT))
+
+
+def test_cube_speculative_scatter_buffer_growth(gpu, oracle):
+    """The cube scatter is enqueued before the host reads the record count when a record
+    buffer is left from an earlier call (round 5): a small call, then one needing a larger
+    buffer (the speculative launch must be a no-op, the buffer grows, the records are
+    scattered again), then the small one again (fits: the speculative launch is the
+    scatter).  Counts bit-exact each time."""
+    from asp_amd import _lib
+    from asp_amd.tools.projections import create_cube, indicator_kernel
+    _lib.check(_lib.lib().asp_release(0))
+    size = (48, 48, 48)
+    for n, seed in ((5000, 11), (60000, 12), (5000, 13)):
+        x, y, z, h, m = _plummer(n, seed, size)
+        ones = np.ones_like(h)
+        g = create_cube(np.stack([x, y, z], 1), h, ones, size, *EXT, kernel_func=indicator_kernel)
+        r = oracle.project3d(x, y, z, h, ones, size, EXT, kernel="indicator")
+        assert np.array_equal(g, r), (n, np.count_nonzero(g != r))
