@@ -12,11 +12,16 @@
 //                insertions per workgroup -> hist[block][brick]
 //   C2 colscan / tilescan   shared with the 2-D path (asp_binning.hpp), bricks in 3-D
 //                Morton order
-//   C3 scatter   second pass: 32-byte records {x, y, z, h}, {a} into their bricks' runs
-//   C4 deposit   one workgroup per work item: fp64 LDS brick accumulator (64 KiB);
-//                small boxes lane-per-record, large ones swept by a whole wave over the
-//                flattened box; the neighbour decision is the oracle's fp64 arithmetic
-//                (bit-exact neighbour sets), the term A*W is fp32, summed in fp64
+//   C3 scatter   second pass: 32-byte records {x, y, z, h}, {a, box, lx, ly} (the box
+//                clipped to the brick and the column offsets, formed here) into their
+//                bricks' runs; a wave's (particle, brick) pairs dealt one per lane, paired
+//                stores through an LDS stage
+//   C4 deposit   one workgroup per work item, largest first: fp64 LDS brick accumulator
+//                (64 KiB + a spare plane); records classified by their box's column count,
+//                boxes of <= 48 columns lane-per-record, wider ones a wave per record with
+//                lanes over the columns; each column walks only its sphere's planes (packed
+//                fp32 pairs for the edge kernels; the indicator kernel keeps the oracle's
+//                fp64 test: bit-exact neighbour sets); the term A*W is fp32, summed in fp64
 //   C5 merge     bricks split over several items: fp64 slab sum in slab order
 // A call may produce a slab of planes [k_lo, k_hi) only (Z-slab ownership across GPUs,
 // asp_amd.distributed.project3d_sharded).
