@@ -90,7 +90,10 @@ constexpr int kLaneCols = ASP_CUBE_LANE_COLS;  // boxes up to this many (i, j) c
 // Deposit rounds: records classified per round (LDS list of 2-byte indices) and the
 // classes (0: boxes of more than lane_cols columns, 1..kNCCls + 1: lane-per-record boxes by
 // column count, large to small)
-constexpr int kRound = 4096;
+#ifndef ASP_CUBE_ROUND
+#define ASP_CUBE_ROUND 4096
+#endif
+constexpr int kRound = ASP_CUBE_ROUND;
 // Lane classes by the box's column count (round 5): a lane-per-record wave runs
 // max-over-lanes column steps, so records of similar column counts go together.  The box
 // volume classes before (80 / 32 / 12) mixed column counts within a class (CPU model:
