@@ -57,6 +57,11 @@ def parse():
     ap.add_argument("--n", "--particles", dest="n", type=int, default=100_000_000)
     ap.add_argument("--grid", type=int, default=4096)
     ap.add_argument("--h-law", default="pixel", choices=["pixel", "physical"])
+    ap.add_argument("--order", default="random", choices=["random", "cell"],
+                    help="particle order: random (the default workload) or sorted by "
+                         "64x64-pixel tile in Morton order, as a cell-ordered snapshot "
+                         "(SWIFT / EAGLE files store particles by cell): an input-order "
+                         "sensitivity check, not the benchmark")
     ap.add_argument("--kernel", default="wendland_c2", choices=["wendland_c2", "cubic"])
     ap.add_argument("--map", default="weighted", choices=["weighted", "surface"])
     ap.add_argument("--op", default="reduce",
@@ -730,6 +735,15 @@ def main():
     ext = (-extent, extent, -extent, extent)
     t0 = time.time()
     d = plummer_torch(args.n, seed=0, h_law=args.h_law, extent=extent, grid=G, device=dev)
+    if args.order == "cell":  # cell-ordered input (the particles' tile, Morton order)
+        tx = ((d["x"] + extent) * (G / (2 * extent))).long().clamp(0, G - 1) >> 6
+        ty = ((d["y"] + extent) * (G / (2 * extent))).long().clamp(0, G - 1) >> 6
+        key = torch.zeros_like(tx)
+        for b in range(12):  # interleave the tile coordinates' bits
+            key |= ((tx >> b) & 1) << (2 * b + 1) | ((ty >> b) & 1) << (2 * b)
+        perm = torch.argsort(key)
+        d = {k: v[perm].contiguous() for k, v in d.items()}
+        del tx, ty, key, perm
     R = None  # --decomp rows: the row-slab bounds
     partition_ms = None  # --decomp rows: the timed all-to-all from the reader's split
     rows_got = None
@@ -1055,7 +1069,7 @@ def main():
                                       else "gather to rank 0"))
                                   if world > 1 else ""),
                    "particles": args.n, "grid": G, "kernel": args.kernel, "h_law": args.h_law,
-                   "map": args.map,
+                   "map": args.map, **({"order": "cell"} if args.order == "cell" else {}),
                    "parallelism": (f"zslab{world}" if R is None else f"rows{world}")
                    if world > 1 else "single",
                    **({"backend": backend_label, "decomp": args.decomp,
