@@ -109,12 +109,11 @@ static __global__ __launch_bounds__(kColscanBlock) void k_colscan(int* __restric
 // chunked independently: each stream aims at its own item count.
 // ----------------------------------------------------------------------------------
 constexpr int kScanThreads = 1024;
-// Regular items per call (split granularity of the small/mid stream): the cube's bricks
-// (kTargetItems) and the 2-D map's tiles (kTargetItems2d).  2-D, same-box A/B
+// Regular items per call (split granularity of the small/mid stream): the 2-D map's tiles
+// (kTargetItems2d; the cube sets its own, 1024, asp_project3d.hip).  2-D, same-box A/B
 // (profiles/r03/items/): 1024 / 2048 / 4096 items give the 10^8 map 3.229-3.234 /
 // 3.234-3.236 / 3.269-3.276 ms and the 1.25e7 shard (the N = 8 rank) 0.517 / 0.537 /
 // 0.601 ms -- fewer, longer items cost the shard less merge and tilescan work.
-constexpr int kTargetItems = 2048;
 #ifndef ASP_TARGET_ITEMS
 #define ASP_TARGET_ITEMS 1024
 #endif
