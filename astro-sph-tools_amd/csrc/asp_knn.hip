@@ -609,8 +609,16 @@ __device__ __forceinline__ void wave_scan32(long long a, long long b, const doub
     }
 }
 
+#ifndef ASP_KNN_WPE
+#define ASP_KNN_WPE 0  // waves per SIMD the search is compiled for (0: the compiler's choice)
+#endif
+#if ASP_KNN_WPE
+#define ASP_KNN_OCC __attribute__((amdgpu_waves_per_eu(ASP_KNN_WPE)))
+#else
+#define ASP_KNN_OCC
+#endif
 template <int K>
-__global__ __launch_bounds__(kKnnBlock) void k_knn_wave(const double* __restrict__ xs,
+__global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double* __restrict__ xs,
                                                         const double* __restrict__ ys,
                                                         const double* __restrict__ zs,
                                                         const unsigned long long* __restrict__ keys,
