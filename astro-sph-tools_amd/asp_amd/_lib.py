@@ -39,6 +39,7 @@ ASP_ERR_UNSUPPORTED = -4
 # Every symbol include/asp.h declares (tests check the library exports all of them).
 EXPORTS = ("asp_version", "asp_last_error", "asp_device_count", "asp_project2d",
            "asp_project2d_rows", "asp_project2d_props", "asp_project2d_props_f64",
+           "asp_project2d_sph", "asp_project2d_sph_f64",
            "asp_project2d_f64", "asp_pairs_begin", "asp_pairs_emit", "asp_pairs_end",
            "asp_project3d", "asp_kernel_eval", "asp_chunk_ranges", "asp_pixel_neighbours", "asp_ratio",
            "asp_profile", "asp_profile_stages", "asp_profile_read", "asp_last_stats",
@@ -102,6 +103,16 @@ def lib():
                                               C.c_double, C.c_int32, C.c_int32, C.c_int32,
                                               C.c_int32, C.c_int32, C.POINTER(_f), C.c_int32,
                                               C.c_void_p]
+    if hasattr(L, "asp_project2d_sph"):
+        L.asp_project2d_sph.argtypes = [_f, _f, _f, _f, _f, C.POINTER(_f), C.c_int32, C.c_int64,
+                                        C.c_double, C.c_double, C.c_double, C.c_double,
+                                        C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                        C.POINTER(_f), C.c_int32, C.c_void_p]
+        L.asp_project2d_sph_f64.argtypes = [_d, _d, _d, _d, C.POINTER(_d), C.c_int32, C.c_int64,
+                                            C.c_int32, C.c_double, C.c_double, C.c_double,
+                                            C.c_double, C.c_int32, C.c_int32, C.c_int32,
+                                            C.c_int32, C.c_int32, C.POINTER(_f), C.c_int32,
+                                            C.c_void_p]
     L.asp_project2d_f64.argtypes = [_d, _d, _d, _d, C.c_int64, C.c_int32, C.c_double,
                                     C.c_double, C.c_double, C.c_double, C.c_int32, C.c_int32,
                                     C.c_int32, C.c_int32, C.c_int32, _f, _f, C.c_int32,
@@ -185,11 +196,12 @@ def ptr(a, t=_f):
 
 
 def last_stats(device: int = 0):
-    s = (C.c_int64 * 13)()
-    check(lib().asp_last_stats(device, s, 13))
+    s = (C.c_int64 * 15)()
+    check(lib().asp_last_stats(device, s, 15))
     return {"records": s[0], "items": s[1], "wide": s[2], "tile": s[3], "tiles": s[4],
             "records_per_item": s[5], "merges": s[6], "slabs": s[7], "large": s[8],
-            "evals": s[9], "evals_small": s[10], "evals_gather": s[11], "evals_wide": s[12]}
+            "evals": s[9], "evals_small": s[10], "evals_gather": s[11], "evals_wide": s[12],
+            "scatter_path": s[13], "placement_runs": s[14]}
 
 
 def profile(device: int = 0, enable: bool = True, stages=None):

@@ -87,10 +87,15 @@ def project2d(u, v, h, a0, a1=None, *, image_size, extent, chunk_size: int = 64,
 
 
 def project2d_props(u, v, h, props, *, image_size, extent, chunk_size: int = 64,
-                    kernel="cubic", accumulate: bool = False, outs=None, stream=None):
+                    kernel="cubic", accumulate: bool = False, outs=None, stream=None,
+                    mass=None, density=None, ratio: bool = False):
     """asp_project2d_props: one map per property of ``props`` (1..6 device float32 arrays)
     from ONE binning of the particles -- the same neighbour sets, the counting and
-    scattering done once.  Returns the list of (nx, ny) float32 maps."""
+    scattering done once.  Returns the list of (nx, ny) float32 maps.
+
+    ``mass`` (and ``density``): the SPH-weighted maps of asp_project2d_sph,
+    sum_j (m_j / rho_j) A_j W (``density`` None: sum_j m_j A_j W); ``ratio`` (two
+    properties): out0 = the weighted mean of props[0] over props[1]'s weights."""
     import torch
     dev = u.device
     n = u.shape[0]
@@ -101,6 +106,13 @@ def project2d_props(u, v, h, props, *, image_size, extent, chunk_size: int = 64,
         _check(t, name, n, dev)
     for j, a in enumerate(props):
         _check(a, f"props[{j}]", n, dev)
+    if density is not None and mass is None:
+        raise ValueError("density needs mass (the weights are m / rho)")
+    for t, name in ((mass, "mass"), (density, "density")):
+        if t is not None:
+            _check(t, name, n, dev)
+    if ratio and k != 2:
+        raise ValueError("ratio needs exactly two properties")
     nx, ny = int(image_size[0]), int(image_size[1])
     if outs is None:
         outs = [torch.empty((nx, ny), dtype=torch.float32, device=dev) for _ in range(k)]
@@ -110,24 +122,33 @@ def project2d_props(u, v, h, props, *, image_size, extent, chunk_size: int = 64,
         if t.dtype != torch.float32 or t.device != dev or not t.is_contiguous() or \
                 t.numel() != nx * ny:
             raise ValueError("outputs must be contiguous float32 (nx, ny) tensors on the device")
-    flags = _lib.ASP_F_DEVICE_PTRS | (_lib.ASP_F_ACCUMULATE if accumulate else 0)
+    flags = _lib.ASP_F_DEVICE_PTRS | (_lib.ASP_F_ACCUMULATE if accumulate else 0) | \
+        (_lib.ASP_F_RATIO if ratio else 0)
     if stream is None:
         stream = torch.cuda.current_stream(dev).cuda_stream
     P = _lib.ptr
     pa = (_lib._f * k)(*[P(a) for a in props])
     po = (_lib._f * k)(*[P(o) for o in outs])
     x_min, x_max, y_min, y_max = (float(e) for e in extent)
-    _lib.check(_lib.lib().asp_project2d_props(
-        P(u), P(v), P(h), pa, k, n, x_min, x_max, y_min, y_max, nx, ny, int(chunk_size),
-        kernel_id(kernel), flags, po, dev.index or 0, stream))
+    tail = (n, x_min, x_max, y_min, y_max, nx, ny, int(chunk_size), kernel_id(kernel), flags, po,
+            dev.index or 0, stream)
+    if mass is not None:
+        _lib.check(_lib.lib().asp_project2d_sph(
+            P(u), P(v), P(h), P(mass), P(density) if density is not None else None, pa, k,
+            *tail))
+    else:
+        _lib.check(_lib.lib().asp_project2d_props(P(u), P(v), P(h), pa, k, *tail))
     return outs
 
 
 def project2d_props_f64(positions, h, props, *, projection_axis=2, image_size, extent,
-                        chunk_size: int = 64, kernel="cubic", device: int = 0):
+                        chunk_size: int = 64, kernel="cubic", device: int = 0, mass=None,
+                        density=None, ratio: bool = False):
     """asp_project2d_props_f64 on the reader's float64 arrays (host NumPy arrays or float64
     device tensors; host arrays are copied to the device): the maps of every property from
-    one binning, every decision the reference's fp64 test.  Returns float32 device maps."""
+    one binning, every decision the reference's fp64 test.  Returns float32 device maps.
+    ``mass`` / ``density`` / ``ratio``: as :func:`project2d_props` (asp_project2d_sph_f64;
+    the weights m / rho are formed in fp64 from the reader's values)."""
     import numpy as np
     import torch
     from ._axes import axis_index
@@ -156,16 +177,28 @@ def project2d_props_f64(positions, h, props, *, projection_axis=2, image_size, e
     hh = on_dev(np.asarray(h).reshape(-1) if not hasattr(h, "is_cuda") else h.reshape(-1), (n,))
     pr = [on_dev(np.asarray(a).reshape(-1) if not hasattr(a, "is_cuda") else a.reshape(-1), (n,))
           for a in props]
+    if density is not None and mass is None:
+        raise ValueError("density needs mass (the weights are m / rho)")
+    if ratio and k != 2:
+        raise ValueError("ratio needs exactly two properties")
+    flat = lambda a: np.asarray(a).reshape(-1) if not hasattr(a, "is_cuda") else a.reshape(-1)  # noqa: E731
+    wm = None if mass is None else on_dev(flat(mass), (n,))
+    wr = None if density is None else on_dev(flat(density), (n,))
     nx, ny = int(image_size[0]), int(image_size[1])
     outs = [torch.empty((nx, ny), dtype=torch.float32, device=dev) for _ in range(k)]
     P = _lib.ptr
     pa = (_lib._d * k)(*[P(a, _lib._d) for a in pr])
     po = (_lib._f * k)(*[P(o) for o in outs])
     x_min, x_max, y_min, y_max = (float(e) for e in extent)
-    _lib.check(_lib.lib().asp_project2d_props_f64(
-        P(pos, _lib._d), P(hh, _lib._d), pa, k, n, axis, x_min, x_max, y_min, y_max, nx, ny,
-        int(chunk_size), kernel_id(kernel), _lib.ASP_F_DEVICE_PTRS, po, dev.index or 0,
-        torch.cuda.current_stream(dev).cuda_stream))
+    flags = _lib.ASP_F_DEVICE_PTRS | (_lib.ASP_F_RATIO if ratio else 0)
+    tail = (n, axis, x_min, x_max, y_min, y_max, nx, ny, int(chunk_size), kernel_id(kernel), flags,
+            po, dev.index or 0, torch.cuda.current_stream(dev).cuda_stream)
+    if wm is not None:
+        _lib.check(_lib.lib().asp_project2d_sph_f64(
+            P(pos, _lib._d), P(hh, _lib._d), P(wm, _lib._d),
+            P(wr, _lib._d) if wr is not None else None, pa, k, *tail))
+    else:
+        _lib.check(_lib.lib().asp_project2d_props_f64(P(pos, _lib._d), P(hh, _lib._d), pa, k, *tail))
     return outs
 
 

@@ -354,6 +354,11 @@ def row_slabs(nx: int, world_size: int, u=None, u_extent=None, weights=None,
         return [0, nx]
     if nx < W:
         raise ValueError(f"{nx} rows cannot make {W} row slabs")
+    if group is not None and u is None:
+        # every member must join the all-reduce below: a member without particles passes
+        # an empty u (its histogram is zero), never None, or the others would hang
+        raise ValueError("row_slabs with a group needs u on every rank (an empty tensor if "
+                         "the rank holds no particles)")
     if u is None or (u.shape[0] == 0 and group is None):
         inner = [(nx * r) // W for r in range(1, W)]
     else:

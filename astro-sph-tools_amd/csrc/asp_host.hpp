@@ -35,7 +35,7 @@ struct Buf {
 };
 
 constexpr int kStages = 19;
-constexpr int kNStats = 13;  // asp_last_stats
+constexpr int kNStats = 15;  // asp_last_stats
 constexpr int kMarks = 8;  // launches of one stage timed per call
 enum Stage {
     kSMemset = 0, kSCount, kSColscan, kSTilescan, kSScatter, kSScale, kSDeposit, kSMerge,
@@ -61,13 +61,18 @@ struct Workspace {
     int pset = 0;                  // the set the current call records into
     double stage_ms[kStages] = {};
     long long stage_n[kStages] = {};
-    Buf knn[11];  // asp_knn_smoothing_lengths (knn[7]: the level-L cell table, knn[8..9]: sub-tables, knn[10]: its scan)
+    // asp_knn_smoothing_lengths (knn[7]: the level-L cell table, knn[8..9]: sub-tables,
+    // knn[10]: the suffix-minimum block minima of its scan, knn[11]: the ASP_KNN_COUNT
+    // distance counters)
+    Buf knn[12];
     Buf in[5], out[2], hist, cmx, tile_total, tile_start, tile_k, items, merges, counters, recs,
         wide, slabs, morton, aux[6], iorder;
     Buf in64[4];     // asp_project2d_f64: the caller's fp64 arrays, resident for exact decisions
     Buf ext;         // asp_project2d_props: per record, the coefficients of properties 2..5
     Buf inx[4];      // asp_project2d_props_f64: fp32 working copies of properties 2..5
     Buf pairs[4];    // asp_pair_list
+    Buf inw[2];      // asp_project2d_sph(_f64) from host arrays: the masses and densities
+    Buf wts[6];      // asp_project2d_sph(_f64): fp32 working copies of m / rho * property
     int* h_counters = nullptr;  // pinned
     int morton_ntx = -1, morton_nty = -1;
     int morton3_key[3] = {-1, -1, -1};
@@ -99,6 +104,8 @@ struct Workspace {
         for (auto& b : knn) v.push_back(&b);
         for (auto& b : in64) v.push_back(&b);
         for (auto& b : pairs) v.push_back(&b);
+        for (auto& b : inw) v.push_back(&b);
+        for (auto& b : wts) v.push_back(&b);
         return v;
     }
 };
@@ -339,6 +346,33 @@ inline int ensure(Buf& b, size_t bytes) {
         if (rc_ != ASP_OK) return rc_; \
     } while (0)
 
+// Dynamic LDS above the 64 KiB default: the kernel's attribute is raised once per (kernel,
+// device) to at least `bytes`, under a lock -- calls may run on several threads (one per
+// map slot or stream) and several devices in one process.
+inline int allow_dyn_lds(const void* kern, size_t bytes) {
+    if (bytes <= 65536) return ASP_OK;
+    int dev = 0;
+    ASP_HIP(hipGetDevice(&dev));
+    struct Set {
+        const void* kern;
+        int dev;
+        size_t bytes;
+    };
+    static std::mutex mu;
+    static std::vector<Set> done;
+    std::lock_guard<std::mutex> lk(mu);
+    for (Set& d : done)
+        if (d.kern == kern && d.dev == dev) {
+            if (d.bytes >= bytes) return ASP_OK;
+            ASP_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+            d.bytes = bytes;
+            return ASP_OK;
+        }
+    ASP_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    done.push_back({kern, dev, bytes});
+    return ASP_OK;
+}
+
 // Record-buffer placement trials.  The scatter's time depends on where the record buffer
 // lands in physical memory: the same call runs 1.88 or 2.38 ms at 10^8 depending on the
 // allocation (tools/alloc_probe.py: both modes within one process as the
@@ -350,8 +384,10 @@ inline int ensure(Buf& b, size_t bytes) {
 // Used by the 2-D and the 3-D scatter (ws.recs).
 // A one-time cost on the first large call (~3 ms per trial at 10^8); 0 or 1 disables it.
 template <class F>
-inline int place_records(Workspace& ws, size_t bytes, hipStream_t st, F&& scatter, bool& placed) {
+inline int place_records(Workspace& ws, size_t bytes, hipStream_t st, F&& scatter, bool& placed,
+                         int* ntrials = nullptr) {
     placed = false;
+    if (ntrials) *ntrials = 0;
     const char* e = getenv("ASP_PLACEMENT_TRIALS");
     const int trials = e ? std::max(0, atoi(e)) : 16;
     const char* mb = getenv("ASP_PLACEMENT_MIN_MB");  // tests lower it
@@ -369,6 +405,7 @@ inline int place_records(Workspace& ws, size_t bytes, hipStream_t st, F&& scatte
     };
     float best_ms = 0.0f;
     int rc = timed(best_ms);  // the buffer ensure() just allocated
+    int runs = 1;
     float worst_ms = best_ms;
     // Stop once the best placement is 18 % under the slowest seen: the fast mode (1.8 ms at
     // 10^8) is ~20-25 % under the slow one (2.3-2.4 ms).  Round 2 stopped at 15 % under the
@@ -384,6 +421,7 @@ inline int place_records(Workspace& ws, size_t bytes, hipStream_t st, F&& scatte
         ws.recs = cand;
         float ms = 0.0f;
         rc = timed(ms);
+        ++runs;
         worst_ms = std::max(worst_ms, ms);
         if (rc == ASP_OK && ms < 0.97f * best_ms) {
             (void)hipFree(best.p);  // the candidate wins and holds this call's records
@@ -397,6 +435,7 @@ inline int place_records(Workspace& ws, size_t bytes, hipStream_t st, F&& scatte
     }
     (void)hipEventDestroy(t0);
     (void)hipEventDestroy(t1);
+    if (ntrials) *ntrials = runs;
     placed = rc == ASP_OK;
     return rc;
 }

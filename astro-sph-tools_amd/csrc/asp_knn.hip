@@ -811,8 +811,8 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     // one atomic per lane, so off in timed runs) -> asp_last_stats [9] window, [10] cells
     unsigned long long* evc = nullptr;
     if (getenv("ASP_KNN_COUNT")) {
-        ASP_TRY(ensure(ws.knn[10], 2 * sizeof(unsigned long long)));
-        evc = (unsigned long long*)ws.knn[10].p;
+        ASP_TRY(ensure(ws.knn[11], 2 * sizeof(unsigned long long)));
+        evc = (unsigned long long*)ws.knn[11].p;
         ASP_HIP(hipMemsetAsync(evc, 0, 2 * sizeof(unsigned long long), st));
     }
     StageMark msearch(ws, kSKnnSearch, st);

@@ -1956,18 +1956,6 @@ static inline size_t scatter_lds(const Grid& g, int nout, bool det) {
     return scatter_lds_base(g) + (det ? (size_t)g.ntiles * nout * sizeof(unsigned) : 0);
 }
 
-// Dynamic LDS above the 64 KiB default needs the kernel's attribute raised once.
-template <class K>
-static int allow_lds(K kern, size_t bytes) {
-    static bool done = false;  // per kernel instantiation
-    if (!done && bytes > 65536) {
-        ASP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)bytes));
-        done = true;
-    }
-    return ASP_OK;
-}
-
 // K3 on stream st.  rec_cap / wide_cap: the capacities the kernel checks against the
 // device counters (speculative launch; see project2d).
 template <int KID, int NOUT, int ACC, bool CULL, int SRC, int PROBE, int NX>
@@ -2043,6 +2031,7 @@ static int run_tail(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl
     {
         StageMark m(ws, kSDeposit, st);
         const size_t lds = deposit_lds<NOUT>();
+        ASP_TRY(allow_dyn_lds((const void*)k_deposit<KID, NOUT, ACC>, lds));
         hipLaunchKernelGGL((k_deposit<KID, NOUT, ACC>), dim3(pl.n_items), dim3(kDepBlock), lds, st, g, s, (const float4*)ws.recs.p,
                            (const Item*)ws.items.p, (const int*)ws.iorder.p, (const int2*)ws.tile_k.p,
                            (unsigned long long*)ws.slabs.p, o0, o1, dflags, (const float4*)nullptr, 0);
@@ -2105,6 +2094,7 @@ static int run_ext_pass(const Grid& g, const Src64& s, Workspace& ws, const Plan
     const float4* ext = (const float4*)ws.ext.p;
     {
         StageMark m(ws, kSDeposit, st);
+        ASP_TRY(allow_dyn_lds((const void*)k_deposit<KID, NOUT, kAccF64, 1>, deposit_lds<NOUT>()));
         hipLaunchKernelGGL((k_deposit<KID, NOUT, kAccF64, 1>), dim3(pl.n_items), dim3(kDepBlock),
                            deposit_lds<NOUT>(), st, g, s, (const float4*)ws.recs.p,
                            (const Item*)ws.items.p, (const int*)ws.iorder.p,
@@ -2285,6 +2275,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
         xw.ext = (float4*)ws.ext.p;
     }
     bool placed = false;  // the records are already scattered (by the placement trials)
+    int ntrials = 0;      // scatter runs of the placement trials
     if (!bin_only && !xa && !pre && ws.recs.p != recs_before) {
 #define ASP_SC(K, N, A) \
     launch_scatter<K, N, A>(g, s, ws, pl, du, dv, dh, da0, da1, 0x7fffffffLL, 0x7fffffff, st, true)
@@ -2298,7 +2289,8 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
 #undef ASP_SC3
 #undef ASP_SC2
 #undef ASP_SC
-        ASP_TRY(place_records(ws, (size_t)pl.n_recs * 2 * sizeof(float4), st, scatter, placed));
+        ASP_TRY(place_records(ws, (size_t)pl.n_recs * 2 * sizeof(float4), st, scatter, placed,
+                              &ntrials));
     }
     const bool pre_all = pre || placed;
     if (bin_only) {  // the plugin session: the records, for k_pairs
@@ -2357,6 +2349,12 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     ws.stats[6] = pl.n_merges;
     ws.stats[7] = pl.n_slabs;
     ws.stats[8] = pl.n_large;
+    // how this pass's records were scattered: 1 the speculative launch (enqueued before the
+    // counter read-back) was kept, 2 placement trials (stats[14] scatter runs), 3 the
+    // speculative launch found the buffers too small and the scatter was relaunched after
+    // growing them, 0 no earlier buffers (one plain launch)
+    ws.stats[13] = pre ? 1 : placed ? 2 : spec ? 3 : 0;
+    ws.stats[14] = ntrials;
     return ASP_OK;
 }
 
@@ -2435,7 +2433,8 @@ int project2d_full(Workspace& ws, const Grid& full, const Src64& s, const float*
             }
             ASP_TRY(rc);
             ++passes;
-            for (int k : {0, 1, 2, 6, 7, 8, 9, 10, 11, 12}) agg[k] += ws.stats[k];
+            for (int k : {0, 1, 2, 6, 7, 8, 9, 10, 11, 12, 14}) agg[k] += ws.stats[k];
+            agg[13] = std::max(agg[13], ws.stats[13]);
         }
         if (passes > 1 && (flags & ASP_F_RATIO)) {
             const long long npix = (long long)g.nx * g.ny;
@@ -2447,7 +2446,7 @@ int project2d_full(Workspace& ws, const Grid& full, const Src64& s, const float*
             m.done();
         }
     }
-    for (int k : {0, 1, 2, 6, 7, 8, 9, 10, 11, 12}) ws.stats[k] = agg[k];
+    for (int k : {0, 1, 2, 6, 7, 8, 9, 10, 11, 12, 13, 14}) ws.stats[k] = agg[k];
     ws.stats[4] = (long long)((row_hi - row_lo + kTile - 1) / kTile) * full.nty;
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess && &ws != &g_ws[dev]) {  // asp_last_stats reads slot 0
@@ -2529,12 +2528,53 @@ static int check_props(int nxp, const void* const* xprops, float* const* xouts, 
     return ASP_OK;
 }
 
+// SPH weights (asp_project2d_sph, north_star's "mass/rho-weighted scatter"): the fp32
+// working copy of a property A is fl32(A * (m / rho)) -- evaluated in fp64 from the
+// caller's values, rounded once (rho NULL: fl32(A * m)).  The SPH estimate of a field is
+// sum_j (m_j / rho_j) A_j W(r_ij, h_j) (get_densities: _SnapshotBase.py:833); the scatter
+// then bins and deposits these coefficients as any property's.
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_weigh(const T* __restrict__ a, const T* __restrict__ m,
+                                                  const T* __restrict__ rho,
+                                                  float* __restrict__ out, long long n) {
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (long long)gridDim.x * kBlock) {
+        const double w = rho ? (double)m[i] / (double)rho[i] : (double)m[i];
+        out[i] = (float)((double)a[i] * w);
+    }
+}
+
+// The weighted fp32 copies of a0 (, a1) and properties 2.. into ws.wts (slot k = property
+// k), on st; the pointers are redirected to them.
+template <class T>
+static int weigh_props(Workspace& ws, const T* a0, const T* a1, const T* const* xprops, int nxp,
+                       const T* m, const T* rho, long long n, hipStream_t st, const float** da0,
+                       const float** da1, const float** xw) {
+    const T* src[6] = {a0, a1, nullptr, nullptr, nullptr, nullptr};
+    for (int j = 0; j < nxp; ++j) src[2 + j] = xprops[j];
+    const long long blocks = std::min<long long>((n + kBlock - 1) / kBlock, 8192);
+    for (int k = 0; k < 6; ++k) {
+        if (!src[k]) continue;
+        ASP_TRY(ensure(ws.wts[k], (size_t)std::max(n, 1LL) * sizeof(float)));
+        if (n > 0) {
+            hipLaunchKernelGGL(k_weigh<T>, dim3((unsigned)blocks), dim3(kBlock), 0, st, src[k], m,
+                               rho, (float*)ws.wts[k].p, n);
+            ASP_LAUNCHED();
+        }
+    }
+    *da0 = (const float*)ws.wts[0].p;
+    if (a1) *da1 = (const float*)ws.wts[1].p;
+    for (int j = 0; j < nxp; ++j) xw[j] = (const float*)ws.wts[2 + j].p;
+    return ASP_OK;
+}
+
 static int project2d(const float* u, const float* v, const float* h, const float* a0,
                      const float* a1, long long n, double x_min, double x_max, double y_min,
                      double y_max, int nx, int ny, int cs, int kid, int flags, float* out0,
                      float* out1, int device, void* stream, int row_lo = 0, int row_hi = -1,
                      const float* const* xprops = nullptr, int nxp = 0,
-                     float* const* xouts = nullptr) {
+                     float* const* xouts = nullptr, const float* wm = nullptr,
+                     const float* wr = nullptr) {
     ASP_TRY(check_args(a1, out0, out1, n, kid, flags));
     ASP_TRY(check_props(nxp, (const void* const*)xprops, xouts, flags));
     if (nxp > 0 && !a1) return fail(ASP_ERR_INVALID, "properties 2.. need a1 / out1");
@@ -2569,9 +2609,25 @@ static int project2d(const float* u, const float* v, const float* h, const float
         da1 = nout == 2 ? (const float*)ws.in[4].p : nullptr;
         ASP_TRY(host_outputs(ws, out0, out1, npix, flags, st, d0, d1));
     }
+    const float* xw[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (int j = 0; j < nxp; ++j) xw[j] = xprops[j];
+    if (wm) {  // asp_project2d_sph: the properties times m / rho
+        const float *dm = wm, *dr = wr;
+        if (!dev) {
+            const float* src[2] = {wm, wr};
+            for (int k = 0; k < 2; ++k) {
+                if (!src[k]) continue;
+                ASP_TRY(ensure(ws.inw[k], (size_t)n * sizeof(float)));
+                ASP_TRY(h2d_staged(ws, ws.inw[k].p, src[k], (size_t)n * sizeof(float), st));
+            }
+            dm = (const float*)ws.inw[0].p;
+            dr = wr ? (const float*)ws.inw[1].p : nullptr;
+        }
+        ASP_TRY(weigh_props<float>(ws, da0, da1, xprops, nxp, dm, dr, n, st, &da0, &da1, xw));
+    }
     const Src64 s{nullptr, nullptr, nullptr, nullptr, nullptr, 0, du, dv, dh};
     XArgs xa{};
-    for (int j = 0; j < 4; ++j) xa.a[j] = j < nxp ? xprops[j] : (nxp ? xprops[0] : nullptr);
+    for (int j = 0; j < 4; ++j) xa.a[j] = j < nxp ? xw[j] : (nxp ? xw[0] : nullptr);
     ASP_TRY(project2d_full(ws, g, s, du, dv, dh, da0, da1, n, kid, flags, d0, d1, st, row_lo,
                            row_hi, nxp ? &xa : nullptr, nxp, xouts));
     if (!dev) ASP_TRY(host_results(out0, out1, d0, d1, npix, st));
@@ -2592,7 +2648,8 @@ static int project2d_f64(const double* pos, const double* h, const double* a0,
                          double y_min, double y_max, int nx, int ny, int cs, int kid, int flags,
                          float* out0, float* out1, int device, void* stream,
                          const double* const* xprops = nullptr, int nxp = 0,
-                         float* const* xouts = nullptr) {
+                         float* const* xouts = nullptr, const double* wm = nullptr,
+                         const double* wr = nullptr) {
     ASP_TRY(check_args(a1, out0, out1, n, kid, flags));
     ASP_TRY(check_props(nxp, (const void* const*)xprops, xouts, flags));
     if (nxp > 0 && !a1) return fail(ASP_ERR_INVALID, "properties 2.. need a1 / out1");
@@ -2634,12 +2691,32 @@ static int project2d_f64(const double* pos, const double* h, const double* a0,
     for (int k = 0; k < 4 + (nout == 2); ++k) ASP_TRY(ensure(ws.in[k], (size_t)n * sizeof(float)));
     float* f[5] = {(float*)ws.in[0].p, (float*)ws.in[1].p, (float*)ws.in[2].p, (float*)ws.in[3].p,
                    nout == 2 ? (float*)ws.in[4].p : nullptr};
-    ASP_TRY(stage_device(dpos, dh64, da0, da1, n, axis, f[0], f[1], f[2], f[3], f[4], st));
+    // asp_project2d_sph_f64: the properties' fp32 copies are m / rho * A (weigh_props), so
+    // the staging converts positions and h only
+    ASP_TRY(stage_device(dpos, dh64, wm ? nullptr : da0, wm ? nullptr : da1, n, axis, f[0], f[1],
+                         f[2], wm ? nullptr : f[3], wm ? nullptr : f[4], st));
+    const float* fa0 = f[3];
+    const float* fa1 = f[4];
+    const float* xw[4] = {nullptr, nullptr, nullptr, nullptr};
+    if (wm) {
+        const double *dm = wm, *dr = wr;
+        if (!dev) {
+            const double* src[2] = {wm, wr};
+            for (int k = 0; k < 2; ++k) {
+                if (!src[k]) continue;
+                ASP_TRY(ensure(ws.inw[k], (size_t)n * sizeof(double)));
+                ASP_TRY(h2d_staged(ws, ws.inw[k].p, src[k], (size_t)n * sizeof(double), st));
+            }
+            dm = (const double*)ws.inw[0].p;
+            dr = wr ? (const double*)ws.inw[1].p : nullptr;
+        }
+        ASP_TRY(weigh_props<double>(ws, da0, da1, xprops, nxp, dm, dr, n, st, &fa0, &fa1, xw));
+    }
     static const int cols[3][2] = {{1, 2}, {0, 2}, {0, 1}};  // _projector.py:38-46
     const Src64 s{dpos + cols[axis][0], dpos + cols[axis][1], dpos + cols[cull_axis][0],
                   dpos + cols[cull_axis][1], dh64, 3, f[0], f[1], f[2]};
     XArgs xa{};
-    for (int j = 0; j < nxp; ++j) {  // fp32 working copies of properties 2..
+    for (int j = 0; j < nxp && !wm; ++j) {  // fp32 working copies of properties 2..
         ASP_TRY(ensure(ws.inx[j], (size_t)std::max(n, 1LL) * sizeof(float)));
         if (n > 0) {
             const long long blocks = std::min<long long>((n + kBlock - 1) / kBlock, 8192);
@@ -2647,9 +2724,10 @@ static int project2d_f64(const double* pos, const double* h, const double* a0,
                                (float*)ws.inx[j].p, n);
             ASP_LAUNCHED();
         }
+        xw[j] = (const float*)ws.inx[j].p;
     }
-    for (int j = 0; j < 4; ++j) xa.a[j] = nxp ? (const float*)ws.inx[j < nxp ? j : 0].p : nullptr;
-    ASP_TRY(project2d_full(ws, g, s, f[0], f[1], f[2], f[3], f[4], n, kid,
+    for (int j = 0; j < 4; ++j) xa.a[j] = nxp ? xw[j < nxp ? j : 0] : nullptr;
+    ASP_TRY(project2d_full(ws, g, s, f[0], f[1], f[2], fa0, fa1, n, kid,
                            (flags & ~ASP_F_DEVICE_OUTPUTS) | ASP_F_DEVICE_PTRS, d0, d1, st, 0, -1,
                            nxp ? &xa : nullptr, nxp, xouts));
     if (!dev_out) ASP_TRY(host_results(out0, out1, d0, d1, npix, st));
@@ -2945,6 +3023,39 @@ int asp_project2d_props_f64(const double* positions, const double* h,
                          nprops > 1 ? outs[1] : nullptr, device, stream,
                          nprops > 2 ? props + 2 : nullptr, std::max(0, nprops - 2),
                          nprops > 2 ? outs + 2 : nullptr);
+}
+
+int asp_project2d_sph(const float* u, const float* v, const float* h, const float* mass,
+                      const float* rho, const float* const* props, int32_t nprops, int64_t n,
+                      double u_min, double u_max, double v_min, double v_max, int32_t nx,
+                      int32_t ny, int32_t chunk_size, int32_t kernel_id, int32_t flags,
+                      float* const* outs, int32_t device, void* stream) {
+    t_err.clear();
+    if (nprops < 1 || nprops > 6 || !props || !outs)
+        return fail(ASP_ERR_INVALID, "nprops must be 1 .. 6 with props / outs given");
+    if (n > 0 && !mass) return fail(ASP_ERR_INVALID, "NULL mass array");
+    return project2d(u, v, h, props[0], nprops > 1 ? props[1] : nullptr, n, u_min, u_max, v_min,
+                     v_max, nx, ny, chunk_size, kernel_id, flags, outs[0],
+                     nprops > 1 ? outs[1] : nullptr, device, stream, 0, -1,
+                     nprops > 2 ? props + 2 : nullptr, std::max(0, nprops - 2),
+                     nprops > 2 ? outs + 2 : nullptr, mass, rho);
+}
+
+int asp_project2d_sph_f64(const double* positions, const double* h, const double* mass,
+                          const double* rho, const double* const* props, int32_t nprops,
+                          int64_t n, int32_t axis, double u_min, double u_max, double v_min,
+                          double v_max, int32_t nx, int32_t ny, int32_t chunk_size,
+                          int32_t kernel_id, int32_t flags, float* const* outs, int32_t device,
+                          void* stream) {
+    t_err.clear();
+    if (nprops < 1 || nprops > 6 || !props || !outs)
+        return fail(ASP_ERR_INVALID, "nprops must be 1 .. 6 with props / outs given");
+    if (n > 0 && !mass) return fail(ASP_ERR_INVALID, "NULL mass array");
+    return project2d_f64(positions, h, props[0], nprops > 1 ? props[1] : nullptr, n, axis, u_min,
+                         u_max, v_min, v_max, nx, ny, chunk_size, kernel_id, flags, outs[0],
+                         nprops > 1 ? outs[1] : nullptr, device, stream,
+                         nprops > 2 ? props + 2 : nullptr, std::max(0, nprops - 2),
+                         nprops > 2 ? outs + 2 : nullptr, mass, rho);
 }
 
 int asp_project2d_f64(const double* positions, const double* h, const double* a0,

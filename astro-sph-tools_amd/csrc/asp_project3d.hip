@@ -328,8 +328,8 @@ __global__ __launch_bounds__(TB) void k3_scatter(
                    rec_half1(g, b.i0, b.i1, b.j0, b.j1, b.k0, b.k1, bi0, bj0, bk0, cx, cy, ca));
             return;
         }
-        // the box, packed for the deal (16 bits per bound: cube edges < 65536)
-        const int pi = b.i0 | b.i1 << 16, pj = b.j0 | b.j1 << 16, pk = b.k0 | b.k1 << 16;
+        // the box's six absolute bounds are dealt unpacked (any cube edge: a 16-bit packing
+        // overflowed the sign bit from voxel 32768 on)
         int incl = nbr;  // inclusive scan of the pair counts over the wave
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -349,11 +349,11 @@ __global__ __launch_bounds__(TB) void k3_scatter(
             const int q = p - __shfl(excl, s);
             const int t = q / sk, dk = q - t * sk, di = t / sj, dj = t - di * sj;
             const int bi = __shfl(bi0, s) + di, bj = __shfl(bj0, s) + dj, bk = __shfl(bk0, s) + dk;
-            const int si = __shfl(pi, s), sjj = __shfl(pj, s), skk = __shfl(pk, s);
+            const int i0 = __shfl(b.i0, s), i1 = __shfl(b.i1, s), j0 = __shfl(b.j0, s);
+            const int j1 = __shfl(b.j1, s), k0 = __shfl(b.k0, s), k1 = __shfl(b.k1, s);
             const int slot = p < total ? atomicAdd(&cur[(bi * g.nby + bj) * g.nbz + bk], 1) : -1;
             pstore(slot, make_float4(fx, fy, fz, fh),
-                   rec_half1(g, si & 0xffff, si >> 16, sjj & 0xffff, sjj >> 16, skk & 0xffff,
-                             skk >> 16, bi, bj, bk, fx, fy, fa));
+                   rec_half1(g, i0, i1, j0, j1, k0, k1, bi, bj, bk, fx, fy, fa));
         }
     };
     // Two particle buffers in ping-pong (no register copies at the loop's back edge, which
@@ -937,7 +937,10 @@ static bool make_grid3(const double* ext, int nx, int ny, int nz, int k_lo, int 
     return true;
 }
 
-constexpr int kRetSplit3 = 1;  // internal: >= 2^31 records in one pass, nothing written
+// internal: >= 2^31 records in one pass.  The speculative scatter (enqueued before the
+// counters are read) may already have written records into the spare capacity of the
+// existing buffer; the caller's split discards them.
+constexpr int kRetSplit3 = 1;
 
 // One window (w.i_lo, w.nxl; <= kMaxBricks bricks) of the cube on stream st: count,
 // scans, scatter (placement trials on a fresh record buffer), deposit, merge.
@@ -1010,13 +1013,9 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
         const int tb = g2 ? 2 * k3Block : k3Block;
         const size_t lds_sc = (size_t)((g.nb + 3) & ~3) * sizeof(int) +
                               (size_t)(tb / 64) * kStage3 * sizeof(float4);
-        static bool lds_sc_set[2][2] = {{false, false}, {false, false}};  // [probe][g2]
-        if (!lds_sc_set[probe][g2]) {  // (the largest: 16384 bricks + 16 waves' staging)
-            const size_t mx = (size_t)kMaxBricks * sizeof(int) + (size_t)(tb / 64) * kStage3 * sizeof(float4);
-            ASP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)mx));
-            lds_sc_set[probe][g2] = true;
-        }
+        // (the largest: 16384 bricks + 16 waves' staging, so the attribute is set once)
+        ASP_TRY(allow_dyn_lds((const void*)kern, (size_t)kMaxBricks * sizeof(int) +
+                                                     (size_t)(tb / 64) * kStage3 * sizeof(float4)));
         hipLaunchKernelGGL(kern, dim3((unsigned)(g2 ? nblk / 2 : nblk)), dim3(tb), lds_sc, st, dx,
                            dy, dz, dh, da, n, per_block, g, (const int*)ws.hist.p,
                            (const long long*)ws.tile_start.p, (float4*)ws.recs.p, inter,
@@ -1062,12 +1061,7 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
         StageMark m(ws, kS3Deposit, st);
         size_t lds = (size_t)kBrickLds * sizeof(double) + (kBX + kBY + kBZ) * sizeof(double);
         auto kern = kid == 0 ? k3_deposit<0> : kid == 1 ? k3_deposit<1> : k3_deposit<2>;
-        static bool lds_set[3] = {false, false, false};  // (per process; idempotent)
-        if (!lds_set[kid]) {
-            ASP_HIP(hipFuncSetAttribute((const void*)kern,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            lds_set[kid] = true;
-        }
+        ASP_TRY(allow_dyn_lds((const void*)kern, lds));
         hipLaunchKernelGGL(kern, dim3(n_items), dim3(kDBlock), lds, st, g,
                            (const float4*)ws.recs.p, (const Item*)ws.items.p, (const int*)iord,
                            (double*)ws.slabs.p, dout, acc);
@@ -1200,6 +1194,7 @@ static int project3d(const float* x, const float* y, const float* z, const float
     ws.stats[6] = agg[2];
     ws.stats[7] = agg[3];
     ws.stats[8] = n > 0 ? 1 : 0;
+    for (int k = 9; k < kNStats; ++k) ws.stats[k] = 0;  // 2-D-only counters
     if (&ws != &g_ws[device]) {  // asp_last_stats reads slot 0 (under its lock, as in 2-D)
         std::lock_guard<std::mutex> lk(g_ws[device].mu);
         std::copy(ws.stats, ws.stats + kNStats, g_ws[device].stats);

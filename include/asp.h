@@ -140,6 +140,31 @@ int asp_project2d_props_f64(const double *positions, const double *h,
                             int32_t device, void *stream);
 
 /*
+ * SPH-weighted property maps -- north_star's "mass/rho-weighted scatter" over the SoA
+ * (x, y, z, h, m, rho, A): out_k = sum_j (m_j / rho_j) props[k]_j W(r_ij, h_j), the SPH
+ * estimate of the field props[k] integrated along the line of sight, with rho the
+ * reader's densities (io/data_structures/_SnapshotBase.py:833, get_densities) and m its
+ * masses (:618-700).  rho NULL: the mass-weighted sums sum_j m_j props[k]_j W.  Each
+ * property's fp32 working copy is fl32(props[k] * (m / rho)), evaluated in fp64 and
+ * rounded once on the device; binning, neighbour decisions and the deposit are
+ * asp_project2d_props'(_f64) -- so with nprops = 2 and ASP_F_RATIO, out0 is the
+ * (m/rho)-weighted mean of props[0] over props[1]'s weights.  Host pointers are accepted
+ * for nprops <= 2 (as asp_project2d / asp_project2d_f64); mass / rho live where the
+ * properties live.
+ */
+int asp_project2d_sph(const float *u, const float *v, const float *h, const float *mass,
+                      const float *rho, const float *const *props, int32_t nprops, int64_t n,
+                      double u_min, double u_max, double v_min, double v_max, int32_t nx,
+                      int32_t ny, int32_t chunk_size, int32_t kernel_id, int32_t flags,
+                      float *const *outs, int32_t device, void *stream);
+int asp_project2d_sph_f64(const double *positions, const double *h, const double *mass,
+                          const double *rho, const double *const *props, int32_t nprops,
+                          int64_t n, int32_t axis, double u_min, double u_max, double v_min,
+                          double v_max, int32_t nx, int32_t ny, int32_t chunk_size,
+                          int32_t kernel_id, int32_t flags, float *const *outs, int32_t device,
+                          void *stream);
+
+/*
  * create_image on the reader's own float64 arrays: the drop-in for create_image
  * (_projector.py:75-120) as it is called, with positions (n, 3) float64 row-major (the
  * reader's get_positions, _SnapshotBase.py:708-722), smoothing lengths and properties
@@ -367,8 +392,12 @@ int asp_table_interp(const double *table, int32_t ndim, const int32_t *shape,
  * stats[8] = records in the large (gathered) stream; with the environment variable
  * ASP_COUNT_EVALS set (diagnostic: one extra kernel, a host sync), the (pixel, particle)
  * lane-slots the deposit kernels spend: stats[9] total = stats[10] small / mid-size stream
- * + stats[11] gathered large stream + stats[12] wide particles (else 0).  Images of more
- * than 4096 tiles and batched calls: the sums over all passes.
+ * + stats[11] gathered large stream + stats[12] wide particles (else 0); stats[13] how the
+ * records were scattered (1 the speculative scatter enqueued before the counter read-back
+ * was kept, 2 record-placement trials, 3 the speculative scatter found the buffers too
+ * small and was relaunched after growing them, 0 one plain launch; the largest code over
+ * the passes), stats[14] scatter runs of the placement trials.  Images of more than 4096
+ * tiles and batched calls: the sums over all passes.
  */
 int asp_last_stats(int32_t device, int64_t *stats, int32_t nstats);
 

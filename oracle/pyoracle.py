@@ -16,7 +16,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+# ASP_ORACLE_LIB: another build of the same source (tests/test_oracle_sanitized.py loads the
+# AddressSanitizer / UBSan build oracle/_san/liboracle_san.so through it)
+LIB_PATH = os.environ.get("ASP_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 
 KERNELS = {"cubic": 0, "quartic_spline_kernel": 0, "wendland_c2": 1, "indicator": 2}
 AXIS_COLS = {0: (1, 2), 1: (0, 2), 2: (0, 1)}

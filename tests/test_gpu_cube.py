@@ -166,6 +166,33 @@ def test_cube_x_windows_beyond_16384_bricks(gpu, oracle):
     assert_map_close(d, oracle.project3d(x, y, z, h, m, size, ext))
 
 
+def test_cube_axis_beyond_32768_multibrick(gpu, oracle):
+    """An elongated 40000 x 40 x 36 cube: particles near voxel 32768 and beyond, with
+    footprints over several 16 x 16 x 32 bricks (the scatter's multi-brick deal).  Voxel
+    bounds past 32767 used to be packed in 16-bit halves of a signed word (ADVICE r05);
+    counts bit-exact and density within the bar against oracle_project3d."""
+    from asp_amd.tools.projections import create_cube, indicator_kernel
+    size = (40000, 40, 36)
+    ext = (0.0, 4000.0, 0.0, 4.0, 0.0, 3.6)  # 0.1 per voxel on every axis
+    rng = np.random.default_rng(17)
+    n = 3000
+    x = np.concatenate([rng.uniform(3200.0, 3400.0, n // 2), rng.uniform(3900.0, 4000.0, n // 2)])
+    y = rng.uniform(0.0, 4.0, n)
+    z = rng.uniform(0.0, 3.6, n)
+    h = rng.uniform(0.3, 1.2, n)  # 2h of 6-24 voxels: several bricks per particle
+    m = rng.uniform(0.5, 2.0, n)
+    x, y, z, h, m = _f32(x, y, z, h, m)
+    pos = np.stack([x, y, z], 1)
+    ones = np.ones_like(h)
+    g = create_cube(pos, h, ones, size, *ext, kernel_func=indicator_kernel)
+    r = oracle.project3d(x, y, z, h, ones, size, ext, kernel="indicator")
+    assert r[32768:].sum() > 0 and r[32000:32768].sum() > 0
+    assert np.array_equal(g, r), f"{np.count_nonzero(g != r)} voxels differ"
+    del g, r
+    d = create_cube(pos, h, m, size, *ext)
+    assert_map_close(d, oracle.project3d(x, y, z, h, m, size, ext))
+
+
 @pytest.mark.parametrize("knob", [("ASP_MAX_BATCH", "7000"), ("ASP_MAX_RECORDS", "9000")])
 def test_cube_particle_batches(gpu, oracle, monkeypatch, knob):
     from asp_amd.tools.projections import create_cube, indicator_kernel

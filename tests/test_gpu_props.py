@@ -88,3 +88,67 @@ def test_props_argument_errors(gpu):
                                         -4.0, 4.0, 64, 64, 64, 1,
                                         _lib.ASP_F_DEVICE_PTRS | _lib.ASP_F_RATIO, po, 0, None)
     assert rc == _lib.ASP_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("nprops", [2, 5])
+def test_sph_weighted_maps_vs_oracle(gpu, oracle, nprops):
+    """asp_project2d_sph (north_star's mass/rho-weighted scatter over (x, y, z, h, m, rho,
+    A)): map_k = sum_j (m_j / rho_j) A_kj W against the oracle on the composed property
+    A' = A m / rho (fp64); the two-property ratio is the (m/rho)-weighted mean.  rho from
+    the Plummer law, so the weights span orders of magnitude.  Reference getters:
+    _SnapshotBase.py:833 (get_densities), the maps _projector.py:75-120."""
+    import torch
+    from asp_amd.device import project2d_props
+    from asp_amd.plummer import plummer
+    from test_gpu_parity import assert_map_close, assert_ratio_close
+    G, ext = 512, (-3.0, 3.0, -3.0, 3.0)
+    p = plummer(300_000, seed=13, h_law="physical")
+    f32 = lambda a: np.ascontiguousarray(a, np.float32)  # noqa: E731
+    x, y, h, m, T = (f32(a) for a in (p["pos"][:, 0], p["pos"][:, 1], p["h"], p["m"], p["T"]))
+    rho = f32(p["rho"])
+    props = [T, np.ones_like(T), f32(T * T * 1e-4), f32(1.0 + x * x), f32(np.abs(y))][:nprops]
+    dev = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    kw = dict(image_size=(G, G), extent=ext, kernel="wendland_c2")
+    outs = project2d_props(dev(x), dev(y), dev(h), [dev(a) for a in props], mass=dev(m),
+                           density=dev(rho), **kw)
+    d64 = lambda a: a.astype(np.float64)  # noqa: E731
+    w = d64(m) / d64(rho)
+    for a, o in zip(props, outs):
+        want, _ = oracle.project_scatter(d64(x), d64(y), d64(h), d64(a) * w, None, (G, G), 64,
+                                         *ext, kernel="wendland_c2")
+        assert_map_close(o.cpu().numpy(), want)
+    # rho omitted: mass-weighted sums
+    mo = project2d_props(dev(x), dev(y), dev(h), [dev(props[0])], mass=dev(m), **kw)[0]
+    want, _ = oracle.project_scatter(d64(x), d64(y), d64(h), d64(props[0]) * d64(m), None,
+                                     (G, G), 64, *ext, kernel="wendland_c2")
+    assert_map_close(mo.cpu().numpy(), want)
+    if nprops == 2:  # the (m/rho)-weighted mean temperature
+        q = project2d_props(dev(x), dev(y), dev(h), [dev(T), dev(np.ones_like(T))], mass=dev(m),
+                            density=dev(rho), ratio=True, **kw)[0]
+        o0, o1 = oracle.project_scatter(d64(x), d64(y), d64(h), d64(T) * w, w, (G, G), 64, *ext,
+                                        kernel="wendland_c2")
+        assert_ratio_close(q.cpu().numpy(), o0, o1)
+
+
+def test_sph_weighted_f64_reader_arrays(gpu, oracle):
+    """asp_project2d_sph_f64 on the reader's raw fp64 arrays (host): the weights formed in
+    fp64 and rounded once; values against the oracle on A m / rho, neighbour sets those of
+    the unweighted fp64 path (exact decisions), for a mixed axis spelling too."""
+    from asp_amd.device import project2d_props_f64
+    from test_gpu_parity import assert_map_close
+    rng = np.random.default_rng(31)
+    n = 40_000
+    pos = rng.normal(0, 0.5, (n, 3))
+    h = rng.uniform(0.005, 0.15, n)
+    m = rng.uniform(0.5, 2.0, n)
+    rho = np.exp(rng.uniform(-6, 3, n))
+    A = rng.uniform(1e3, 1e6, n)
+    G, ext = (384, 256), (-2.0, 2.0, -2.0, 2.0)
+    for axis in (2, 0):
+        maps = project2d_props_f64(pos, h, [A, np.ones(n)], projection_axis=axis, image_size=G,
+                                   extent=ext, kernel="cubic", mass=m, density=rho)
+        cols = {2: (0, 1), 0: (1, 2)}[axis]
+        for a, got in zip((A, np.ones(n)), maps):
+            want, _ = oracle.project_scatter(pos[:, cols[0]], pos[:, cols[1]], h, a * m / rho,
+                                             None, G, 64, *ext, kernel="cubic")
+            assert_map_close(got.cpu().numpy(), want)

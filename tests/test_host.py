@@ -213,3 +213,12 @@ def test_bench_n_gt_1_defaults(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
     a = b.parse()
     assert a.decomp == "zslab" and a.op == "reduce" and a.rows_gather == "all"
+
+
+def test_row_slabs_group_needs_u():
+    """A group member passing u=None would skip the all-reduce the others join (a hang);
+    it is refused instead."""
+    import pytest
+    from asp_amd.distributed import row_slabs
+    with pytest.raises(ValueError, match="needs u on every rank"):
+        row_slabs(4096, 4, None, (-1.0, 1.0), group=object())

@@ -11,7 +11,7 @@
 # (round 4's one-off scripts tools/gpu/r04/*.sh are all instances of these modes)
 cd "$GRAFT_REPO_ROOT" || exit 9
 export TMPDIR=/tmp
-o=gpurun_out/${OUT:-r05}; mkdir -p $o
+o=gpurun_out/${OUT:-r06}; mkdir -p $o
 mode=$1; shift
 summ() {  # name: ms, output check, dominant kernel, frac, per-stage ms
   python3 -c "import json,sys;d=json.loads(open('$o/$1.json').read().strip().splitlines()[-1]);r=d.get('roofline',{});print('$1', d['ms_per_step'], d.get('output_ok'), r.get('kernel'), r.get('frac'), 'ovl', (d.get('overlapped') or {}).get('ms_per_step'), (d.get('overlapped') or {}).get('output_ok'), {k:round(v.get('ms_per_step', v.get('ms_per_launch', 0)),3) for k,v in d.get('stages',{}).items()})"
