@@ -48,7 +48,7 @@ EXPORTS = ("asp_version", "asp_last_error", "asp_device_count", "asp_project2d",
 
 STAGES = ("memset", "count", "colscan", "tilescan", "scatter", "scale", "deposit", "merge",
           "wide", "ratio", "cube_count", "cube_colscan", "cube_tilescan", "cube_scatter",
-          "cube_deposit", "cube_merge", "gather", "knn_prep", "knn_search", "sp_finalize")
+          "cube_deposit", "cube_merge", "gather", "knn_prep", "knn_search")
 
 _lib = None
 

@@ -34,7 +34,7 @@ struct Buf {
     size_t cap = 0;
 };
 
-constexpr int kStages = 20;
+constexpr int kStages = 19;
 constexpr int kNStats = 15;  // asp_last_stats
 constexpr int kMarks = 8;  // launches of one stage timed per call
 enum Stage {
@@ -43,8 +43,7 @@ enum Stage {
     // 3-D cube (asp_project3d)
     kS3Count = 10, kS3Colscan, kS3Tilescan, kS3Scatter, kS3Deposit, kS3Merge,
     kSGather = 16,  // 2-D gathered deposit of the large-record stream
-    kSKnnPrep = 17, kSKnnSearch = 18,  // k-NN: keys / sort / tables; the search kernel
-    kSSPFinalize = 19  // single-pass binning experiment (ASP_SP_EXPERIMENT): chunk lists
+    kSKnnPrep = 17, kSKnnSearch = 18  // k-NN: keys / sort / tables; the search kernel
 };
 
 struct Workspace {
@@ -74,9 +73,6 @@ struct Workspace {
     Buf pairs[4];    // asp_pair_list
     Buf inw[2];      // asp_project2d_sph(_f64) from host arrays: the masses and densities
     Buf wts[6];      // asp_project2d_sph(_f64): fp32 working copies of m / rho * property
-    // single-pass binning experiment (ASP_SP_EXPERIMENT): the chunk pool,
-    // its directory, the control words, per-column chunk counts / starts, the chunk lists
-    Buf sp_pool, sp_dir, sp_ctl, sp_col, sp_clist;
     int* h_counters = nullptr;  // pinned
     int morton_ntx = -1, morton_nty = -1;
     int morton3_key[3] = {-1, -1, -1};
@@ -110,7 +106,6 @@ struct Workspace {
         for (auto& b : pairs) v.push_back(&b);
         for (auto& b : inw) v.push_back(&b);
         for (auto& b : wts) v.push_back(&b);
-        for (Buf* b : {&sp_pool, &sp_dir, &sp_ctl, &sp_col, &sp_clist}) v.push_back(b);
         return v;
     }
 };

@@ -69,12 +69,6 @@ constexpr int kCountUnroll = ASP_COUNT_UNROLL;  // particles per lane and batch 
 constexpr int kScatterBlock = ASP_SCATTER_BLOCK;
 constexpr int kScatterGroup = ASP_SCATTER_GROUP_DEF;
 constexpr int kUnroll = (int)(kCountBlock * kCountUnroll / kScatterBlock);  // particles per lane and batch in scatter
-// batches a scatter loop iteration takes at once (ASP_SCATTER_BATCHES, an A/B build switch;
-// 1 measured best)
-#ifndef ASP_SCATTER_BATCHES
-#define ASP_SCATTER_BATCHES 1
-#endif
-constexpr int kSB = ASP_SCATTER_BATCHES;
 // Particles per loop iteration of a count / scatter workgroup (a "batch").  Batches are
 // dealt to the count workgroups round-robin (batch j to workgroup j % nblk; the scatter
 // workgroup of count workgroups sb*grp.. takes their batches in order), so at any moment
@@ -258,31 +252,13 @@ __device__ __forceinline__ void load_props(const float* __restrict__ a0,
 struct XArgs {
     const float* a[4];
     float4* ext;
-    // single-pass binning experiment (SP = 1, ASP_SP_EXPERIMENT): records go to 16-record
-    // chunks of a pool, claimed per (workgroup, column) while scattering, instead of to the
-    // runs the count pass sized.  pool: the chunks (2 float4 per record), dir: per chunk its
-    // column | fill << 16 (-1 unused), ctl: [0] superblocks claimed (chunks), [1] failure bits
-    float4* pool;
-    int* dir;
-    int* ctl;
-    long long pool_chunks;
 };
-
-// SP chunk geometry: 16 records (512 B, 4 lines) per chunk, chunks claimed from
-// workgroup-private superblocks of 256 chunks (one global atomic per 128 KiB).
-constexpr int kSPChunkShift = 4;
-constexpr int kSPChunk = 1 << kSPChunkShift;
-constexpr int kSPSBShift = 8;
-constexpr int kSPSB = 1 << kSPSBShift;
-constexpr int kSPMaxSB = 1024;  // superblocks per workgroup (its LDS table)
-constexpr int kSPEmpty = -0x7fffffff;
-constexpr int kSPSpinMax = 1 << 20;  // bounded waits: a stuck wait sets a failure bit
 
 // Per-wave staging of the paired record stores: first halves at [lane], second halves at
 // [72 + lane] (8 float4 apart: neither the b128 writes nor the b128 reads conflict).
 constexpr int kStageF4 = 136;
 
-template <int KID, int NOUT, int ACC, bool CULL, int SRC, int PROBE, int NX = 0, int SP = 0>
+template <int KID, int NOUT, int ACC, bool CULL, int SRC, int PROBE, int NX = 0>
 __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     const float* __restrict__ u, const float* __restrict__ v, const float* __restrict__ h,
     const float* __restrict__ a0, const float* __restrict__ a1, long long n, long long nblk,
@@ -300,115 +276,31 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
     // 8 float4 further on, so neither the b128 writes nor the b128 reads conflict)
     float4* stage = (float4*)(cur + 2 * g.ntiles);
     unsigned* cm = (unsigned*)(stage + (kScatterBlock / 64) * kStageF4);
-    // SP: per column a ring of the addresses of its chunks k and k + 1 (tag k & 255 in the
-    // top byte, chunk id below), the superblock table and the pool cursor
-    unsigned* ring = (unsigned*)(stage + (kScatterBlock / 64) * kStageF4);
-    int* sbt = (int*)(ring + (SP ? 4 * g.ntiles : 0));
-    int* sp_cnt = sbt + kSPMaxSB;
     // this workgroup takes over count workgroups grp * sb ..: its cursors start at the
     // prefix row of the first of them
     const long long sb = blockIdx.x;
-    if constexpr (SP) {
-        for (int t = threadIdx.x; t < 2 * g.ntiles; t += kScatterBlock) {
-            cur[t] = 0;  // records of the column so far (this workgroup's)
-            ring[2 * t] = 254u << 24;      // tags k - 2: nothing written yet
-            ring[2 * t + 1] = 255u << 24;
-        }
-        for (int q = threadIdx.x; q < kSPMaxSB; q += kScatterBlock) sbt[q] = kSPEmpty;
-        if (threadIdx.x == 0) {  // superblocks 0 and 1; each later one is claimed one ahead
-            const int b = atomicAdd(&xa.ctl[0], 2 * kSPSB);
-            const bool ok = (long long)b + 2 * kSPSB <= xa.pool_chunks;
-            if (!ok) atomicOr(&xa.ctl[1], 1);
-            sbt[0] = ok ? b : -1;
-            sbt[1] = ok ? b + kSPSB : -1;
-            *sp_cnt = 0;
-        }
-    } else {
-        const int* row = hist + sb * grp * 2 * g.ntiles;
-        for (int t = threadIdx.x; t < 2 * g.ntiles; t += kScatterBlock)
-            cur[t] = (int)tile_start[t] + row[t];  // n_recs < 2^31 (checked on the host)
-        if constexpr (ACC == kAccFix)
-            for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kScatterBlock) cm[t] = 0u;
-    }
+    const int* row = hist + sb * grp * 2 * g.ntiles;
+    for (int t = threadIdx.x; t < 2 * g.ntiles; t += kScatterBlock)
+        cur[t] = (int)tile_start[t] + row[t];  // n_recs < 2^31 (checked on the host)
+    if constexpr (ACC == kAccFix)
+        for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kScatterBlock) cm[t] = 0u;
     __syncthreads();
-    // SP: a chunk of this workgroup's pool (global chunk id; -1 on failure)
-    auto sp_alloc = [&]() -> int {
-        const int j = atomicAdd(sp_cnt, 1);
-        const int q = j >> kSPSBShift, r = j & (kSPSB - 1);
-        if (q + 2 >= kSPMaxSB) {
-            atomicOr(&xa.ctl[1], 2);
-            return -1;
-        }
-        if (r == 0 && q >= 1) {  // superblock q + 1, one ahead of its first use
-            int b = atomicAdd(&xa.ctl[0], kSPSB);
-            if ((long long)b + kSPSB > xa.pool_chunks) {
-                atomicOr(&xa.ctl[1], 1);
-                b = -1;
-            }
-            __hip_atomic_store(&sbt[q + 1], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        int base = kSPEmpty;
-        for (int spin = 0; spin < kSPSpinMax; ++spin) {
-            base = __hip_atomic_load(&sbt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (base != kSPEmpty) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (base == kSPEmpty) atomicOr(&xa.ctl[1], 4);
-        return base < 0 ? -1 : base + r;
-    };
-    // SP: the slot of the next record of column col (record index in the pool; -1 failed)
-    auto sp_slot = [&](int col) -> int {
-        const int i = atomicAdd(&cur[col], 1);
-        const int k = i >> kSPChunkShift, o = i & (kSPChunk - 1);
-        // The record opening chunk k claims it and publishes it in ring slot k & 1 (over
-        // chunk k - 2's entry: a lane still reading that one would lag 17+ records behind;
-        // claiming one chunk ahead instead let two lanes of ONE instruction at 16k - 1 and
-        // 16k overwrite each other's entry -- measured: failure bit 8 on the first map).
-        if (o == 0) {
-            const int a = sp_alloc();
-            if (a >= 0) xa.dir[a] = col | (kSPChunk << 16);
-            __hip_atomic_store(&ring[2 * col + (k & 1)],
-                               ((unsigned)(k & 255) << 24) | (unsigned)(a & 0xffffff),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        unsigned e = 0u;
-        int d = -1;
-        for (int spin = 0; spin < kSPSpinMax; ++spin) {
-            e = __hip_atomic_load(&ring[2 * col + (k & 1)], __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-            d = (int)(((e >> 24) - (unsigned)k) & 255u);
-            if (d != 254) break;  // 254: still chunk k - 2 (chunk k's claim not yet stored)
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (d != 0) {  // lapped (2) or never stored: failure
-            atomicOr(&xa.ctl[1], 8);
-            return -1;
-        }
-        if ((e & 0xffffffu) == 0xffffffu) return -1;  // its claim failed (flagged there)
-        return (int)(e & 0xffffffu) * kSPChunk + o;
-    };
-    float4* const R = SP ? xa.pool : recs;
-    // the batches of count workgroups sb * grp .. (< nblk), in order:
-    // batch it * nblk + sb * grp + j for j < gcnt, it = 0, 1, ...
+    // the batches of count workgroups sb * grp .. (< nblk), in order: batch q * nblk +
+    // sb * grp + r for r < gcnt, q = 0, 1, ...  The loop steps (q, r) and carries the batch's
+    // first particle index c: a division by gcnt per batch made the compiler emit two
+    // 64-bit divisions per iteration (SALU was 147 instructions per wave and iteration,
+    // round 6).  One batch per iteration: 2 and 4 batches measured slower (1.794 / 1.918 vs
+    // 1.756 ms, round 5, DESIGN_LOG.md §18) -- the scatter is bound by its stores, not by
+    // load latency.  Lane particle k of the batch at c: c + k * kScatterBlock + threadIdx.x
+    // (coalesced dword loads).  Every load is unconditional -- index clamped to the last
+    // particle, h = 0 past the end (no footprint) -- so the compiler can count the loads in
+    // flight: with load_vec's vector-or-scalar branches it put s_waitcnt vmcnt(0) right after
+    // issuing the NEXT batch's loads.
     const long long gcnt = min((long long)grp, nblk - sb * grp);
-    auto batch_base = [&](long long c) {
-        return ((c / gcnt) * nblk + sb * grp + c % gcnt) * kBatch;
-    };
-    // A loop iteration takes kSB consecutive batches of this workgroup (kLane particles per
-    // lane).  More batches per iteration put more loads in flight per wave and wait less
-    // often for the previous iteration's stores (gfx950 counts loads and stores in one
-    // vmcnt), but measured slower: 1 / 2 / 4 batches 1.756 / 1.794 / 1.918 ms (same box,
-    // round 5) -- the scatter is bound by its stores, not by load latency.
-    // Lane particle k of iteration c: batch c * kSB + k / kUnroll,
-    // base + (k % kUnroll) * kScatterBlock + threadIdx.x (coalesced dword loads).  Every load
-    // is unconditional -- index clamped to the last particle, h = 0 past the end (no
-    // footprint) -- so the compiler can count the loads in flight: with load_vec's
-    // vector-or-scalar branches it put s_waitcnt vmcnt(0) right after issuing the NEXT
-    // batch's loads.
-    constexpr int kLane = kUnroll * kSB;
-    auto pidx = [&](long long c, int k) {
-        return batch_base(c * kSB + k / kUnroll) + (long long)(k % kUnroll) * kScatterBlock +
-               threadIdx.x;
+    auto base_of = [&](long long q, long long r) { return (q * nblk + sb * grp + r) * kBatch; };
+    constexpr int kLane = kUnroll;
+    auto pidx = [&](long long b, int k) {
+        return b + (long long)k * kScatterBlock + threadIdx.x;
     };
     auto ld = [&](const float* __restrict__ a, long long c, float* out) {
 #pragma unroll
@@ -463,16 +355,22 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             for (int j = 0; j < 4; ++j) ld(xa.a[j], c, dst[j]);
         }
     };
-    load_all(0, pu, pv, ph, pa0, pa1);
-    load_src(0, pU, pV);
-    load_x(0, px);
-    for (long long c = 0; batch_base(c * kSB) < n; ++c) {
+    long long bq = 0, br = 0;
+    long long c = base_of(0, 0);  // the current batch's first particle
+    load_all(c, pu, pv, ph, pa0, pa1);
+    load_src(c, pU, pV);
+    load_x(c, px);
+    while (c < n) {
+        const bool wrap = br + 1 == gcnt;
+        bq += wrap ? 1 : 0;
+        br = wrap ? 0 : br + 1;
+        const long long cn = base_of(bq, br);  // the next batch's
         float nu[kLane], nv[kLane], nh[kLane], na0[kLane], na1[kLane];
-        load_all(c + 1, nu, nv, nh, na0, na1);
+        load_all(cn, nu, nv, nh, na0, na1);
         double nU[kLane], nV[kLane];
-        load_src(c + 1, nU, nV);
+        load_src(cn, nU, nV);
         float nx_[NX ? 4 : 1][kLane];
-        load_x(c + 1, nx_);
+        load_x(cn, nx_);
 #pragma unroll
         for (int k = 0; k < kLane; ++k) {
             const int p = (int)pidx(c, k);
@@ -519,7 +417,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                 const int t = tx * g.nty + ty;
                 const unsigned bp = tile_box(b, tx, ty);
                 const int col = mb && box_large(bp, g) ? t + g.ntiles : t;
-                int slot = SP ? sp_slot(col) : atomicAdd(&cur[col], 1);
+                int slot = atomicAdd(&cur[col], 1);
                 if constexpr (NX) rec_store(&xa.ext[slot], cx);
                 if constexpr (ACC == kAccFix) {
                     atomicMax(&cm[t * NOUT], c0);
@@ -528,12 +426,12 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                 if (first) {
                     first_slot[k] = slot;  // written by the paired store below
                     first_box[k] = bp;
-                } else if (!SP || slot >= 0) {
-                    rec_store(&R[2 * (long long)slot],
+                } else {
+                    rec_store(&recs[2 * (long long)slot],
                               make_float4((float)(U - corner_x(g, max(b.x0, tx * kTile))),
                                           (float)(V - corner_y(g, max(b.y0, ty * kTile))),
                                           ph[k], cf0));
-                    rec_store(&R[2 * (long long)slot + 1],
+                    rec_store(&recs[2 * (long long)slot + 1],
                               make_float4(cf1, __int_as_float(p), band, __uint_as_float(bp)));
                 }
             };
@@ -567,7 +465,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                 int src = half * 32 + (lane >> 1);
                 int slot = __shfl(first_slot[k], src);
                 float4 val = st[(lane & 1) * 72 + src];
-                if (slot >= 0) rec_store(&R[2 * (long long)slot + (lane & 1)], val);
+                if (slot >= 0) rec_store(&recs[2 * (long long)slot + (lane & 1)], val);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -588,83 +486,12 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int k = 0; k < kLane; ++k) px[j][k] = nx_[j][k];
+        c = cn;
     }
     __syncthreads();
     if constexpr (ACC == kAccFix) {
         unsigned* out = cmx + (long long)blockIdx.x * g.ntiles * NOUT;  // per scatter block
         for (int t = threadIdx.x; t < g.ntiles * NOUT; t += kScatterBlock) out[t] = cm[t];
-    }
-    if constexpr (SP) {  // each column's last chunk: its fill
-        for (int t = threadIdx.x; t < 2 * g.ntiles; t += kScatterBlock) {
-            const int c = cur[t];
-            if (c == 0) continue;
-            const int kl = (c - 1) >> kSPChunkShift;
-            const unsigned el = ring[2 * t + (kl & 1)];
-            if (((el >> 24) & 255u) == (unsigned)(kl & 255)) {
-                if ((el & 0xffffffu) != 0xffffffu)
-                    xa.dir[el & 0xffffffu] = t | ((c - (kl << kSPChunkShift)) << 16);
-            } else {
-                atomicOr(&xa.ctl[1], 16);
-            }
-        }
-    }
-}
-
-// SP finalize: the chunk lists per column from the directory (counting sort of chunk ids by
-// column).  k_sp_count: per-workgroup LDS histogram -> col_cnt; k_sp_scan: exclusive
-// prefix (one workgroup); k_sp_place: each chunk id to its column's list.
-constexpr int kSPFinBlock = 1024;
-__global__ __launch_bounds__(kSPFinBlock) void k_sp_count(const int* __restrict__ dir,
-                                                          const int* __restrict__ ctl, int ncol,
-                                                          int* __restrict__ col_cnt) {
-    extern __shared__ int lc[];
-    for (int c = threadIdx.x; c < ncol; c += kSPFinBlock) lc[c] = 0;
-    __syncthreads();
-    const long long nch = ctl[0];
-    for (long long i = (long long)blockIdx.x * kSPFinBlock + threadIdx.x; i < nch;
-         i += (long long)gridDim.x * kSPFinBlock) {
-        const int d = dir[i];
-        if (d >= 0) atomicAdd(&lc[d & 0xffff], 1);
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < ncol; c += kSPFinBlock)
-        if (lc[c]) atomicAdd(&col_cnt[c], lc[c]);
-}
-__global__ __launch_bounds__(kSPFinBlock) void k_sp_scan(int* __restrict__ col_cnt, int ncol,
-                                                         int* __restrict__ col_start) {
-    __shared__ int part[kSPFinBlock];
-    const int per = (ncol + kSPFinBlock - 1) / kSPFinBlock;
-    const int c0 = min(ncol, (int)threadIdx.x * per), c1 = min(ncol, c0 + per);
-    int s = 0;
-    for (int c = c0; c < c1; ++c) s += col_cnt[c];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 1; o < kSPFinBlock; o <<= 1) {
-        const int x = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-        __syncthreads();
-        part[threadIdx.x] += x;
-        __syncthreads();
-    }
-    int b = part[threadIdx.x] - s;
-    for (int c = c0; c < c1; ++c) {
-        col_start[c] = b;
-        b += col_cnt[c];
-        col_cnt[c] = 0;  // the placement's cursors
-    }
-}
-__global__ __launch_bounds__(kSPFinBlock) void k_sp_place(const int* __restrict__ dir,
-                                                          const int* __restrict__ ctl,
-                                                          const int* __restrict__ col_start,
-                                                          int* __restrict__ col_cur,
-                                                          int* __restrict__ clist) {
-    const long long nch = ctl[0];
-    for (long long i = (long long)blockIdx.x * kSPFinBlock + threadIdx.x; i < nch;
-         i += (long long)gridDim.x * kSPFinBlock) {
-        const int d = dir[i];
-        if (d >= 0) {
-            const int c = d & 0xffff;
-            clist[col_start[c] + atomicAdd(&col_cur[c], 1)] = (int)i;
-        }
     }
 }
 
@@ -2144,82 +1971,6 @@ static int scatter_variant(const Grid& g, const Src64& s, Workspace& ws, const P
     return ASP_OK;
 }
 
-// Single-pass binning EXPERIMENT (ASP_SP_EXPERIMENT=1; DESIGN.md §4, verdict r05 item 1):
-// the scatter claims 16-record chunks per (workgroup, column) while it scatters (SP = 1)
-// into a pool, and three small kernels build the per-column chunk lists a count-free
-// deposit would walk.  It measures the cost of that bookkeeping against the count pass and
-// scans it would replace; the deposit still reads the records of the last two-pass scatter
-// (the placement trials' -- bench maps repeat the same particles), so maps stay right but
-// the timing of the SP scatter and its finalize is what the experiment reports.  Fp32
-// inputs, square grids, two fp64 maps only; never on by default.
-static bool sp_experiment() {
-    static const bool on = getenv("ASP_SP_EXPERIMENT") && atoi(getenv("ASP_SP_EXPERIMENT")) != 0;
-    return on;
-}
-
-template <int KID>
-static int launch_scatter_sp(const Grid& g, const Src64& s, Workspace& ws, const Plan& pl,
-                             const float* u, const float* v, const float* h, const float* a0,
-                             const float* a1, hipStream_t st) {
-    const int ncol = 2 * g.ntiles;
-    long long chunks = pl.n / kSPChunk * 3 / 2 + (long long)ncol * pl.nblk_s + 2LL * kSPSB * pl.nblk_s + kSPSB;
-    chunks = std::min<long long>(chunks, 0xfffff0LL);  // 24-bit chunk ids
-    ASP_TRY(ensure(ws.sp_pool, (size_t)chunks * kSPChunk * 2 * sizeof(float4)));
-    ASP_TRY(ensure(ws.sp_dir, (size_t)chunks * sizeof(int)));
-    ASP_TRY(ensure(ws.sp_ctl, 4 * sizeof(int)));
-    ASP_TRY(ensure(ws.sp_col, (size_t)2 * ncol * sizeof(int)));
-    ASP_TRY(ensure(ws.sp_clist, (size_t)chunks * sizeof(int)));
-    int* ctl = (int*)ws.sp_ctl.p;
-    int* col_cnt = (int*)ws.sp_col.p;
-    ASP_HIP(hipMemsetAsync(ctl, 0, 4 * sizeof(int), st));
-    {
-        StageMark m(ws, kSScatter, st);
-        XArgs xa{};
-        xa.pool = (float4*)ws.sp_pool.p;
-        xa.dir = (int*)ws.sp_dir.p;
-        xa.ctl = ctl;
-        xa.pool_chunks = chunks;
-        // cursors + staging, the two-entry rings of every column, the superblock table
-        const size_t lds = scatter_lds_base(g) + (size_t)2 * ncol * sizeof(unsigned) +
-                           (kSPMaxSB + 1) * sizeof(int);
-        auto kern = k_scatter<KID, 2, kAccF64, false, 0, 0, 0, 1>;
-        ASP_TRY(allow_dyn_lds((const void*)kern, lds));
-        hipLaunchKernelGGL(kern, dim3((unsigned)pl.nblk_s), dim3(kScatterBlock), lds, st, u, v,
-                           h, a0, a1, pl.n, pl.nblk, g, s, (const int*)ws.hist.p,
-                           (const long long*)ws.tile_start.p, (const int*)ws.tile_total.p,
-                           (float4*)ws.recs.p, (unsigned*)ws.cmx.p, (int*)ws.wide.p,
-                           (int*)ws.counters.p, pl.grp, 0x7fffffffLL, 0x7fffffff, xa);
-        ASP_LAUNCHED();
-        m.done();
-    }
-    {
-        StageMark m(ws, kSSPFinalize, st);
-        ASP_HIP(hipMemsetAsync(col_cnt, 0, (size_t)ncol * sizeof(int), st));
-        hipLaunchKernelGGL(k_sp_count, dim3(256), dim3(kSPFinBlock), (size_t)ncol * sizeof(int), st,
-                           (const int*)ws.sp_dir.p, (const int*)ctl, ncol, col_cnt);
-        ASP_LAUNCHED();
-        hipLaunchKernelGGL(k_sp_scan, dim3(1), dim3(kSPFinBlock), 0, st, col_cnt, ncol,
-                           col_cnt + ncol);
-        ASP_LAUNCHED();
-        hipLaunchKernelGGL(k_sp_place, dim3(256), dim3(kSPFinBlock), 0, st, (const int*)ws.sp_dir.p,
-                           (const int*)ctl, (const int*)(col_cnt + ncol), col_cnt,
-                           (int*)ws.sp_clist.p);
-        ASP_LAUNCHED();
-        m.done();
-    }
-    int hc[2] = {0, 0};
-    ASP_HIP(hipMemcpyAsync(hc, ctl, sizeof(hc), hipMemcpyDeviceToHost, st));
-    ASP_HIP(hipStreamSynchronize(st));
-    static int reports = 0;
-    if (hc[1] != 0 || reports < 2) {
-        ++reports;
-        fprintf(stderr, "asp SP experiment: %d chunks claimed of %lld (%.2f GB), failure bits %d\n",
-                hc[0], chunks, (double)hc[0] * kSPChunk * 32 / 1e9, hc[1]);
-    }
-    if (hc[1] != 0) return fail(ASP_ERR_UNSUPPORTED, "SP experiment: chunk bookkeeping failed");
-    return ASP_OK;
-}
-
 // xa (asp_project2d_props): also write every record's coefficients of properties 2..5
 // (two-map fp64 calls only).
 template <int KID, int NOUT, int ACC>
@@ -2227,10 +1978,6 @@ static int launch_scatter(const Grid& g, const Src64& s, Workspace& ws, const Pl
                           const float* u, const float* v, const float* h, const float* a0,
                           const float* a1, long long rec_cap, int wide_cap, hipStream_t st,
                           bool probe = false, const XArgs* xa = nullptr) {
-    if constexpr (NOUT == 2 && ACC == kAccF64) {
-        if (!probe && !xa && !(g.nonsquare || g.mixed) && !s.u64 && sp_experiment())
-            return launch_scatter_sp<KID>(g, s, ws, pl, u, v, h, a0, a1, st);
-    }
     StageMark m(ws, kSScatter, st);
     const XArgs none{};
     int rc;

@@ -152,3 +152,32 @@ def test_sph_weighted_f64_reader_arrays(gpu, oracle):
             want, _ = oracle.project_scatter(pos[:, cols[0]], pos[:, cols[1]], h, a * m / rho,
                                              None, G, 64, *ext, kernel="cubic")
             assert_map_close(got.cpu().numpy(), want)
+
+
+def test_sph_f64_host_arrays_through_the_c_abi(gpu, oracle):
+    """INTEGRATION.md §3's binding: asp_project2d_sph_f64 on the reader's HOST float64
+    arrays (no device pointers; positions, h, m, rho and the property staged by the library),
+    the map written to a host float32 buffer; ρ NULL gives the mass-weighted map."""
+    import ctypes as C
+    from asp_amd import _lib
+    from test_gpu_parity import assert_map_close
+    L = _lib.lib()
+    rng = np.random.default_rng(5)
+    n, G, ext = 20_000, (200, 160), (-1.5, 1.5, -1.5, 1.5)
+    pos = rng.normal(0, 0.4, (n, 3))
+    h = rng.uniform(0.01, 0.1, n)
+    m = rng.uniform(0.5, 2.0, n)
+    rho = np.exp(rng.uniform(-3, 3, n))
+    A = rng.uniform(1.0, 10.0, n)
+    d = lambda a: a.ctypes.data_as(_lib._d)  # noqa: E731
+    for dens in (rho, None):
+        img = np.zeros(G, np.float32)
+        props = (_lib._d * 1)(d(A))
+        outs = (_lib._f * 1)(img.ctypes.data_as(_lib._f))
+        rc = L.asp_project2d_sph_f64(d(pos), d(h), d(m), d(dens) if dens is not None else None,
+                                     props, 1, n, 2, *ext, G[0], G[1], 32, 0, 0, outs, 0, None)
+        _lib.check(rc)
+        w = m / dens if dens is not None else m
+        want, _ = oracle.project_scatter(pos[:, 0], pos[:, 1], h, A * w, None, G, 32, *ext,
+                                         kernel="cubic")
+        assert_map_close(img, want)
