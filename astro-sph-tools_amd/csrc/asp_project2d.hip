@@ -209,10 +209,26 @@ __global__ __launch_bounds__(kCountBlock) void k_count(const float* __restrict__
 
 // Record stores of the scatter: plain stores (non-temporal ones measured 2x slower, the
 // L2 merges the 32-B halves of a line).
+// ASP_SCATTER_ABLATE (experiment builds only, never the default): 1 -- the record stores
+// become a store under a condition no record meets (the records are still formed), 2 -- as
+// 1 and the cursor claims become a plain index (no LDS atomics).  The deposit kernels then
+// return at once (the record buffer holds no records).  DESIGN.md §4, round 6.
+#ifndef ASP_SCATTER_ABLATE
+#define ASP_SCATTER_ABLATE 0
+#endif
+// batches of particle loads the scatter keeps in flight ahead of the one it bins (1, or 2
+// as an A/B build switch)
+#ifndef ASP_SCATTER_PREFETCH
+#define ASP_SCATTER_PREFETCH 1
+#endif
 __device__ __forceinline__ void rec_store(float4* dst, float4 v) {
     // one global_store_dwordx4 per half record: the empty asm keeps the vectorizer from
     // regrouping two halves as dwordx3 + unaligned dwordx4 + dword
+#if ASP_SCATTER_ABLATE
+    if (v.x == 1.25e-37f && v.y == -1.25e-37f) *dst = v;
+#else
     *dst = v;
+#endif
     asm volatile("" ::: "memory");
 }
 
@@ -356,15 +372,28 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
         }
     };
     long long bq = 0, br = 0;
+    auto step_batch = [&]() {
+        const bool wrap = br + 1 == gcnt;
+        bq += wrap ? 1 : 0;
+        br = wrap ? 0 : br + 1;
+        return base_of(bq, br);
+    };
     long long c = base_of(0, 0);  // the current batch's first particle
     load_all(c, pu, pv, ph, pa0, pa1);
     load_src(c, pU, pV);
     load_x(c, px);
+#if ASP_SCATTER_PREFETCH >= 2
+    // A/B build switch: the batch after next in flight as well
+    long long cmid = step_batch();
+    float mu[kLane], mv[kLane], mh[kLane], ma0[kLane], ma1[kLane];
+    load_all(cmid, mu, mv, mh, ma0, ma1);
+    double mU[kLane], mV[kLane];
+    load_src(cmid, mU, mV);
+    float mx_[NX ? 4 : 1][kLane];
+    load_x(cmid, mx_);
+#endif
     while (c < n) {
-        const bool wrap = br + 1 == gcnt;
-        bq += wrap ? 1 : 0;
-        br = wrap ? 0 : br + 1;
-        const long long cn = base_of(bq, br);  // the next batch's
+        const long long cn = step_batch();  // the next batch to load
         float nu[kLane], nv[kLane], nh[kLane], na0[kLane], na1[kLane];
         load_all(cn, nu, nv, nh, na0, na1);
         double nU[kLane], nV[kLane];
@@ -417,7 +446,11 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
                 const int t = tx * g.nty + ty;
                 const unsigned bp = tile_box(b, tx, ty);
                 const int col = mb && box_large(bp, g) ? t + g.ntiles : t;
+#if ASP_SCATTER_ABLATE >= 2
+                int slot = col;
+#else
                 int slot = atomicAdd(&cur[col], 1);
+#endif
                 if constexpr (NX) rec_store(&xa.ext[slot], cx);
                 if constexpr (ACC == kAccFix) {
                     atomicMax(&cm[t * NOUT], c0);
@@ -471,6 +504,25 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
             __builtin_amdgcn_wave_barrier();
             first_slot[k] = -1;
         }
+#if ASP_SCATTER_PREFETCH >= 2
+#pragma unroll
+        for (int k = 0; k < kLane; ++k) {
+            pu[k] = mu[k], mu[k] = nu[k];
+            pv[k] = mv[k], mv[k] = nv[k];
+            ph[k] = mh[k], mh[k] = nh[k];
+            pa0[k] = ma0[k], ma0[k] = na0[k];
+            pa1[k] = ma1[k], ma1[k] = na1[k];
+            pU[k] = mU[k], mU[k] = nU[k];
+            pV[k] = mV[k], mV[k] = nV[k];
+        }
+        if constexpr (NX)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int k = 0; k < kLane; ++k) px[j][k] = mx_[j][k], mx_[j][k] = nx_[j][k];
+        c = cmid;
+        cmid = cn;
+#else
 #pragma unroll
         for (int k = 0; k < kLane; ++k) {
             pu[k] = nu[k];
@@ -487,6 +539,7 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(
 #pragma unroll
                 for (int k = 0; k < kLane; ++k) px[j][k] = nx_[j][k];
         c = cn;
+#endif
     }
     __syncthreads();
     if constexpr (ACC == kAccFix) {
@@ -1250,6 +1303,9 @@ __global__ __launch_bounds__(kDepBlock) __attribute__((amdgpu_waves_per_eu(4))) 
     float* xt = (float*)(acc + NOUT * kTileWords);
     float* yt = xt + kTile;
     __shared__ int defer_lds[kDepBlock / 64][kDeferCap];
+#if ASP_SCATTER_ABLATE
+    return;
+#endif
     const Item it = items[order[blockIdx.x]];  // largest items first (k_tilescan)
     if (it.mode != 0) return;  // the large stream's (K4g)
     int tx = it.tile / g.nty, ty = it.tile - (it.tile / g.nty) * g.nty;
@@ -1379,6 +1435,9 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(
     unsigned long long* __restrict__ slabs, float* __restrict__ out0, float* __restrict__ out1,
     int flags, const float4* __restrict__ ext, int pass) {
     extern __shared__ __attribute__((aligned(16))) double tot[];
+#if ASP_SCATTER_ABLATE
+    return;
+#endif
     const Item it = items[order[blockIdx.x / kGatherRegions]];  // largest first
     if (it.mode != 1) return;
     const int tx = it.tile / g.nty, ty = it.tile - (it.tile / g.nty) * g.nty;
@@ -1426,6 +1485,9 @@ __global__ __launch_bounds__(kBlock) void k_merge(Grid g, const Merge* __restric
                                                   const int2* __restrict__ tile_k,
                                                   float* __restrict__ out0,
                                                   float* __restrict__ out1, int flags) {
+#if ASP_SCATTER_ABLATE
+    return;
+#endif
     const Merge m = merges[blockIdx.x];
     int tx = m.tile / g.nty, ty = m.tile - (m.tile / g.nty) * g.nty;
     int X0 = tx * kTile, Y0 = ty * kTile;
