@@ -8,7 +8,17 @@
 #                                                     one line per VAR=Vi -> NAME_Vi.json
 #   bash tools/gpu/run.sh reps N NAME [bench args]    N fresh processes -> NAME_i.json
 #   bash tools/gpu/run.sh prof TAG [prof_driver args] kernel trace + PMC passes (prof_full.sh)
-# (round 4's one-off scripts tools/gpu/r04/*.sh are all instances of these modes)
+#   bash tools/gpu/run.sh ab NAME "LIBS" REPS [bench args]
+#                                                     same-box A/B: REPS rounds, each running one
+#                                                     line per build in LIBS ("work" = the working
+#                                                     library, X = astro-sph-tools_amd/ab_X/, from
+#                                                     tools/ab_build.sh) -> NAME_<lib>_<rep>.json
+#   bash tools/gpu/run.sh trace NAME [bench args]     rocprofv3 kernel trace of one bench line ->
+#                                                     NAME/, per-stream and timeline summaries
+#   bash tools/gpu/run.sh cube_ab NAME 'ENV=A' ...    tools/cube_ab.py: same-process cube A/B of
+#                                                     environment settings -> NAME.log
+# Every per-round script of rounds 3-6 was an instance of these modes; tools/gpu/README.md
+# lists the command line of each measurement kept under profiles/.
 cd "$GRAFT_REPO_ROOT" || exit 9
 export TMPDIR=/tmp
 o=gpurun_out/${OUT:-r06}; mkdir -p $o
@@ -43,5 +53,25 @@ case $mode in
     for i in $(seq 1 $n); do line ${name}_$i "$@" || exit 3; done ;;
   prof)
     bash tools/gpu/prof_full.sh "$@" || exit 4 ;;
+  ab)
+    name=$1; libs=$2; reps=$3; shift 3
+    for r in $(seq 1 $reps); do
+      for l in $libs; do
+        if [ "$l" = work ]; then lib=astro-sph-tools_amd/lib/libasp_hip.so; else lib=astro-sph-tools_amd/ab_$l/libasp_hip.so; fi
+        ASP_LIB=$lib line ${name}_${l}_$r "$@" || exit 5
+      done
+    done ;;
+  trace)
+    name=$1; shift
+    echo "== $(date +%T) trace $name: $*"
+    timeout -k 10 ${LIMIT:-300} rocprofv3 --kernel-trace --output-format csv -d $o/$name -o kt -- python3 bench.py "$@" > $o/$name.json 2> $o/$name.err || { tail -5 $o/$name.err; exit 6; }
+    python3 tools/stream_phase.py $o/$name/kt_kernel_trace.csv > $o/${name}_streams.txt
+    python3 tools/timeline.py $o/$name/kt_kernel_trace.csv > $o/${name}_timeline.txt
+    tail -1 $o/${name}_timeline.txt ;;
+  cube_ab)
+    name=$1; shift
+    echo "== $(date +%T) cube_ab $name: $*"
+    timeout -k 10 ${LIMIT:-400} python tools/cube_ab.py "$@" > $o/$name.log 2>&1 || { tail -20 $o/$name.log; exit 7; }
+    grep "rep 1" $o/$name.log ;;
   *) echo "unknown mode $mode"; exit 8 ;;
 esac
