@@ -80,9 +80,10 @@ def main():
         stage = {}
         for k, row in out.items():
             s = STAGE_OF.get(k.split("<")[0])
-            # the placement trials' probe instantiation (k_scatter<..., 1>, last template
-            # argument PROBE = 1) is not the steady state: never the stage's record
-            if k.startswith("k_scatter<") and k.rstrip(">").split(",")[-1].strip() == "1":
+            # the placement trials' probe instantiation (k_scatter<KID, NOUT, ACC, CULL, SRC,
+            # PROBE, NX>, PROBE = 1) is not the steady state: never the stage's record
+            targs = [x.strip() for x in k[k.find("<") + 1:].rstrip(">").split(",")]
+            if k.startswith("k_scatter<") and len(targs) >= 6 and targs[5] == "1":
                 continue
             # the first (largest total time) kernel of a stage
             if s and s not in stage and "hbm_bytes_per_launch" in row:
