@@ -460,6 +460,7 @@ constexpr int kBufSlots = 8;
 constexpr int kWinHalf = 64;   // W: curve window each side of the wave (swept: 64-512; 64 since the sub-tables)
 constexpr int kCellFine = 1;   // verification cells >= half the ball radius (swept: 0-3)
 constexpr int kWindowF32 = 1;  // the window pass with the fp32 prefilter (wave_scan32)
+constexpr int kUnionQ = 0;     // the shared cell pass's lane quantile (of 64; 0: off)
 
 template <int K>
 struct Cand {
@@ -548,37 +549,48 @@ __device__ __forceinline__ double wave_max(double v) {
 // per entry for every lane whenever any lane has a candidate.  The buffer is flushed
 // before the chunk's LDS is rewritten.  Results are the fp64 path's exactly (mx only
 // shrinks, so a bound from an earlier mx stays valid).
-template <int K>
-__device__ __forceinline__ void wave_scan32(long long a, long long b, const double* __restrict__ xs,
-                                            const double* __restrict__ ys,
-                                            const double* __restrict__ zs, double* lx, double* ly,
-                                            double* lz, float* fx, float* fy, float* fz, int lane,
-                                            double x, double y, double z, TopK<K>& T) {
+// The stream is entries f = 0 .. nent - 1 of the sorted arrays, entry f at sorted index
+// at(f) (-1: skip it -- its fp32 copy is NaN, which no bound passes); lanes with part false
+// take no candidates (their bound is -1).
+template <int K, class At>
+__device__ __forceinline__ void wave_stream32(long long nent, At at, const double* __restrict__ xs,
+                                              const double* __restrict__ ys,
+                                              const double* __restrict__ zs, double* lx, double* ly,
+                                              double* lz, float* fx, float* fy, float* fz, int lane,
+                                              double x, double y, double z, bool part, TopK<K>& T) {
     const double ox = __shfl(x, 0, 64), oy = __shfl(y, 0, 64), oz = __shfl(z, 0, 64);
     const double rx = x - ox, ry = y - oy, rz = z - oz;
     const float qx = (float)rx, qy = (float)ry, qz = (float)rz;
     const double mq = wave_max(fmax(fabs(rx), fmax(fabs(ry), fabs(rz))));
     int ib[kBufSlots];
     int cnt = 0;
-    for (long long c = a; c < b; c += 64) {
-        const int m = (int)min(64LL, b - c);
+    for (long long c = 0; c < nent; c += 64) {
+        const int m = (int)min(64LL, nent - c);
         double me = 0.0;
         if (lane < m) {
-            const double ex = xs[c + lane], ey = ys[c + lane], ez = zs[c + lane];
-            lx[lane] = ex;
-            ly[lane] = ey;
-            lz[lane] = ez;
-            const double dx = ex - ox, dy = ey - oy, dz = ez - oz;
-            fx[lane] = (float)dx;
-            fy[lane] = (float)dy;
-            fz[lane] = (float)dz;
-            me = fmax(fabs(dx), fmax(fabs(dy), fabs(dz)));
+            const long long g = at(c + lane);
+            if (g >= 0) {
+                const double ex = xs[g], ey = ys[g], ez = zs[g];
+                lx[lane] = ex;
+                ly[lane] = ey;
+                lz[lane] = ez;
+                const double dx = ex - ox, dy = ey - oy, dz = ez - oz;
+                fx[lane] = (float)dx;
+                fy[lane] = (float)dy;
+                fz[lane] = (float)dz;
+                me = fmax(fabs(dx), fmax(fabs(dy), fabs(dz)));
+            } else {
+                fx[lane] = __builtin_nanf("");
+                fy[lane] = 0.0f;
+                fz[lane] = 0.0f;
+            }
         }
         const double M = fmax(mq, wave_max(me));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         auto bound = [&]() -> float {
+            if (!part) return -1.0f;
             if (!(T.mx < INFINITY)) return INFINITY;
             const double r = sqrt(T.mx) * (1.0 + 0x1p-22) + 0x1p-21 * M;
             return (float)(r * r * (1.0 + 0x1p-21)) * (1.0f + 0x1p-22f);
@@ -609,6 +621,52 @@ __device__ __forceinline__ void wave_scan32(long long a, long long b, const doub
     }
 }
 
+template <int K>
+__device__ __forceinline__ void wave_scan32(long long a, long long b, const double* __restrict__ xs,
+                                            const double* __restrict__ ys,
+                                            const double* __restrict__ zs, double* lx, double* ly,
+                                            double* lz, float* fx, float* fy, float* fz, int lane,
+                                            double x, double y, double z, TopK<K>& T) {
+    wave_stream32<K>(b - a, [&](long long f) { return a + f; }, xs, ys, zs, lx, ly, lz, fx, fy, fz,
+                     lane, x, y, z, true, T);
+}
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+
+// The shared cell pass (round 6).  Each lane's cell pass below looks up and scans its own
+// cells, one dependent load chain after another, while the other lanes of the wave, whose
+// balls overlap its own, look up the same cells.  Here the wave takes the cells ONCE:
+//   * a common level: the finest level whose edge is >= half the ball radius for uq / 64 of
+//     the lanes (the others keep their own pass: one loose radius must not coarsen the
+//     cells for all);
+//   * the cells of that level meeting any such lane's ball (the per-lane test, ballot) and
+//     not inside the window's key span, listed in LDS;
+//   * their index ranges looked up by the lanes in parallel (64 lookups in flight), prefix
+//     offsets formed by a wave scan;
+//   * the concatenated ranges streamed once through LDS with the window pass's fp32
+//     prefilter (indices inside the window skipped: they are in already).
+// Exact for the same reason as the per-lane pass: any level's cells meeting a ball cover it.
+constexpr int kUCells = 512;      // cells listed per wave (LDS); more: the per-lane pass
+constexpr int kUScan = 4096;      // cells of the common box tested per wave at most
+constexpr int kUMaxEnt = 1 << 16; // entries streamed per wave at most
+
 #ifndef ASP_KNN_WPE
 #define ASP_KNN_WPE 0  // waves per SIMD the search is compiled for (0: the compiler's choice)
 #endif
@@ -626,9 +684,10 @@ __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double
                                                         int k, const KGrid* __restrict__ g,
                                                         double* __restrict__ h, int diag,
                                                         int whalf, int fine, CellTab CT,
-                                                        int f32, unsigned long long* evc) {
+                                                        int f32, int uq, unsigned long long* evc) {
     __shared__ double sx[kKnnBlock / 64][64], sy[kKnnBlock / 64][64], sz[kKnnBlock / 64][64];
     __shared__ float fx[kKnnBlock / 64][64], fy[kKnnBlock / 64][64], fz[kKnnBlock / 64][64];
+    __shared__ unsigned long long ucl[kKnnBlock / 64][kUCells];  // shared pass: cell keys, then (offset, start)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long long base = ((long long)blockIdx.x * (kKnnBlock / 64) + wv) * 64;
     if (base >= n) return;  // wave-uniform
@@ -648,10 +707,111 @@ __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double
         wave_scan<K>(win0, win1, xs, ys, zs, sx[wv], sy[wv], sz[wv], lane, x, y, z, C);
         C.flush();
     }
-    if (act && n >= k && diag == 0) {
-        // key span the window covers completely (open at the ends of the array)
-        const unsigned long long klo = win0 == 0 ? 0ULL : keys[win0] + 1;
-        const unsigned long long khi = win1 == n ? ~0ULL : keys[win1 - 1];
+    // key span the window covers completely (open at the ends of the array)
+    const unsigned long long klo = win0 == 0 ? 0ULL : keys[win0] + 1;
+    const unsigned long long khi = win1 == n ? ~0ULL : keys[win1 - 1];
+    bool shared = false;  // this lane's ball is covered by the shared cell pass
+    if (uq > 0 && f32 && n >= k && diag == 0) {  // wave-uniform
+        const bool ok = act && C.T.mx < INFINITY;
+        const double R = sqrt(C.T.mx) * (1.0 + 0x1p-40);
+        int sft = 99;  // this lane's own cell level (as the per-lane pass)
+        if (ok) {
+            int e;
+            frexp(R * G.scale + 1.0, &e);
+            sft = max(0, min(e, kQBits) - fine);
+        }
+        const int nact = __popcll(__ballot(ok));
+        if (nact > 0) {
+            const int need = (nact * uq + 63) >> 6;
+            int sw = wave_min_i(sft);
+            while (__popcll(__ballot(ok && sft <= sw)) < need) ++sw;
+            const bool rg = ok && sft <= sw;
+            const double c3[3] = {x, y, z};
+            int A[3], B[3];
+            long long ncell = 1;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const int lo = (int)(max(0LL, quant(c3[a] - R, G.lo[a], G.scale) - 1) >> sw);
+                const int hi = (int)(min(kQMax, quant(c3[a] + R, G.lo[a], G.scale) + 1) >> sw);
+                A[a] = wave_min_i(rg ? lo : INT_MAX);
+                B[a] = wave_max_i(rg ? hi : -1);
+                ncell *= B[a] - A[a] + 1;
+            }
+            const int sh3 = 3 * sw;
+            auto gap = [&](int a, int cc) {  // distance from this lane's particle to the slab of cell cc
+                const double clo = G.lo[a] + (double)((long long)cc << sw) * G.quantum - G.quantum;
+                const double chi = G.lo[a] + (double)((long long)(cc + 1) << sw) * G.quantum + G.quantum;
+                return c3[a] < clo ? clo - c3[a] : (c3[a] > chi ? c3[a] - chi : 0.0);
+            };
+            int nc = 0;
+            bool ovf = ncell > kUScan;
+            for (int cx = A[0]; cx <= B[0] && !ovf; ++cx) {
+                const double d0 = gap(0, cx), s0 = d0 * d0;
+                for (int cy = A[1]; cy <= B[1] && !ovf; ++cy) {
+                    const double d1 = gap(1, cy), s1 = s0 + d1 * d1;
+                    for (int cz = A[2]; cz <= B[2]; ++cz) {
+                        const double d2 = gap(2, cz), md = s1 + d2 * d2;
+                        if (!__ballot(rg && !(md * (1.0 - 0x1p-40) > C.T.mx))) continue;
+                        const unsigned long long p = morton3(cx, cy, cz);
+                        const unsigned long long k0 = sh3 >= 63 ? 0ULL : p << sh3;
+                        const unsigned long long k1 = sh3 >= 63 ? ~0ULL : (p + 1) << sh3;
+                        if (k0 >= klo && k1 <= khi) continue;  // inside the window already
+                        if (nc == kUCells) {
+                            ovf = true;
+                            break;
+                        }
+                        if (lane == 0) ucl[wv][nc] = k0;
+                        ++nc;
+                    }
+                }
+            }
+            long long tot = 0;
+            if (!ovf && nc > 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (int c0 = 0; c0 < nc; c0 += 64) {  // lookups, 64 cells at a time
+                    const int c = c0 + lane;
+                    long long j0 = 0, len = 0;
+                    if (c < nc) {
+                        const unsigned long long k0 = ucl[wv][c];
+                        const unsigned long long k1 = sh3 >= 63 ? ~0ULL : k0 + (1ULL << sh3);
+                        j0 = cell_lower(keys, n, CT, k0);
+                        const long long j1 = sh3 >= 63 || (k1 >> 63) ? n : cell_lower(keys, n, CT, k1);
+                        len = j1 - j0;
+                    }
+                    const int l32 = (int)min(len, (long long)kUMaxEnt + 1);
+                    const long long incl = tot + wave_incl_scan(l32, lane);
+                    if (c < nc)
+                        ucl[wv][c] = ((unsigned long long)min(incl - l32, (long long)kUMaxEnt + 1) << 32) |
+                                     (unsigned long long)(unsigned)j0;
+                    tot = __shfl(incl, 63, 64);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            if (!ovf && tot <= kUMaxEnt) {
+                const unsigned long long* L = ucl[wv];
+                auto at = [&](long long f) -> long long {  // the last cell starting at or before f
+                    int lo = 0, hi = nc - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if ((long long)(L[mid] >> 32) <= f) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    const unsigned long long e = L[lo];
+                    const long long g = (long long)(unsigned)(e & 0xffffffffULL) + (f - (long long)(e >> 32));
+                    return g >= win0 && g < win1 ? -1 : g;
+                };
+                wave_stream32<K>(tot, at, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv], fy[wv], fz[wv],
+                                 lane, x, y, z, rg, C.T);
+                shared = rg;
+                if (evc && lane == 0) atomicAdd(&evc[2], (unsigned long long)tot);
+            }
+        }
+    }
+    if (act && !shared && n >= k && diag == 0) {
         const double R = sqrt(C.T.mx) * (1.0 + 0x1p-40);
         int e;
         frexp(R * G.scale + 1.0, &e);  // cell edge 2^shift >= R + 1 quantum ...
@@ -807,13 +967,16 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     const int whalf = getenv("ASP_KNN_WINDOW") ? atoi(getenv("ASP_KNN_WINDOW")) : kWinHalf;
     const int fine = getenv("ASP_KNN_FINE") ? atoi(getenv("ASP_KNN_FINE")) : kCellFine;
     const int f32 = getenv("ASP_KNN_F32") ? atoi(getenv("ASP_KNN_F32")) : kWindowF32;
+    // the shared cell pass: the common level covers uq / 64 of a wave's lanes (0: off)
+    const int uq = getenv("ASP_KNN_UNION") ? std::min(64, std::max(0, atoi(getenv("ASP_KNN_UNION")))) : kUnionQ;
     // ASP_KNN_COUNT: count the distances the search evaluates (bench.py's k-NN roofline;
-    // one atomic per lane, so off in timed runs) -> asp_last_stats [9] window, [10] cells
+    // one atomic per lane, so off in timed runs) -> asp_last_stats [9] window, [10] cells,
+    // [11] entries the shared cell pass streamed (once per wave)
     unsigned long long* evc = nullptr;
     if (getenv("ASP_KNN_COUNT")) {
-        ASP_TRY(ensure(ws.knn[11], 2 * sizeof(unsigned long long)));
+        ASP_TRY(ensure(ws.knn[11], 3 * sizeof(unsigned long long)));
         evc = (unsigned long long*)ws.knn[11].p;
-        ASP_HIP(hipMemsetAsync(evc, 0, 2 * sizeof(unsigned long long), st));
+        ASP_HIP(hipMemsetAsync(evc, 0, 3 * sizeof(unsigned long long), st));
     }
     StageMark msearch(ws, kSKnnSearch, st);
 #define ASP_KNN(KN)                                                                               \
@@ -828,7 +991,7 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
                                dim3(kKnnBlock), 0, st, (const double*)xs, (const double*)ys,      \
                                (const double*)zs, (const unsigned long long*)kout,                \
                                (const int*)iout, (long long)n, k, (const KGrid*)dg, dh, diag, whalf,  \
-                               fine, CT, f32, evc);\
+                               fine, CT, f32, uq, evc);\
     } while (0)
     if (k <= 32)
         ASP_KNN(32);
@@ -839,11 +1002,12 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     msearch.done();
     for (int j = 9; j <= 12; ++j) ws.stats[j] = 0;
     if (evc) {
-        unsigned long long e[2];
+        unsigned long long e[3];
         ASP_HIP(hipMemcpyAsync(e, evc, sizeof(e), hipMemcpyDeviceToHost, st));
         ASP_HIP(hipStreamSynchronize(st));
         ws.stats[9] = (long long)e[0];
         ws.stats[10] = (long long)e[1];
+        ws.stats[11] = (long long)e[2];
     }
     if (!dev) {
         ASP_HIP(hipMemcpyAsync(h, dh, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st));

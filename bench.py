@@ -451,7 +451,8 @@ def run_knn(args, dev):
 
     Roofline (VALU): the search kernel evaluates squared distances -- fp32 ones in the
     curve-window pass (the prefilter; exact fp64 only for the few candidates) and fp64
-    ones in the cell scans -- counted in one untimed diagnostic call (ASP_KNN_COUNT), 8
+    ones in the cell scans, fp32 ones (every lane of a wave) in the shared cell pass --
+    counted in one untimed diagnostic call (ASP_KNN_COUNT), 8
     flops each; the time that work needs at the FP32 / FP64 vector peaks, over the search
     kernel's HIP-event time in the timed steps, is the fraction."""
     import numpy as np
@@ -486,7 +487,10 @@ def run_knn(args, dev):
     finally:
         del os.environ["ASP_KNN_COUNT"]
     same = bool(torch.equal(h, h2))
-    e32, e64 = float(st["evals"]), float(st["evals_small"])  # window (fp32), cell scans (fp64)
+    # window (fp32), cell scans (fp64), the shared cell pass's entries (fp32, every lane)
+    e32, e64 = float(st["evals"]), float(st["evals_small"])
+    eshared = float(st["evals_gather"]) * 64
+    e32 += eshared
     s_ms = prof["knn_search"][0] / max(1, prof["knn_search"][1]) if "knn_search" in prof else None
     roof = None
     if s_ms:
@@ -498,6 +502,7 @@ def run_knn(args, dev):
                 "peak": round(flops / t_peak / 1e12, 3), "unit": "TFLOP/s",
                 "frac": round(t_peak / (s_ms * 1e-3), 4),
                 "distances_fp32": int(e32), "distances_fp64": int(e64),
+                "distances_shared_pass": int(eshared),
                 "distances_per_particle": round((e32 + e64) / args.n, 1),
                 "flops_per_distance": DIST_FLOPS,
                 "kernel_ms_per_step": round(s_ms, 4),

@@ -112,3 +112,27 @@ def test_knn_fp32_window_prefilter_far_coordinates(gpu, monkeypatch):
     h64 = knn_smoothing_lengths(pos, 32)
     assert np.array_equal(bits(h32), bits(want))
     assert np.array_equal(bits(h64), bits(want))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("uq", ["32", "56", "64"])
+def test_knn_shared_cell_pass(gpu, monkeypatch, uq):
+    """The shared cell pass (asp_knn.hip, ASP_KNN_UNION = the lane quantile of the common
+    cell level): bit-exact against scipy on every input kind, the far-coordinate clusters
+    and 2e6 Plummer particles; the lanes it leaves out (looser radii) keep their own pass."""
+    from asp_amd.knn import knn_smoothing_lengths
+    monkeypatch.setenv("ASP_KNN_UNION", uq)
+    rng = np.random.default_rng(11)
+    g = np.arange(30.0) * 0.5
+    sets = [rng.uniform(0.0, 25.0, (60_000, 3)), _plummer(200_000, 5),
+            np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3),
+            np.concatenate([rng.uniform(0.0, 1.0, (2000, 3))] * 10 + [rng.uniform(0.0, 1.0, (4000, 3))]),
+            np.concatenate([rng.uniform(0, 1, (30_000, 2)), np.full((30_000, 1), 3.0)], axis=1),
+            np.concatenate([rng.uniform(0.0, 1.0, (20_000, 3)) + np.array([1e6, -2e6, 5e5]),
+                            rng.uniform(-1e9, 1e9, (50, 3))])]
+    for pos in sets:
+        for k in (32, 7):
+            assert np.array_equal(bits(knn_smoothing_lengths(pos, k)), bits(scipy_h(pos, k))), (len(pos), k)
+    pos = _plummer(2_000_000, 6)
+    want = KDTree(pos).query(pos, k=32, workers=-1)[0][:, 31]
+    assert np.array_equal(bits(knn_smoothing_lengths(pos, 32)), bits(want))

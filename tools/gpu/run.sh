@@ -64,7 +64,7 @@ case $mode in
   trace)
     name=$1; shift
     echo "== $(date +%T) trace $name: $*"
-    timeout -k 10 ${LIMIT:-300} rocprofv3 --kernel-trace --output-format csv -d $o/$name -o kt -- python3 bench.py "$@" > $o/$name.json 2> $o/$name.err || { tail -5 $o/$name.err; exit 6; }
+    timeout -k 10 ${LIMIT:-300} rocprofv3 --kernel-trace --stats --output-format csv -d $o/$name -o kt -- python3 bench.py "$@" > $o/$name.json 2> $o/$name.err || { tail -5 $o/$name.err; exit 6; }
     python3 tools/stream_phase.py $o/$name/kt_kernel_trace.csv > $o/${name}_streams.txt
     python3 tools/timeline.py $o/$name/kt_kernel_trace.csv > $o/${name}_timeline.txt
     tail -1 $o/${name}_timeline.txt ;;
