@@ -159,20 +159,38 @@ __global__ __launch_bounds__(kKnnBlock) void k_gather(const double* __restrict__
 // v[K - 1].  Inserting d (< v[K - 1]) is a branch-free merge step:
 //   v'[q] = min(v[q], max(v[q - 1], d)),  v[-1] = -inf
 // = the q-th smallest of v and d (v[q] if d > v[q], else max(v[q - 1], d)): 2K min / max.
+// v_min_f64 / v_max_f64 as plain instructions.  fmin / fmax lower to the same instructions
+// plus a v_max_f64 x, x quieting each loop-carried operand (IEEE mode: a signalling NaN
+// must not pass through), a third instruction per slot of the insertion.  The top-k never
+// holds a NaN (insert() admits only d < mx), so the quieting is dead weight.
+__device__ __forceinline__ double hw_min(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double hw_max(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 template <int K>
 struct TopK {
     double v[K];
     double mx;  // the k-th smallest so far (+inf until k values are in)
+    int nins;   // insertions (diagnostic counter, ASP_KNN_COUNT)
     __device__ __forceinline__ void init(int k) {
 #pragma unroll
         for (int q = 0; q < K; ++q) v[q] = q < K - k ? -INFINITY : INFINITY;
         mx = INFINITY;
+        nins = 0;
     }
     __device__ __forceinline__ void insert(double d) {
         if (!(d < mx)) return;
+        ++nins;
 #pragma unroll
-        for (int q = K - 1; q > 0; --q) v[q] = fmin(v[q], fmax(v[q - 1], d));
-        v[0] = fmin(v[0], d);
+        for (int q = K - 1; q > 0; --q) v[q] = hw_min(v[q], hw_max(v[q - 1], d));
+        v[0] = hw_min(v[0], d);
         mx = v[K - 1];
     }
 };
@@ -460,7 +478,9 @@ constexpr int kBufSlots = 8;
 constexpr int kWinHalf = 64;   // W: curve window each side of the wave (swept: 64-512; 64 since the sub-tables)
 constexpr int kCellFine = 1;   // verification cells >= half the ball radius (swept: 0-3)
 constexpr int kWindowF32 = 1;  // the window pass with the fp32 prefilter (wave_scan32)
-constexpr int kUnionQ = 0;     // the shared cell pass's lane quantile (of 64; 0: off)
+constexpr bool kMaskTest = false;  // the entry test's form (wave_stream32 MASK)
+constexpr int kUnionQ = 0;
+constexpr int kNearFirst = 0;  // window chunks nearest first (wave_scan32_near)     // the shared cell pass's lane quantile (of 64; 0: off)
 
 template <int K>
 struct Cand {
@@ -552,38 +572,48 @@ __device__ __forceinline__ double wave_max(double v) {
 // The stream is entries f = 0 .. nent - 1 of the sorted arrays, entry f at sorted index
 // at(f) (-1: skip it -- its fp32 copy is NaN, which no bound passes); lanes with part false
 // take no candidates (their bound is -1).
-template <int K, class At>
+template <int K, bool MASK, class At>
 __device__ __forceinline__ void wave_stream32(long long nent, At at, const double* __restrict__ xs,
                                               const double* __restrict__ ys,
                                               const double* __restrict__ zs, double* lx, double* ly,
                                               double* lz, float* fx, float* fy, float* fz, int lane,
-                                              double x, double y, double z, bool part, TopK<K>& T) {
+                                              double x, double y, double z, bool part, int grp,
+                                              TopK<K>& T) {
     const double ox = __shfl(x, 0, 64), oy = __shfl(y, 0, 64), oz = __shfl(z, 0, 64);
     const double rx = x - ox, ry = y - oy, rz = z - oz;
     const float qx = (float)rx, qy = (float)ry, qz = (float)rz;
     const double mq = wave_max(fmax(fabs(rx), fmax(fabs(ry), fabs(rz))));
-    int ib[kBufSlots];
-    int cnt = 0;
+    // chunk c + 64's entries are loaded (clamped index, unconditional loads) before chunk c
+    // is tested, so the gathers' latency overlaps the tests
+    auto entry = [&](long long c, long long& g, double& ex, double& ey, double& ez) {
+        g = c + lane < nent ? at(c + lane) : -1;
+        const long long gi = g >= 0 ? g : 0;
+        ex = xs[gi];
+        ey = ys[gi];
+        ez = zs[gi];
+    };
+    long long gn;
+    double exn, eyn, ezn;
+    entry(0, gn, exn, eyn, ezn);
     for (long long c = 0; c < nent; c += 64) {
         const int m = (int)min(64LL, nent - c);
         double me = 0.0;
-        if (lane < m) {
-            const long long g = at(c + lane);
-            if (g >= 0) {
-                const double ex = xs[g], ey = ys[g], ez = zs[g];
-                lx[lane] = ex;
-                ly[lane] = ey;
-                lz[lane] = ez;
-                const double dx = ex - ox, dy = ey - oy, dz = ez - oz;
-                fx[lane] = (float)dx;
-                fy[lane] = (float)dy;
-                fz[lane] = (float)dz;
-                me = fmax(fabs(dx), fmax(fabs(dy), fabs(dz)));
-            } else {
-                fx[lane] = __builtin_nanf("");
-                fy[lane] = 0.0f;
-                fz[lane] = 0.0f;
-            }
+        const long long g = gn;
+        const double ex = exn, ey = eyn, ez = ezn;
+        if (c + 64 < nent) entry(c + 64, gn, exn, eyn, ezn);
+        if (g >= 0) {
+            lx[lane] = ex;
+            ly[lane] = ey;
+            lz[lane] = ez;
+            const double dx = ex - ox, dy = ey - oy, dz = ez - oz;
+            fx[lane] = (float)dx;
+            fy[lane] = (float)dy;
+            fz[lane] = (float)dz;
+            me = fmax(fabs(dx), fmax(fabs(dy), fabs(dz)));
+        } else {  // no entry (past the chunk's end, or skipped): NaN passes no bound
+            fx[lane] = __builtin_nanf("");
+            fy[lane] = 0.0f;
+            fz[lane] = 0.0f;
         }
         const double M = fmax(mq, wave_max(me));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -595,13 +625,50 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
             const double r = sqrt(T.mx) * (1.0 + 0x1p-22) + 0x1p-21 * M;
             return (float)(r * r * (1.0 + 0x1p-21)) * (1.0f + 0x1p-22f);
         };
+        float tb = bound();
+        if constexpr (MASK) {
+            // grp entries at a time (16 / 32): their fp32 copies by 16-byte LDS reads
+            // (every slot of the chunk is written, NaN past its end), the passing ones as a
+            // bit mask, then each lane walks its own bits (exact fp64 distance, insert) --
+            // the wave pays one walk per group in which any lane has a candidate
+            const int me4 = (m + 3) & ~3;
+            for (int g0 = 0; g0 < me4; g0 += grp) {
+                unsigned pm = 0;
+                const int ge = min(g0 + grp, me4);
+#pragma unroll 1
+                for (int q0 = g0; q0 < ge; q0 += 4) {
+                    const float4 X = *(const float4*)(fx + q0);
+                    const float4 Y = *(const float4*)(fy + q0);
+                    const float4 Z = *(const float4*)(fz + q0);
+                    const float ax[4] = {X.x, X.y, X.z, X.w}, ay[4] = {Y.x, Y.y, Y.z, Y.w},
+                                az[4] = {Z.x, Z.y, Z.z, Z.w};
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        const float dx = qx - ax[v], dy = qy - ay[v], dz = qz - az[v];
+                        const float d32 = (dx * dx + dy * dy) + dz * dz;
+                        pm |= (d32 <= tb ? 1u : 0u) << (q0 - g0 + v);
+                    }
+                }
+                if (__builtin_amdgcn_ballot_w64(pm != 0)) {
+                    while (pm) {
+                        const int q = g0 + __builtin_ctz(pm);
+                        pm &= pm - 1;
+                        T.insert(dist2(x, y, z, lx[q], ly[q], lz[q]));
+                    }
+                    tb = bound();
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            continue;
+        }
+        int ib[kBufSlots];
+        int cnt = 0;
         auto flush = [&]() {
 #pragma unroll
             for (int q = 0; q < kBufSlots; ++q)
                 if (q < cnt) T.insert(dist2(x, y, z, lx[ib[q]], ly[ib[q]], lz[ib[q]]));
             cnt = 0;
         };
-        float tb = bound();
         for (int q = 0; q < m; ++q) {
             const float dx = qx - fx[q], dy = qy - fy[q], dz = qz - fz[q];
             const float d32 = (dx * dx + dy * dy) + dz * dz;
@@ -621,14 +688,37 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
     }
 }
 
-template <int K>
+template <int K, bool MASK>
 __device__ __forceinline__ void wave_scan32(long long a, long long b, const double* __restrict__ xs,
                                             const double* __restrict__ ys,
                                             const double* __restrict__ zs, double* lx, double* ly,
                                             double* lz, float* fx, float* fy, float* fz, int lane,
                                             double x, double y, double z, TopK<K>& T) {
-    wave_stream32<K>(b - a, [&](long long f) { return a + f; }, xs, ys, zs, lx, ly, lz, fx, fy, fz,
-                     lane, x, y, z, true, T);
+    wave_stream32<K, MASK>(b - a, [&](long long f) { return a + f; }, xs, ys, zs, lx, ly, lz, fx, fy, fz,
+                     lane, x, y, z, true, 16, T);
+}
+
+// The window [a, b) around the wave's own 64 particles [base, base + 64), streamed
+// nearest chunks first: the wave's own chunk, then the chunks 64 below and above it, then
+// 128 below and above, ...  In random order a lane's top-k takes about k (1 + ln(N / k))
+// insertions for N entries; curve neighbours first, its k-th distance falls early and
+// fewer of the later entries pass.
+template <int K, bool MASK>
+__device__ __forceinline__ void wave_scan32_near(long long a, long long b, long long base,
+                                                 const double* __restrict__ xs,
+                                                 const double* __restrict__ ys,
+                                                 const double* __restrict__ zs, double* lx,
+                                                 double* ly, double* lz, float* fx, float* fy,
+                                                 float* fz, int lane, double x, double y, double z,
+                                                 int grp, TopK<K>& T) {
+    const long long below = (base - a + 63) >> 6, above = (b - base - 1) >> 6;  // chunks each side
+    const long long nch = 1 + 2 * max(below, above);
+    wave_stream32<K, MASK>(nch * 64, [&](long long f) -> long long {
+        const long long j = f >> 6, o = f & 63;
+        const long long s = j == 0 ? 0 : (j & 1 ? -((j + 1) >> 1) : (j >> 1));  // 0, -1, +1, -2, +2, ...
+        const long long g = base + s * 64 + o;
+        return g >= a && g < b ? g : -1;
+    }, xs, ys, zs, lx, ly, lz, fx, fy, fz, lane, x, y, z, true, grp, T);
 }
 
 __device__ __forceinline__ int wave_min_i(int v) {
@@ -675,7 +765,7 @@ constexpr int kUMaxEnt = 1 << 16; // entries streamed per wave at most
 #else
 #define ASP_KNN_OCC
 #endif
-template <int K>
+template <int K, bool MASK>
 __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double* __restrict__ xs,
                                                         const double* __restrict__ ys,
                                                         const double* __restrict__ zs,
@@ -684,9 +774,11 @@ __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double
                                                         int k, const KGrid* __restrict__ g,
                                                         double* __restrict__ h, int diag,
                                                         int whalf, int fine, CellTab CT,
-                                                        int f32, int uq, unsigned long long* evc) {
+                                                        int f32, int uq, int near, int wgrp,
+                                                        int ugrp, unsigned long long* evc) {
     __shared__ double sx[kKnnBlock / 64][64], sy[kKnnBlock / 64][64], sz[kKnnBlock / 64][64];
-    __shared__ float fx[kKnnBlock / 64][64], fy[kKnnBlock / 64][64], fz[kKnnBlock / 64][64];
+    __shared__ __attribute__((aligned(16))) float fx[kKnnBlock / 64][64], fy[kKnnBlock / 64][64],
+        fz[kKnnBlock / 64][64];
     __shared__ unsigned long long ucl[kKnnBlock / 64][kUCells];  // shared pass: cell keys, then (offset, start)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long long base = ((long long)blockIdx.x * (kKnnBlock / 64) + wv) * 64;
@@ -701,8 +793,12 @@ __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double
     C.cnt = 0;
     const long long win0 = max(0LL, base - whalf), win1 = min(n, base + 64 + whalf);
     if (f32) {
-        wave_scan32<K>(win0, win1, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv], fy[wv], fz[wv], lane,
-                       x, y, z, C.T);
+        if (near)
+            wave_scan32_near<K, MASK>(win0, win1, base, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv],
+                                      fy[wv], fz[wv], lane, x, y, z, wgrp, C.T);
+        else
+            wave_scan32<K, MASK>(win0, win1, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv], fy[wv],
+                                 fz[wv], lane, x, y, z, C.T);
     } else {
         wave_scan<K>(win0, win1, xs, ys, zs, sx[wv], sy[wv], sz[wv], lane, x, y, z, C);
         C.flush();
@@ -711,7 +807,9 @@ __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double
     const unsigned long long klo = win0 == 0 ? 0ULL : keys[win0] + 1;
     const unsigned long long khi = win1 == n ? ~0ULL : keys[win1 - 1];
     bool shared = false;  // this lane's ball is covered by the shared cell pass
-    if (uq > 0 && f32 && n >= k && diag == 0) {  // wave-uniform
+    // diag (timing only, wrong results): 2 = the shared pass's cell list and lookups without
+    // its stream, 3 = the shared pass without the per-lane pass
+    if (uq > 0 && f32 && n >= k && (diag == 0 || diag >= 2)) {  // wave-uniform
         const bool ok = act && C.T.mx < INFINITY;
         const double R = sqrt(C.T.mx) * (1.0 + 0x1p-40);
         int sft = 99;  // this lane's own cell level (as the per-lane pass)
@@ -727,31 +825,46 @@ __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double
             while (__popcll(__ballot(ok && sft <= sw)) < need) ++sw;
             const bool rg = ok && sft <= sw;
             const double c3[3] = {x, y, z};
+            // the common box of cells (uniform: scalar loops), this lane's position and
+            // squared radius in quanta (the per-lane pass's slack: one quantum per cell face)
             int A[3], B[3];
-            long long ncell = 1;
+            double tq[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
                 const int lo = (int)(max(0LL, quant(c3[a] - R, G.lo[a], G.scale) - 1) >> sw);
                 const int hi = (int)(min(kQMax, quant(c3[a] + R, G.lo[a], G.scale) + 1) >> sw);
-                A[a] = wave_min_i(rg ? lo : INT_MAX);
-                B[a] = wave_max_i(rg ? hi : -1);
-                ncell *= B[a] - A[a] + 1;
+                A[a] = __builtin_amdgcn_readfirstlane(wave_min_i(rg ? lo : INT_MAX));
+                B[a] = __builtin_amdgcn_readfirstlane(wave_max_i(rg ? hi : -1));
+                tq[a] = (c3[a] - G.lo[a]) * G.scale;
             }
-            const int sh3 = 3 * sw;
-            auto gap = [&](int a, int cc) {  // distance from this lane's particle to the slab of cell cc
-                const double clo = G.lo[a] + (double)((long long)cc << sw) * G.quantum - G.quantum;
-                const double chi = G.lo[a] + (double)((long long)(cc + 1) << sw) * G.quantum + G.quantum;
-                return c3[a] < clo ? clo - c3[a] : (c3[a] > chi ? c3[a] - chi : 0.0);
+            const double r2q = rg ? C.T.mx * G.scale * G.scale * (1.0 + 0x1p-36) : -1.0;
+            const double ed = (double)(1 << sw);  // cell edge in quanta
+            // distance (quanta) from this lane's particle to the slab of cell cc on axis a,
+            // the cell widened by one quantum each side
+            auto gapq = [&](int a, int cc) {
+                const double l = (double)cc * ed - 1.0 - tq[a], h = tq[a] - ((double)cc + 1.0) * ed - 1.0;
+                return fmax(fmax(l, h), 0.0);
             };
+            const int sh3 = 3 * sw;
             int nc = 0;
-            bool ovf = ncell > kUScan;
+            bool ovf = (long long)(B[0] - A[0] + 1) * (B[1] - A[1] + 1) > kUScan;
             for (int cx = A[0]; cx <= B[0] && !ovf; ++cx) {
-                const double d0 = gap(0, cx), s0 = d0 * d0;
+                const double gx = gapq(0, cx), sx2 = gx * gx;
+                if (!__ballot(sx2 <= r2q)) continue;
                 for (int cy = A[1]; cy <= B[1] && !ovf; ++cy) {
-                    const double d1 = gap(1, cy), s1 = s0 + d1 * d1;
-                    for (int cz = A[2]; cz <= B[2]; ++cz) {
-                        const double d2 = gap(2, cz), md = s1 + d2 * d2;
-                        if (!__ballot(rg && !(md * (1.0 - 0x1p-40) > C.T.mx))) continue;
+                    const double gy = gapq(1, cy), s2 = sx2 + gy * gy;
+                    // this lane's cells of the column: gap_z^2 <= r2q - s2, i.e. cz in
+                    // [(t - 1 - w) / ed - 1, (t + 1 + w) / ed], w = sqrt(r2q - s2) (fp32,
+                    // widened by 2^-18 relative + 2 quanta)
+                    int z0 = INT_MAX, z1 = -1;
+                    if (s2 <= r2q) {
+                        const double w = (double)(__builtin_amdgcn_sqrtf((float)(r2q - s2)) * (1.0f + 0x1p-18f)) + 2.0;
+                        z0 = (int)floor((tq[2] - 1.0 - w) / ed) - 1;
+                        z1 = (int)floor((tq[2] + 1.0 + w) / ed);
+                    }
+                    const int cz0 = max(A[2], __builtin_amdgcn_readfirstlane(wave_min_i(z0)));
+                    const int cz1 = min(B[2], __builtin_amdgcn_readfirstlane(wave_max_i(z1)));
+                    for (int cz = cz0; cz <= cz1; ++cz) {
                         const unsigned long long p = morton3(cx, cy, cz);
                         const unsigned long long k0 = sh3 >= 63 ? 0ULL : p << sh3;
                         const unsigned long long k1 = sh3 >= 63 ? ~0ULL : (p + 1) << sh3;
@@ -791,7 +904,7 @@ __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
-            if (!ovf && tot <= kUMaxEnt) {
+            if (!ovf && tot <= kUMaxEnt && diag != 2) {
                 const unsigned long long* L = ucl[wv];
                 auto at = [&](long long f) -> long long {  // the last cell starting at or before f
                     int lo = 0, hi = nc - 1;
@@ -804,8 +917,8 @@ __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double
                     const long long g = (long long)(unsigned)(e & 0xffffffffULL) + (f - (long long)(e >> 32));
                     return g >= win0 && g < win1 ? -1 : g;
                 };
-                wave_stream32<K>(tot, at, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv], fy[wv], fz[wv],
-                                 lane, x, y, z, rg, C.T);
+                wave_stream32<K, MASK>(tot, at, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv], fy[wv], fz[wv],
+                                 lane, x, y, z, rg, ugrp, C.T);
                 shared = rg;
                 if (evc && lane == 0) atomicAdd(&evc[2], (unsigned long long)tot);
             }
@@ -853,10 +966,11 @@ __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double
                     scan_range<K>(max(j0, win1), j1, xs, ys, zs, x, y, z, C.T);
                     if (evc) nscan += max(0LL, min(j1, win0) - j0) + max(0LL, j1 - max(j0, win1));
                 }
-        if (evc) {  // diagnostic: distances evaluated (window pass, cell scans)
-            atomicAdd(&evc[0], (unsigned long long)(win1 - win0));
-            atomicAdd(&evc[1], (unsigned long long)nscan);
-        }
+        if (evc) atomicAdd(&evc[1], (unsigned long long)nscan);  // diagnostic: cell-scan distances
+    }
+    if (evc && act) {
+        atomicAdd(&evc[0], (unsigned long long)(win1 - win0));  // window distances
+        atomicAdd(&evc[3], (unsigned long long)C.T.nins);       // top-k insertions
     }
     if (act) h[idx[i]] = sqrt(C.T.mx);
 }
@@ -968,15 +1082,23 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     const int fine = getenv("ASP_KNN_FINE") ? atoi(getenv("ASP_KNN_FINE")) : kCellFine;
     const int f32 = getenv("ASP_KNN_F32") ? atoi(getenv("ASP_KNN_F32")) : kWindowF32;
     // the shared cell pass: the common level covers uq / 64 of a wave's lanes (0: off)
+    // the window / shared passes' entry test: 16 entries per step into a bit mask (1) or
+    // one entry per step into an 8-slot buffer (0)
+    const bool mask = getenv("ASP_KNN_MASK") ? atoi(getenv("ASP_KNN_MASK")) != 0 : kMaskTest;
+    // the window pass's chunk order: nearest to the wave's own first (1) or in array order (0)
+    const int near = getenv("ASP_KNN_NEAR") ? atoi(getenv("ASP_KNN_NEAR")) : kNearFirst;
+    // the mask test's group sizes (entries per candidate walk) in the window / shared passes
+    auto group = [](const char* v, int d) { const int g = v ? atoi(v) : d; return g == 32 ? 32 : 16; };
+    const int wgrp = group(getenv("ASP_KNN_WGROUP"), 16), ugrp = group(getenv("ASP_KNN_UGROUP"), 16);
     const int uq = getenv("ASP_KNN_UNION") ? std::min(64, std::max(0, atoi(getenv("ASP_KNN_UNION")))) : kUnionQ;
     // ASP_KNN_COUNT: count the distances the search evaluates (bench.py's k-NN roofline;
     // one atomic per lane, so off in timed runs) -> asp_last_stats [9] window, [10] cells,
-    // [11] entries the shared cell pass streamed (once per wave)
+    // [11] entries the shared cell pass streamed (once per wave), [12] top-k insertions
     unsigned long long* evc = nullptr;
     if (getenv("ASP_KNN_COUNT")) {
-        ASP_TRY(ensure(ws.knn[11], 3 * sizeof(unsigned long long)));
+        ASP_TRY(ensure(ws.knn[11], 4 * sizeof(unsigned long long)));
         evc = (unsigned long long*)ws.knn[11].p;
-        ASP_HIP(hipMemsetAsync(evc, 0, 3 * sizeof(unsigned long long), st));
+        ASP_HIP(hipMemsetAsync(evc, 0, 4 * sizeof(unsigned long long), st));
     }
     StageMark msearch(ws, kSKnnSearch, st);
 #define ASP_KNN(KN)                                                                               \
@@ -986,12 +1108,18 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
                                (const double*)ys, (const double*)zs,                              \
                                (const unsigned long long*)kout, (const int*)iout, (long long)n,   \
                                k, (const KGrid*)dg, dh);                                          \
-        else                                                                                      \
-            hipLaunchKernelGGL(k_knn_wave<KN>, dim3((unsigned)((n + 255) / 256)),                  \
+        else if (mask)                                                                            \
+            hipLaunchKernelGGL((k_knn_wave<KN, true>), dim3((unsigned)((n + 255) / 256)),          \
                                dim3(kKnnBlock), 0, st, (const double*)xs, (const double*)ys,      \
                                (const double*)zs, (const unsigned long long*)kout,                \
-                               (const int*)iout, (long long)n, k, (const KGrid*)dg, dh, diag, whalf,  \
-                               fine, CT, f32, uq, evc);\
+                               (const int*)iout, (long long)n, k, (const KGrid*)dg, dh, diag,     \
+                               whalf, fine, CT, f32, uq, near, wgrp, ugrp, evc);                  \
+        else                                                                                      \
+            hipLaunchKernelGGL((k_knn_wave<KN, false>), dim3((unsigned)((n + 255) / 256)),         \
+                               dim3(kKnnBlock), 0, st, (const double*)xs, (const double*)ys,      \
+                               (const double*)zs, (const unsigned long long*)kout,                \
+                               (const int*)iout, (long long)n, k, (const KGrid*)dg, dh, diag,     \
+                               whalf, fine, CT, f32, uq, near, wgrp, ugrp, evc);                  \
     } while (0)
     if (k <= 32)
         ASP_KNN(32);
@@ -1002,12 +1130,13 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     msearch.done();
     for (int j = 9; j <= 12; ++j) ws.stats[j] = 0;
     if (evc) {
-        unsigned long long e[3];
+        unsigned long long e[4];
         ASP_HIP(hipMemcpyAsync(e, evc, sizeof(e), hipMemcpyDeviceToHost, st));
         ASP_HIP(hipStreamSynchronize(st));
         ws.stats[9] = (long long)e[0];
         ws.stats[10] = (long long)e[1];
         ws.stats[11] = (long long)e[2];
+        ws.stats[12] = (long long)e[3];
     }
     if (!dev) {
         ASP_HIP(hipMemcpyAsync(h, dh, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st));

@@ -503,6 +503,7 @@ def run_knn(args, dev):
                 "frac": round(t_peak / (s_ms * 1e-3), 4),
                 "distances_fp32": int(e32), "distances_fp64": int(e64),
                 "distances_shared_pass": int(eshared),
+                "topk_insertions_per_particle": round(float(st["evals_wide"]) / args.n, 1),
                 "distances_per_particle": round((e32 + e64) / args.n, 1),
                 "flops_per_distance": DIST_FLOPS,
                 "kernel_ms_per_step": round(s_ms, 4),

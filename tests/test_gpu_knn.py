@@ -115,13 +115,19 @@ def test_knn_fp32_window_prefilter_far_coordinates(gpu, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("uq", ["32", "56", "64"])
-def test_knn_shared_cell_pass(gpu, monkeypatch, uq):
+@pytest.mark.parametrize("uq,mask,near", [("0", "1", "0"), ("32", "1", "0"), ("56", "1", "0"),
+                                          ("64", "1", "0"), ("56", "0", "0"), ("64", "1", "1"),
+                                          ("0", "0", "1")])
+def test_knn_shared_cell_pass(gpu, monkeypatch, uq, mask, near):
     """The shared cell pass (asp_knn.hip, ASP_KNN_UNION = the lane quantile of the common
-    cell level): bit-exact against scipy on every input kind, the far-coordinate clusters
-    and 2e6 Plummer particles; the lanes it leaves out (looser radii) keep their own pass."""
+    cell level), the bit-mask entry test (ASP_KNN_MASK) and the nearest-chunks-first
+    window (ASP_KNN_NEAR): bit-exact against scipy on
+    every input kind, the far-coordinate clusters and 2e6 Plummer particles; the lanes the
+    shared pass leaves out (looser radii) keep their own pass."""
     from asp_amd.knn import knn_smoothing_lengths
     monkeypatch.setenv("ASP_KNN_UNION", uq)
+    monkeypatch.setenv("ASP_KNN_MASK", mask)
+    monkeypatch.setenv("ASP_KNN_NEAR", near)
     rng = np.random.default_rng(11)
     g = np.arange(30.0) * 0.5
     sets = [rng.uniform(0.0, 25.0, (60_000, 3)), _plummer(200_000, 5),
