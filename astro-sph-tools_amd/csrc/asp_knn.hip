@@ -480,7 +480,15 @@ constexpr int kCellFine = 1;   // verification cells >= half the ball radius (sw
 constexpr int kWindowF32 = 1;  // the window pass with the fp32 prefilter (wave_scan32)
 constexpr bool kMaskTest = false;  // the entry test's form (wave_stream32 MASK)
 constexpr int kUnionQ = 0;
-constexpr int kNearFirst = 0;  // window chunks nearest first (wave_scan32_near)     // the shared cell pass's lane quantile (of 64; 0: off)
+constexpr int kNearFirst = 0;  // window chunks nearest first (wave_scan32_near)
+#ifndef ASP_KNN_WGROUP
+#define ASP_KNN_WGROUP 16
+#endif
+#ifndef ASP_KNN_UGROUP
+#define ASP_KNN_UGROUP 32
+#endif
+constexpr int kWGroup = ASP_KNN_WGROUP;  // mask test: entries per candidate walk, window pass
+constexpr int kUGroup = ASP_KNN_UGROUP;  // ... and shared pass     // the shared cell pass's lane quantile (of 64; 0: off)
 
 template <int K>
 struct Cand {
@@ -572,13 +580,12 @@ __device__ __forceinline__ double wave_max(double v) {
 // The stream is entries f = 0 .. nent - 1 of the sorted arrays, entry f at sorted index
 // at(f) (-1: skip it -- its fp32 copy is NaN, which no bound passes); lanes with part false
 // take no candidates (their bound is -1).
-template <int K, bool MASK, class At>
+template <int K, bool MASK, int GRP, class At>
 __device__ __forceinline__ void wave_stream32(long long nent, At at, const double* __restrict__ xs,
                                               const double* __restrict__ ys,
                                               const double* __restrict__ zs, double* lx, double* ly,
                                               double* lz, float* fx, float* fy, float* fz, int lane,
-                                              double x, double y, double z, bool part, int grp,
-                                              TopK<K>& T) {
+                                              double x, double y, double z, bool part, TopK<K>& T) {
     const double ox = __shfl(x, 0, 64), oy = __shfl(y, 0, 64), oz = __shfl(z, 0, 64);
     const double rx = x - ox, ry = y - oy, rz = z - oz;
     const float qx = (float)rx, qy = (float)ry, qz = (float)rz;
@@ -627,26 +634,25 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
         };
         float tb = bound();
         if constexpr (MASK) {
-            // grp entries at a time (16 / 32): their fp32 copies by 16-byte LDS reads
+            // GRP entries at a time (16 / 32): their fp32 copies by 16-byte LDS reads
             // (every slot of the chunk is written, NaN past its end), the passing ones as a
             // bit mask, then each lane walks its own bits (exact fp64 distance, insert) --
             // the wave pays one walk per group in which any lane has a candidate
-            const int me4 = (m + 3) & ~3;
-            for (int g0 = 0; g0 < me4; g0 += grp) {
+            static_assert(GRP == 16 || GRP == 32, "group of 16 or 32 entries");
+            for (int g0 = 0; g0 < m; g0 += GRP) {
                 unsigned pm = 0;
-                const int ge = min(g0 + grp, me4);
 #pragma unroll 1
-                for (int q0 = g0; q0 < ge; q0 += 4) {
-                    const float4 X = *(const float4*)(fx + q0);
-                    const float4 Y = *(const float4*)(fy + q0);
-                    const float4 Z = *(const float4*)(fz + q0);
+                for (int u = 0; u < GRP; u += 4) {
+                    const float4 X = *(const float4*)(fx + g0 + u);
+                    const float4 Y = *(const float4*)(fy + g0 + u);
+                    const float4 Z = *(const float4*)(fz + g0 + u);
                     const float ax[4] = {X.x, X.y, X.z, X.w}, ay[4] = {Y.x, Y.y, Y.z, Y.w},
                                 az[4] = {Z.x, Z.y, Z.z, Z.w};
 #pragma unroll
                     for (int v = 0; v < 4; ++v) {
                         const float dx = qx - ax[v], dy = qy - ay[v], dz = qz - az[v];
                         const float d32 = (dx * dx + dy * dy) + dz * dz;
-                        pm |= (d32 <= tb ? 1u : 0u) << (q0 - g0 + v);
+                        pm |= (d32 <= tb ? 1u : 0u) << (u + v);
                     }
                 }
                 if (__builtin_amdgcn_ballot_w64(pm != 0)) {
@@ -694,8 +700,8 @@ __device__ __forceinline__ void wave_scan32(long long a, long long b, const doub
                                             const double* __restrict__ zs, double* lx, double* ly,
                                             double* lz, float* fx, float* fy, float* fz, int lane,
                                             double x, double y, double z, TopK<K>& T) {
-    wave_stream32<K, MASK>(b - a, [&](long long f) { return a + f; }, xs, ys, zs, lx, ly, lz, fx, fy, fz,
-                     lane, x, y, z, true, 16, T);
+    wave_stream32<K, MASK, kWGroup>(b - a, [&](long long f) { return a + f; }, xs, ys, zs, lx, ly, lz,
+                                    fx, fy, fz, lane, x, y, z, true, T);
 }
 
 // The window [a, b) around the wave's own 64 particles [base, base + 64), streamed
@@ -710,15 +716,15 @@ __device__ __forceinline__ void wave_scan32_near(long long a, long long b, long 
                                                  const double* __restrict__ zs, double* lx,
                                                  double* ly, double* lz, float* fx, float* fy,
                                                  float* fz, int lane, double x, double y, double z,
-                                                 int grp, TopK<K>& T) {
+                                                 TopK<K>& T) {
     const long long below = (base - a + 63) >> 6, above = (b - base - 1) >> 6;  // chunks each side
     const long long nch = 1 + 2 * max(below, above);
-    wave_stream32<K, MASK>(nch * 64, [&](long long f) -> long long {
+    wave_stream32<K, MASK, kWGroup>(nch * 64, [&](long long f) -> long long {
         const long long j = f >> 6, o = f & 63;
         const long long s = j == 0 ? 0 : (j & 1 ? -((j + 1) >> 1) : (j >> 1));  // 0, -1, +1, -2, +2, ...
         const long long g = base + s * 64 + o;
         return g >= a && g < b ? g : -1;
-    }, xs, ys, zs, lx, ly, lz, fx, fy, fz, lane, x, y, z, true, grp, T);
+    }, xs, ys, zs, lx, ly, lz, fx, fy, fz, lane, x, y, z, true, T);
 }
 
 __device__ __forceinline__ int wave_min_i(int v) {
@@ -766,7 +772,7 @@ constexpr int kUMaxEnt = 1 << 16; // entries streamed per wave at most
 #define ASP_KNN_OCC
 #endif
 template <int K, bool MASK>
-__global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double* __restrict__ xs,
+__global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_knn_wave(const double* __restrict__ xs,
                                                         const double* __restrict__ ys,
                                                         const double* __restrict__ zs,
                                                         const unsigned long long* __restrict__ keys,
@@ -774,8 +780,8 @@ __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double
                                                         int k, const KGrid* __restrict__ g,
                                                         double* __restrict__ h, int diag,
                                                         int whalf, int fine, CellTab CT,
-                                                        int f32, int uq, int near, int wgrp,
-                                                        int ugrp, unsigned long long* evc) {
+                                                        int f32, int uq, int near,
+                                                        unsigned long long* evc) {
     __shared__ double sx[kKnnBlock / 64][64], sy[kKnnBlock / 64][64], sz[kKnnBlock / 64][64];
     __shared__ __attribute__((aligned(16))) float fx[kKnnBlock / 64][64], fy[kKnnBlock / 64][64],
         fz[kKnnBlock / 64][64];
@@ -795,7 +801,7 @@ __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double
     if (f32) {
         if (near)
             wave_scan32_near<K, MASK>(win0, win1, base, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv],
-                                      fy[wv], fz[wv], lane, x, y, z, wgrp, C.T);
+                                      fy[wv], fz[wv], lane, x, y, z, C.T);
         else
             wave_scan32<K, MASK>(win0, win1, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv], fy[wv],
                                  fz[wv], lane, x, y, z, C.T);
@@ -917,8 +923,8 @@ __global__ __launch_bounds__(kKnnBlock) ASP_KNN_OCC void k_knn_wave(const double
                     const long long g = (long long)(unsigned)(e & 0xffffffffULL) + (f - (long long)(e >> 32));
                     return g >= win0 && g < win1 ? -1 : g;
                 };
-                wave_stream32<K, MASK>(tot, at, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv], fy[wv], fz[wv],
-                                 lane, x, y, z, rg, ugrp, C.T);
+                wave_stream32<K, MASK, kUGroup>(tot, at, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv], fy[wv], fz[wv],
+                                 lane, x, y, z, rg, C.T);
                 shared = rg;
                 if (evc && lane == 0) atomicAdd(&evc[2], (unsigned long long)tot);
             }
@@ -1087,9 +1093,6 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     const bool mask = getenv("ASP_KNN_MASK") ? atoi(getenv("ASP_KNN_MASK")) != 0 : kMaskTest;
     // the window pass's chunk order: nearest to the wave's own first (1) or in array order (0)
     const int near = getenv("ASP_KNN_NEAR") ? atoi(getenv("ASP_KNN_NEAR")) : kNearFirst;
-    // the mask test's group sizes (entries per candidate walk) in the window / shared passes
-    auto group = [](const char* v, int d) { const int g = v ? atoi(v) : d; return g == 32 ? 32 : 16; };
-    const int wgrp = group(getenv("ASP_KNN_WGROUP"), 16), ugrp = group(getenv("ASP_KNN_UGROUP"), 16);
     const int uq = getenv("ASP_KNN_UNION") ? std::min(64, std::max(0, atoi(getenv("ASP_KNN_UNION")))) : kUnionQ;
     // ASP_KNN_COUNT: count the distances the search evaluates (bench.py's k-NN roofline;
     // one atomic per lane, so off in timed runs) -> asp_last_stats [9] window, [10] cells,
@@ -1113,13 +1116,13 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
                                dim3(kKnnBlock), 0, st, (const double*)xs, (const double*)ys,      \
                                (const double*)zs, (const unsigned long long*)kout,                \
                                (const int*)iout, (long long)n, k, (const KGrid*)dg, dh, diag,     \
-                               whalf, fine, CT, f32, uq, near, wgrp, ugrp, evc);                  \
+                               whalf, fine, CT, f32, uq, near, evc);                              \
         else                                                                                      \
             hipLaunchKernelGGL((k_knn_wave<KN, false>), dim3((unsigned)((n + 255) / 256)),         \
                                dim3(kKnnBlock), 0, st, (const double*)xs, (const double*)ys,      \
                                (const double*)zs, (const unsigned long long*)kout,                \
                                (const int*)iout, (long long)n, k, (const KGrid*)dg, dh, diag,     \
-                               whalf, fine, CT, f32, uq, near, wgrp, ugrp, evc);                  \
+                               whalf, fine, CT, f32, uq, near, evc);                              \
     } while (0)
     if (k <= 32)
         ASP_KNN(32);
