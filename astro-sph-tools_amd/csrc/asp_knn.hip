@@ -761,7 +761,7 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 // Exact for the same reason as the per-lane pass: any level's cells meeting a ball cover it.
 constexpr int kUCells = 512;      // cells listed per wave (LDS); more: the per-lane pass
 constexpr int kUScan = 4096;      // cells of the common box tested per wave at most
-constexpr int kUMaxEnt = 1 << 16; // entries streamed per wave at most
+constexpr int kUMaxEnt = (1 << 16) - 1;  // entries streamed per wave at most (16-bit la)
 
 #ifndef ASP_KNN_WPE
 #define ASP_KNN_WPE 0  // waves per SIMD the search is compiled for (0: the compiler's choice)
@@ -785,7 +785,8 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
     __shared__ double sx[kKnnBlock / 64][64], sy[kKnnBlock / 64][64], sz[kKnnBlock / 64][64];
     __shared__ __attribute__((aligned(16))) float fx[kKnnBlock / 64][64], fy[kKnnBlock / 64][64],
         fz[kKnnBlock / 64][64];
-    __shared__ unsigned long long ucl[kKnnBlock / 64][kUCells];  // shared pass: cell keys, then (offset, start)
+    __shared__ unsigned long long ucl[kKnnBlock / 64][kUCells];  // shared pass: range keys, then (offset, start)
+    __shared__ unsigned short ucn[kKnnBlock / 64][kUCells];      // ... cells per key range
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long long base = ((long long)blockIdx.x * (kKnnBlock / 64) + wv) * 64;
     if (base >= n) return;  // wave-uniform
@@ -852,7 +853,8 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                 return fmax(fmax(l, h), 0.0);
             };
             const int sh3 = 3 * sw;
-            int nc = 0;
+            int nc = 0, run = 0;
+            unsigned long long lastk1 = 0;
             bool ovf = (long long)(B[0] - A[0] + 1) * (B[1] - A[1] + 1) > kUScan;
             for (int cx = A[0]; cx <= B[0] && !ovf; ++cx) {
                 const double gx = gapq(0, cx), sx2 = gx * gx;
@@ -875,35 +877,51 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                         const unsigned long long k0 = sh3 >= 63 ? 0ULL : p << sh3;
                         const unsigned long long k1 = sh3 >= 63 ? ~0ULL : (p + 1) << sh3;
                         if (k0 >= klo && k1 <= khi) continue;  // inside the window already
+                        if (nc > 0 && k0 == lastk1) {  // key-adjacent to the last entry (z pairs)
+                            ++run;
+                            lastk1 = k1;
+                            continue;
+                        }
                         if (nc == kUCells) {
                             ovf = true;
                             break;
                         }
-                        if (lane == 0) ucl[wv][nc] = k0;
+                        if (lane == 0) {
+                            if (nc > 0) ucn[wv][nc - 1] = (unsigned short)run;
+                            ucl[wv][nc] = k0;
+                        }
                         ++nc;
+                        run = 1;
+                        lastk1 = k1;
                     }
                 }
             }
+            if (lane == 0 && nc > 0) ucn[wv][nc - 1] = (unsigned short)run;
             long long tot = 0;
             if (!ovf && nc > 0) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (int c0 = 0; c0 < nc; c0 += 64) {  // lookups, 64 cells at a time
+                // lookups, 64 entries at a time: each entry's index range minus the window,
+                // as the part below it (la entries from j0) and the part above it (from
+                // max(j0, win1)); entry = offset << 47 | la << 31 | j0
+                for (int c0 = 0; c0 < nc; c0 += 64) {
                     const int c = c0 + lane;
-                    long long j0 = 0, len = 0;
+                    long long j0 = 0, la = 0, len = 0;
                     if (c < nc) {
                         const unsigned long long k0 = ucl[wv][c];
-                        const unsigned long long k1 = sh3 >= 63 ? ~0ULL : k0 + (1ULL << sh3);
+                        const unsigned long long span = (unsigned long long)ucn[wv][c] << sh3;
+                        const unsigned long long k1 = sh3 >= 63 ? ~0ULL : k0 + span;
                         j0 = cell_lower(keys, n, CT, k0);
                         const long long j1 = sh3 >= 63 || (k1 >> 63) ? n : cell_lower(keys, n, CT, k1);
-                        len = j1 - j0;
+                        la = max(0LL, min(j1, win0) - j0);
+                        len = la + max(0LL, j1 - max(j0, win1));
                     }
                     const int l32 = (int)min(len, (long long)kUMaxEnt + 1);
                     const long long incl = tot + wave_incl_scan(l32, lane);
                     if (c < nc)
-                        ucl[wv][c] = ((unsigned long long)min(incl - l32, (long long)kUMaxEnt + 1) << 32) |
-                                     (unsigned long long)(unsigned)j0;
+                        ucl[wv][c] = ((unsigned long long)min(incl - l32, (long long)kUMaxEnt + 1) << 47) |
+                                     ((unsigned long long)min(la, 0xffffLL) << 31) | (unsigned long long)j0;
                     tot = __shfl(incl, 63, 64);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -912,16 +930,17 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
             }
             if (!ovf && tot <= kUMaxEnt && diag != 2) {
                 const unsigned long long* L = ucl[wv];
-                auto at = [&](long long f) -> long long {  // the last cell starting at or before f
+                auto at = [&](long long f) -> long long {  // the last entry starting at or before f
                     int lo = 0, hi = nc - 1;
                     while (lo < hi) {
                         const int mid = (lo + hi + 1) >> 1;
-                        if ((long long)(L[mid] >> 32) <= f) lo = mid;
+                        if ((long long)(L[mid] >> 47) <= f) lo = mid;
                         else hi = mid - 1;
                     }
                     const unsigned long long e = L[lo];
-                    const long long g = (long long)(unsigned)(e & 0xffffffffULL) + (f - (long long)(e >> 32));
-                    return g >= win0 && g < win1 ? -1 : g;
+                    const long long o = f - (long long)(e >> 47), la = (long long)((e >> 31) & 0xffff);
+                    const long long j0 = (long long)(e & 0x7fffffffULL);
+                    return o < la ? j0 + o : max(j0, win1) + (o - la);
                 };
                 wave_stream32<K, MASK, kUGroup>(tot, at, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv], fy[wv], fz[wv],
                                  lane, x, y, z, rg, C.T);
