@@ -174,6 +174,9 @@ __device__ __forceinline__ double hw_max(double a, double b) {
     return r;
 }
 
+typedef float kf2 __attribute__((ext_vector_type(2)));  // packed fp32 pair (v_pk_* ops)
+typedef float kf4 __attribute__((ext_vector_type(4)));
+
 template <int K>
 struct TopK {
     double v[K];
@@ -589,6 +592,7 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
     const double ox = __shfl(x, 0, 64), oy = __shfl(y, 0, 64), oz = __shfl(z, 0, 64);
     const double rx = x - ox, ry = y - oy, rz = z - oz;
     const float qx = (float)rx, qy = (float)ry, qz = (float)rz;
+    const kf2 qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
     const double mq = wave_max(fmax(fabs(rx), fmax(fabs(ry), fabs(rz))));
     // chunk c + 64's entries are loaded (clamped index, unconditional loads) before chunk c
     // is tested, so the gathers' latency overlaps the tests
@@ -643,16 +647,19 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
                 unsigned pm = 0;
 #pragma unroll 1
                 for (int u = 0; u < GRP; u += 4) {
-                    const float4 X = *(const float4*)(fx + g0 + u);
-                    const float4 Y = *(const float4*)(fy + g0 + u);
-                    const float4 Z = *(const float4*)(fz + g0 + u);
-                    const float ax[4] = {X.x, X.y, X.z, X.w}, ay[4] = {Y.x, Y.y, Y.z, Y.w},
-                                az[4] = {Z.x, Z.y, Z.z, Z.w};
+                    // entries (u, u + 1) and (u + 2, u + 3) as packed pairs: the same
+                    // roundings as the scalar form, half the instructions
+                    const kf4 X = *(const kf4*)(fx + g0 + u);
+                    const kf4 Y = *(const kf4*)(fy + g0 + u);
+                    const kf4 Z = *(const kf4*)(fz + g0 + u);
 #pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        const float dx = qx - ax[v], dy = qy - ay[v], dz = qz - az[v];
-                        const float d32 = (dx * dx + dy * dy) + dz * dz;
-                        pm |= (d32 <= tb ? 1u : 0u) << (u + v);
+                    for (int v = 0; v < 4; v += 2) {
+                        const kf2 ex = v == 0 ? X.xy : X.zw, ey = v == 0 ? Y.xy : Y.zw,
+                                  ez = v == 0 ? Z.xy : Z.zw;
+                        const kf2 dx = qx2 - ex, dy = qy2 - ey, dz = qz2 - ez;
+                        const kf2 d = (dx * dx + dy * dy) + dz * dz;
+                        pm |= (d.x <= tb ? 1u : 0u) << (u + v);
+                        pm |= (d.y <= tb ? 1u : 0u) << (u + v + 1);
                     }
                 }
                 if (__builtin_amdgcn_ballot_w64(pm != 0)) {
