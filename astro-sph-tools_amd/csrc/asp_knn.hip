@@ -852,7 +852,7 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                 tq[a] = (c3[a] - G.lo[a]) * G.scale;
             }
             const double r2q = rg ? C.T.mx * G.scale * G.scale * (1.0 + 0x1p-36) : -1.0;
-            const double ed = (double)(1 << sw);  // cell edge in quanta
+            const double ed = (double)(1 << sw), ied = 1.0 / ed;  // cell edge in quanta (a power of two)
             // distance (quanta) from this lane's particle to the slab of cell cc on axis a,
             // the cell widened by one quantum each side
             auto gapq = [&](int a, int cc) {
@@ -874,8 +874,8 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                     int z0 = INT_MAX, z1 = -1;
                     if (s2 <= r2q) {
                         const double w = (double)(__builtin_amdgcn_sqrtf((float)(r2q - s2)) * (1.0f + 0x1p-18f)) + 2.0;
-                        z0 = (int)floor((tq[2] - 1.0 - w) / ed) - 1;
-                        z1 = (int)floor((tq[2] + 1.0 + w) / ed);
+                        z0 = (int)floor((tq[2] - 1.0 - w) * ied) - 1;  // ied = 1 / ed exactly
+                        z1 = (int)floor((tq[2] + 1.0 + w) * ied);
                     }
                     const int cz0 = max(A[2], __builtin_amdgcn_readfirstlane(wave_min_i(z0)));
                     const int cz1 = min(B[2], __builtin_amdgcn_readfirstlane(wave_max_i(z1)));
