@@ -872,7 +872,7 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
     const unsigned long long khi = win1 == n ? ~0ULL : keys[win1 - 1];
     bool shared = false;  // this lane's ball is covered by the shared cell pass
     // diag (timing only, wrong results): 2 = the shared pass's cell list and lookups without
-    // its stream, 3 = the shared pass without the per-lane pass
+    // its stream, 3 = the shared pass without the per-lane pass, 4 = the cell list alone
     if (uq > 0 && f32 && n >= k && (diag == 0 || diag >= 2)) {  // wave-uniform
         const bool ok = act && C.T.mx < INFINITY;
         const double R = sqrt(C.T.mx) * (1.0 + 0x1p-40);
@@ -912,6 +912,10 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
             const int sh3 = 3 * sw;
             int nc = 0, run = 0;
             unsigned long long lastk1 = 0;
+            // cells p with k0 = p << sh3 >= klo and k1 = (p + 1) << sh3 <= khi lie inside the
+            // window's key span: p >= ceil(klo / 2^sh3), p < floor(khi / 2^sh3)
+            const unsigned long long plo = sh3 >= 63 ? 1ULL : (klo >> sh3) + ((klo & ((1ULL << sh3) - 1)) != 0);
+            const unsigned long long phi = sh3 >= 63 ? 0ULL : (khi >> sh3);
             bool ovf = (long long)(B[0] - A[0] + 1) * (B[1] - A[1] + 1) > kUScan;
             for (int cx = A[0]; cx <= B[0] && !ovf; ++cx) {
                 const double gx = gapq(0, cx), sx2 = gx * gx;
@@ -929,11 +933,18 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                     }
                     const int cz0 = max(A[2], __builtin_amdgcn_readfirstlane(wave_min_i(z0)));
                     const int cz1 = min(B[2], __builtin_amdgcn_readfirstlane(wave_max_i(z1)));
-                    for (int cz = cz0; cz <= cz1; ++cz) {
-                        const unsigned long long p = morton3(cx, cy, cz);
+                    // the column's Morton codes: x / y bits once, the z bits stepped by a
+                    // dilated increment (set the non-z bits, add one, keep the z bits) --
+                    // scalar work per cell, which all the waves of a CU share
+                    constexpr unsigned long long kZBits = 0x1249249249249249ULL;
+                    const unsigned long long pxy = (spread21(cx) << 2) | (spread21(cy) << 1);
+                    unsigned long long pz = spread21(cz0);
+                    for (int cz = cz0; cz <= cz1; ++cz, pz = ((pz | ~kZBits) + 1) & kZBits) {
+                        const unsigned long long p = pxy | pz;
+                        // inside the window's key span: p in [plo, phi)
+                        if (p >= plo && p < phi) continue;
                         const unsigned long long k0 = sh3 >= 63 ? 0ULL : p << sh3;
                         const unsigned long long k1 = sh3 >= 63 ? ~0ULL : (p + 1) << sh3;
-                        if (k0 >= klo && k1 <= khi) continue;  // inside the window already
                         if (nc > 0 && k0 == lastk1) {  // key-adjacent to the last entry (z pairs)
                             ++run;
                             lastk1 = k1;
@@ -955,7 +966,7 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
             }
             if (lane == 0 && nc > 0) ucn[wv][nc - 1] = (unsigned short)run;
             long long tot = 0;
-            if (!ovf && nc > 0) {
+            if (!ovf && nc > 0 && diag != 4) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -990,7 +1001,7 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
-            if (!ovf && tot <= kUMaxEnt && diag != 2) {
+            if (!ovf && tot <= kUMaxEnt && diag != 2 && diag != 4) {
                 const unsigned long long* L = ucl[wv];
                 auto at = [&](long long f) -> long long {  // the last entry starting at or before f
                     int lo = 0, hi = nc - 1;
