@@ -611,10 +611,45 @@ __device__ __forceinline__ void scan_range(long long a, long long b, const doubl
     for (; j < b; ++j) T.insert(dist2(x, y, z, xs[j], ys[j], zs[j]));
 }
 
-__device__ __forceinline__ double wave_max(double v) {
+// Wave reductions by DPP (quad_perm xor 1 / xor 2, row_half_mirror, row_mirror, then
+// row_bcast15 / row_bcast31 into lane 63) and one v_readlane: six dependent VALU steps where
+// __shfl_xor took six ds_bpermute round trips through LDS (the shared pass's cell
+// enumeration reduces twice per column).  Every lane of the wave must be active; the result
+// is uniform.
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, RM, 0xf, false);
+}
+template <class Op>
+__device__ __forceinline__ int wave_reduce_i(int v, Op op) {
+    v = op(v, dpp_i<0xb1>(v));       // quad_perm [1, 0, 3, 2]
+    v = op(v, dpp_i<0x4e>(v));       // quad_perm [2, 3, 0, 1]
+    v = op(v, dpp_i<0x141>(v));      // row_half_mirror
+    v = op(v, dpp_i<0x140>(v));      // row_mirror
+    v = op(v, dpp_i<0x142, 0xa>(v)); // row_bcast15 into rows 1, 3
+    v = op(v, dpp_i<0x143, 0xc>(v)); // row_bcast31 into rows 2, 3
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ double dpp_d(double v, int which) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    int lo = (int)(unsigned)b, hi = (int)(unsigned)(b >> 32);
+    switch (which) {
+        case 0: lo = dpp_i<0xb1>(lo); hi = dpp_i<0xb1>(hi); break;
+        case 1: lo = dpp_i<0x4e>(lo); hi = dpp_i<0x4e>(hi); break;
+        case 2: lo = dpp_i<0x141>(lo); hi = dpp_i<0x141>(hi); break;
+        case 3: lo = dpp_i<0x140>(lo); hi = dpp_i<0x140>(hi); break;
+        case 4: lo = dpp_i<0x142, 0xa>(lo); hi = dpp_i<0x142, 0xa>(hi); break;
+        default: lo = dpp_i<0x143, 0xc>(lo); hi = dpp_i<0x143, 0xc>(hi); break;
+    }
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_max(double v) {  // v >= 0 or NaN-free
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
+    for (int w = 0; w < 6; ++w) v = fmax(v, dpp_d(v, w));
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)b, 63);
+    const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(b >> 32), 63);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
 // The window pass with an fp32 prefilter.  Entries go to LDS twice: fp64 (for the exact
@@ -785,14 +820,10 @@ __device__ __forceinline__ void wave_scan32_near(long long a, long long b, long 
 }
 
 __device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
+    return wave_reduce_i(v, [](int a, int b) { return min(a, b); });
 }
 __device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
+    return wave_reduce_i(v, [](int a, int b) { return max(a, b); });
 }
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 #pragma unroll
