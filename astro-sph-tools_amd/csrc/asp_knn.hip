@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 
@@ -528,12 +529,12 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn(const double* __restrict__ xs
 // nothing.
 // ----------------------------------------------------------------------------------
 constexpr int kBufSlots = 8;
-constexpr int kWinHalf = 64;   // W: curve window each side of the wave (swept: 64-512; 64 since the sub-tables)
+constexpr int kWinHalf = 192;  // W: curve window each side of the wave (round 6, with the shared pass: 64-320 swept)
 constexpr int kCellFine = 1;   // verification cells >= half the ball radius (swept: 0-3)
 constexpr int kWindowF32 = 1;  // the window pass with the fp32 prefilter (wave_scan32)
-constexpr bool kMaskTest = false;  // the entry test's form (wave_stream32 MASK)
-constexpr int kUnionQ = 0;
-constexpr int kNearFirst = 0;  // window chunks nearest first (wave_scan32_near)
+constexpr bool kMaskTest = true;  // the entry test's form (wave_stream32 MASK)
+constexpr int kUnionQ = 64;
+constexpr int kNearFirst = 1;  // window chunks nearest first (wave_scan32_near)
 #ifndef ASP_KNN_WGROUP
 #define ASP_KNN_WGROUP 16
 #endif
@@ -941,7 +942,7 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                 return fmax(fmax(l, h), 0.0);
             };
             const int sh3 = 3 * sw;
-            int nc = 0, run = 0;
+            int nc = 0, run = 0, ncol = 0;
             unsigned long long lastk1 = 0;
             // cells p with k0 = p << sh3 >= klo and k1 = (p + 1) << sh3 <= khi lie inside the
             // window's key span: p >= ceil(klo / 2^sh3), p < floor(khi / 2^sh3)
@@ -952,6 +953,7 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                 const double gx = gapq(0, cx), sx2 = gx * gx;
                 if (!__ballot(sx2 <= r2q)) continue;
                 for (int cy = A[1]; cy <= B[1] && !ovf; ++cy) {
+                    ++ncol;
                     const double gy = gapq(1, cy), s2 = sx2 + gy * gy;
                     // this lane's cells of the column: gap_z^2 <= r2q - s2, i.e. cz in
                     // [(t - 1 - w) / ed - 1, (t + 1 + w) / ed], w = sqrt(r2q - s2) (fp32,
@@ -996,6 +998,11 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                 }
             }
             if (lane == 0 && nc > 0) ucn[wv][nc - 1] = (unsigned short)run;
+            if (evc && lane == 0) {  // diagnostic: columns and list entries of the shared pass
+                atomicAdd(&evc[4], (unsigned long long)ncol);
+                atomicAdd(&evc[5], (unsigned long long)nc);
+                atomicAdd(&evc[6], 1ULL);
+            }
             long long tot = 0;
             if (!ovf && nc > 0 && diag != 4) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1222,9 +1229,9 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     // [11] entries the shared cell pass streamed (once per wave), [12] top-k insertions
     unsigned long long* evc = nullptr;
     if (getenv("ASP_KNN_COUNT")) {
-        ASP_TRY(ensure(ws.knn[11], 4 * sizeof(unsigned long long)));
+        ASP_TRY(ensure(ws.knn[11], 8 * sizeof(unsigned long long)));
         evc = (unsigned long long*)ws.knn[11].p;
-        ASP_HIP(hipMemsetAsync(evc, 0, 4 * sizeof(unsigned long long), st));
+        ASP_HIP(hipMemsetAsync(evc, 0, 8 * sizeof(unsigned long long), st));
     }
     StageMark msearch(ws, kSKnnSearch, st);
 #define ASP_KNN(KN)                                                                               \
@@ -1256,13 +1263,16 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     msearch.done();
     for (int j = 9; j <= 12; ++j) ws.stats[j] = 0;
     if (evc) {
-        unsigned long long e[4];
+        unsigned long long e[8];
         ASP_HIP(hipMemcpyAsync(e, evc, sizeof(e), hipMemcpyDeviceToHost, st));
         ASP_HIP(hipStreamSynchronize(st));
         ws.stats[9] = (long long)e[0];
         ws.stats[10] = (long long)e[1];
         ws.stats[11] = (long long)e[2];
         ws.stats[12] = (long long)e[3];
+        if (getenv("ASP_KNN_COUNT_PRINT"))
+            fprintf(stderr, "knn shared pass: %llu waves, %.1f columns and %.1f ranges per wave\n", e[6],
+                    e[6] ? (double)e[4] / e[6] : 0.0, e[6] ? (double)e[5] / e[6] : 0.0);
     }
     if (!dev) {
         ASP_HIP(hipMemcpyAsync(h, dh, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st));

@@ -115,13 +115,15 @@ def test_knn_fp32_window_prefilter_far_coordinates(gpu, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("uq,mask,near", [("0", "1", "0"), ("32", "1", "0"), ("56", "1", "0"),
-                                          ("64", "1", "0"), ("56", "0", "0"), ("64", "1", "1"),
+@pytest.mark.parametrize("uq,mask,near", [("0", "0", "0"), ("0", "1", "0"), ("32", "1", "0"),
+                                          ("56", "1", "0"), ("64", "1", "0"), ("56", "0", "0"),
                                           ("0", "0", "1")])
 def test_knn_shared_cell_pass(gpu, monkeypatch, uq, mask, near):
-    """The shared cell pass (asp_knn.hip, ASP_KNN_UNION = the lane quantile of the common
-    cell level), the bit-mask entry test (ASP_KNN_MASK) and the nearest-chunks-first
-    window (ASP_KNN_NEAR): bit-exact against scipy on
+    """The search's switches off their defaults (the defaults -- shared cell pass over all
+    lanes, bit-mask entry test, nearest-chunks-first window -- run in every other test):
+    the shared cell pass at other lane quantiles (ASP_KNN_UNION, 0 = the per-lane cell pass
+    of round 5), the 8-slot entry buffer (ASP_KNN_MASK=0), the window in array order
+    (ASP_KNN_NEAR=0): bit-exact against scipy on
     every input kind, the far-coordinate clusters and 2e6 Plummer particles; the lanes the
     shared pass leaves out (looser radii) keep their own pass."""
     from asp_amd.knn import knn_smoothing_lengths
