@@ -942,8 +942,7 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                 return fmax(fmax(l, h), 0.0);
             };
             const int sh3 = 3 * sw;
-            int nc = 0, run = 0, ncol = 0;
-            unsigned long long lastk1 = 0;
+            int nc = 0, ncol = 0;
             // cells p with k0 = p << sh3 >= klo and k1 = (p + 1) << sh3 <= khi lie inside the
             // window's key span: p >= ceil(klo / 2^sh3), p < floor(khi / 2^sh3)
             const unsigned long long plo = sh3 >= 63 ? 1ULL : (klo >> sh3) + ((klo & ((1ULL << sh3) - 1)) != 0);
@@ -966,38 +965,34 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                     }
                     const int cz0 = max(A[2], __builtin_amdgcn_readfirstlane(wave_min_i(z0)));
                     const int cz1 = min(B[2], __builtin_amdgcn_readfirstlane(wave_max_i(z1)));
-                    // the column's Morton codes: x / y bits once, the z bits stepped by a
-                    // dilated increment (set the non-z bits, add one, keep the z bits) --
-                    // scalar work per cell, which all the waves of a CU share
-                    constexpr unsigned long long kZBits = 0x1249249249249249ULL;
+                    // the column's cells, one per lane: Morton code, the window test, and
+                    // the key-adjacent (even z, z + 1) pairs merged into one range -- the
+                    // only cells of a column adjacent in key order (z is the lowest bit)
                     const unsigned long long pxy = (spread21(cx) << 2) | (spread21(cy) << 1);
-                    unsigned long long pz = spread21(cz0);
-                    for (int cz = cz0; cz <= cz1; ++cz, pz = ((pz | ~kZBits) + 1) & kZBits) {
-                        const unsigned long long p = pxy | pz;
-                        // inside the window's key span: p in [plo, phi)
-                        if (p >= plo && p < phi) continue;
-                        const unsigned long long k0 = sh3 >= 63 ? 0ULL : p << sh3;
-                        const unsigned long long k1 = sh3 >= 63 ? ~0ULL : (p + 1) << sh3;
-                        if (nc > 0 && k0 == lastk1) {  // key-adjacent to the last entry (z pairs)
-                            ++run;
-                            lastk1 = k1;
-                            continue;
-                        }
-                        if (nc == kUCells) {
+                    for (int zb = cz0; zb <= cz1 && !ovf; zb += 64) {
+                        const int cz = zb + lane;
+                        const unsigned long long p = pxy | spread21(cz);
+                        const bool inc = cz <= cz1 && !(p >= plo && p < phi);
+                        const unsigned long long I = __ballot(inc);
+                        const bool prev = lane > 0 && ((I >> (lane - 1)) & 1);
+                        const bool next = lane < 63 && ((I >> (lane + 1)) & 1);
+                        const bool start = inc && !((cz & 1) && prev);
+                        const unsigned long long S = __ballot(start);
+                        const int idx = nc + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(S >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((unsigned)S, 0u));
+                        const int cnt = __popcll(S);
+                        if (nc + cnt > kUCells) {
                             ovf = true;
                             break;
                         }
-                        if (lane == 0) {
-                            if (nc > 0) ucn[wv][nc - 1] = (unsigned short)run;
-                            ucl[wv][nc] = k0;
+                        if (start) {
+                            ucl[wv][idx] = sh3 >= 63 ? 0ULL : p << sh3;
+                            ucn[wv][idx] = (unsigned short)(1 + ((cz & 1) == 0 && next));
                         }
-                        ++nc;
-                        run = 1;
-                        lastk1 = k1;
+                        nc += cnt;
                     }
                 }
             }
-            if (lane == 0 && nc > 0) ucn[wv][nc - 1] = (unsigned short)run;
             if (evc && lane == 0) {  // diagnostic: columns and list entries of the shared pass
                 atomicAdd(&evc[4], (unsigned long long)ncol);
                 atomicAdd(&evc[5], (unsigned long long)nc);
