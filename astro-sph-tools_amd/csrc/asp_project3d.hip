@@ -58,6 +58,9 @@ constexpr int kBrickVox = kBX * kBY * kBZ;   // 8192 -> 64 KiB of fp64 accumulat
 #ifndef ASP_CUBE_PLANES
 #define ASP_CUBE_PLANES 1
 #endif
+#ifndef ASP_CUBE_ODD_MASK
+#define ASP_CUBE_ODD_MASK 0  // 1: mask the odd column's extra plane-pair add (A/B switch)
+#endif
 // LDS accumulator layout.  Plane-major (ASP_CUBE_PLANES, default): voxel (i, j, k) at
 // k * 256 + i * 16 + j, so a plane is 256 doubles = 8 x 64 banks and a voxel's bank pair
 // depends on its column only -- the lanes of a wave walking adjacent columns from
@@ -467,7 +470,10 @@ __device__ __forceinline__ void plane_walk(double* col, float fa, float fb, floa
     for (; lk2.x <= fb; lk2 += (f2){2.0f, 2.0f}, p += 2 * kKStride) {
         const f2 w = planes2(lk2);
         atomicAdd(p, (double)w.x);
-        atomicAdd(p + kKStride, (double)w.y);
+#if ASP_CUBE_ODD_MASK
+        if (lk2.y <= fb)  // the odd column's extra plane: no LDS add (the LDS pipe is shared)
+#endif
+            atomicAdd(p + kKStride, (double)w.y);
     }
 }
 
