@@ -956,7 +956,10 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
     long long n_recs = 0;
     int n_items = 0, n_merges = 0, n_slabs = 0;
     ASP_TRY(ensure_morton3(ws, g, st));
-    long long nblk = std::min<long long>(512, std::max<long long>(1, (n + 8191) / 8192));
+    // count workgroups (scatter workgroups: half as many): ASP_CUBE_BLOCKS overrides the 512
+    // (read per call; fewer scatter workgroups keep fewer (workgroup, brick) runs open)
+    const long long max_blk = getenv("ASP_CUBE_BLOCKS") ? std::max(2, atoi(getenv("ASP_CUBE_BLOCKS"))) : 512;
+    long long nblk = std::min<long long>(max_blk, std::max<long long>(1, (n + 8191) / 8192));
     // batch-interleaved count / scatter (ASP_CUBE_INTERLEAVE=0: contiguous ranges per block)
     static const int inter = getenv("ASP_CUBE_INTERLEAVE") ? atoi(getenv("ASP_CUBE_INTERLEAVE")) : 1;
     long long per_block = (n + nblk - 1) / nblk;
