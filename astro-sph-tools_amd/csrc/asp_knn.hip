@@ -716,11 +716,20 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const float Mf = (float)M * (1.0f + 0x1p-22f);  // >= M
         auto bound = [&]() -> float {
             if (!part) return -1.0f;
             if (!(T.mx < INFINITY)) return INFINITY;
-            const double r = sqrt(T.mx) * (1.0 + 0x1p-22) + 0x1p-21 * M;
-            return (float)(r * r * (1.0 + 0x1p-21)) * (1.0f + 0x1p-22f);
+            if (T.mx < 0x1p-100) {  // fp32 would lose the radius: the fp64 form
+                const double r = sqrt(T.mx) * (1.0 + 0x1p-22) + 0x1p-21 * M;
+                return (float)(r * r * (1.0 + 0x1p-21)) * (1.0f + 0x1p-22f);
+            }
+            // the same bound in fp32 (round 6): sqrt of fl32(mx) is within ~2^-23 of
+            // sqrt(mx); widened by 2^-18 (and Mf >= M (1 + 2^-23)), the fp32 sum is >= the
+            // fp64 form's (1 + 2^-22) sqrt(mx) + 2^-21 M, and its square times (1 + 2^-18)
+            // >= that squared times (1 + 2^-21): never below the fp64 bound
+            const float r = __builtin_amdgcn_sqrtf((float)T.mx) * (1.0f + 0x1p-18f) + 0x1p-21f * Mf;
+            return r * r * (1.0f + 0x1p-18f);
         };
         float tb = bound();
         if constexpr (MASK) {
