@@ -535,6 +535,9 @@ constexpr int kWindowF32 = 1;  // the window pass with the fp32 prefilter (wave_
 constexpr bool kMaskTest = true;  // the entry test's form (wave_stream32 MASK)
 constexpr int kUnionQ = 64;
 constexpr int kNearFirst = 1;  // window chunks nearest first (wave_scan32_near)
+#ifndef ASP_KNN_PREFETCH2
+#define ASP_KNN_PREFETCH2 0  // 1: the stream's gathers two chunks ahead (A/B switch)
+#endif
 #ifndef ASP_KNN_WGROUP
 #define ASP_KNN_WGROUP 16
 #endif
@@ -682,22 +685,38 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
     const double mq = wave_max(fmax(fabs(rx), fmax(fabs(ry), fabs(rz))));
     // chunk c + 64's entries are loaded (clamped index, unconditional loads) before chunk c
     // is tested, so the gathers' latency overlaps the tests
-    auto entry = [&](long long c, long long& g, double& ex, double& ey, double& ez) {
-        g = c + lane < nent ? at(c + lane) : -1;
-        const long long gi = g >= 0 ? g : 0;
+    auto entry = [&](long long c, int& g, double& ex, double& ey, double& ez) {
+        g = c + lane < nent ? (int)at(c + lane) : -1;  // sorted indices < 2^31
+        const int gi = g >= 0 ? g : 0;
         ex = xs[gi];
         ey = ys[gi];
         ez = zs[gi];
     };
-    long long gn;
+#if ASP_KNN_PREFETCH2
+    // two chunks ahead
+    int gn, gn2;
+    double exn, eyn, ezn, exn2, eyn2, ezn2;
+    entry(0, gn, exn, eyn, ezn);
+    entry(64, gn2, exn2, eyn2, ezn2);
+#else
+    int gn;
     double exn, eyn, ezn;
     entry(0, gn, exn, eyn, ezn);
+#endif
     for (long long c = 0; c < nent; c += 64) {
         const int m = (int)min(64LL, nent - c);
         double me = 0.0;
-        const long long g = gn;
+        const int g = gn;
         const double ex = exn, ey = eyn, ez = ezn;
+#if ASP_KNN_PREFETCH2
+        gn = gn2;
+        exn = exn2;
+        eyn = eyn2;
+        ezn = ezn2;
+        if (c + 128 < nent) entry(c + 128, gn2, exn2, eyn2, ezn2);
+#else
         if (c + 64 < nent) entry(c + 64, gn, exn, eyn, ezn);
+#endif
         if (g >= 0) {
             lx[lane] = ex;
             ly[lane] = ey;
