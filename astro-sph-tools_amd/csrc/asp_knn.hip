@@ -535,9 +535,6 @@ constexpr int kWindowF32 = 1;  // the window pass with the fp32 prefilter (wave_
 constexpr bool kMaskTest = true;  // the entry test's form (wave_stream32 MASK)
 constexpr int kUnionQ = 64;
 constexpr int kNearFirst = 1;  // window chunks nearest first (wave_scan32_near)
-#ifndef ASP_KNN_PREFETCH2
-#define ASP_KNN_PREFETCH2 0  // 1: the stream's gathers two chunks ahead (A/B switch)
-#endif
 #ifndef ASP_KNN_WGROUP
 #define ASP_KNN_WGROUP 16
 #endif
@@ -692,31 +689,16 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
         ey = ys[gi];
         ez = zs[gi];
     };
-#if ASP_KNN_PREFETCH2
-    // two chunks ahead
-    int gn, gn2;
-    double exn, eyn, ezn, exn2, eyn2, ezn2;
-    entry(0, gn, exn, eyn, ezn);
-    entry(64, gn2, exn2, eyn2, ezn2);
-#else
+    // (two chunks ahead measured slower: 18.81 vs 18.59 ms at 10^7, same box)
     int gn;
     double exn, eyn, ezn;
     entry(0, gn, exn, eyn, ezn);
-#endif
     for (long long c = 0; c < nent; c += 64) {
         const int m = (int)min(64LL, nent - c);
         double me = 0.0;
         const int g = gn;
         const double ex = exn, ey = eyn, ez = ezn;
-#if ASP_KNN_PREFETCH2
-        gn = gn2;
-        exn = exn2;
-        eyn = eyn2;
-        ezn = ezn2;
-        if (c + 128 < nent) entry(c + 128, gn2, exn2, eyn2, ezn2);
-#else
         if (c + 64 < nent) entry(c + 64, gn, exn, eyn, ezn);
-#endif
         if (g >= 0) {
             lx[lane] = ex;
             ly[lane] = ey;
