@@ -674,7 +674,8 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
                                               const double* __restrict__ ys,
                                               const double* __restrict__ zs, double* lx, double* ly,
                                               double* lz, float* fx, float* fy, float* fz, int lane,
-                                              double x, double y, double z, bool part, TopK<K>& T) {
+                                              double x, double y, double z, bool part, TopK<K>& T,
+                                              bool fill = false) {
     const double ox = __shfl(x, 0, 64), oy = __shfl(y, 0, 64), oz = __shfl(z, 0, 64);
     const double rx = x - ox, ry = y - oy, rz = z - oz;
     const float qx = (float)rx, qy = (float)ry, qz = (float)rz;
@@ -739,7 +740,38 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
             // bit mask, then each lane walks its own bits (exact fp64 distance, insert) --
             // the wave pays one walk per group in which any lane has a candidate
             static_assert(GRP == 16 || GRP == 32, "group of 16 or 32 entries");
-            for (int g0 = 0; g0 < m; g0 += GRP) {
+            int gstart = 0;
+            if (fill && c == 0 && m >= K) {
+                // the first K entries straight into the empty top-k (k == K: no -inf slots):
+                // their exact distances (an entry without a particle, or a NaN distance,
+                // as +inf -- what insert() would not take), sorted by a bitonic network
+                // (K/2 log2 K (log2 K + 1)/2 compare-exchanges, 480 min / max for K = 32)
+                // instead of K insertions of 2K min / max each
+#pragma unroll
+                for (int q = 0; q < K; ++q) {
+                    const double d = fx[q] == fx[q] ? dist2(x, y, z, lx[q], ly[q], lz[q]) : INFINITY;
+                    T.v[q] = d < INFINITY ? d : INFINITY;
+                }
+#pragma unroll
+                for (int sz = 2; sz <= K; sz <<= 1)
+#pragma unroll
+                    for (int st = sz >> 1; st > 0; st >>= 1)
+#pragma unroll
+                        for (int i = 0; i < K; ++i) {
+                            const int j = i ^ st;
+                            if (j > i) {
+                                const double lo = hw_min(T.v[i], T.v[j]), hi = hw_max(T.v[i], T.v[j]);
+                                const bool up = (i & sz) == 0;
+                                T.v[i] = up ? lo : hi;
+                                T.v[j] = up ? hi : lo;
+                            }
+                        }
+                T.mx = T.v[K - 1];
+                T.nins += K;
+                tb = bound();
+                gstart = K;
+            }
+            for (int g0 = gstart; g0 < m; g0 += GRP) {
                 unsigned pm = 0;
 #pragma unroll 1
                 for (int u = 0; u < GRP; u += 4) {
@@ -819,7 +851,7 @@ __device__ __forceinline__ void wave_scan32_near(long long a, long long b, long 
                                                  const double* __restrict__ zs, double* lx,
                                                  double* ly, double* lz, float* fx, float* fy,
                                                  float* fz, int lane, double x, double y, double z,
-                                                 TopK<K>& T) {
+                                                 TopK<K>& T, bool fill) {
     const long long below = (base - a + 63) >> 6, above = (b - base - 1) >> 6;  // chunks each side
     const long long nch = 1 + 2 * max(below, above);
     wave_stream32<K, MASK, kWGroup>(nch * 64, [&](long long f) -> long long {
@@ -827,7 +859,7 @@ __device__ __forceinline__ void wave_scan32_near(long long a, long long b, long 
         const long long s = j == 0 ? 0 : (j & 1 ? -((j + 1) >> 1) : (j >> 1));  // 0, -1, +1, -2, +2, ...
         const long long g = base + s * 64 + o;
         return g >= a && g < b ? g : -1;
-    }, xs, ys, zs, lx, ly, lz, fx, fy, fz, lane, x, y, z, true, T);
+    }, xs, ys, zs, lx, ly, lz, fx, fy, fz, lane, x, y, z, true, T, fill);
 }
 
 __device__ __forceinline__ int wave_min_i(int v) {
@@ -879,7 +911,7 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                                                         int k, const KGrid* __restrict__ g,
                                                         double* __restrict__ h, int diag,
                                                         int whalf, int fine, CellTab CT,
-                                                        int f32, int uq, int near,
+                                                        int f32, int uq, int near, int fill,
                                                         unsigned long long* evc) {
     __shared__ double sx[kKnnBlock / 64][64], sy[kKnnBlock / 64][64], sz[kKnnBlock / 64][64];
     __shared__ __attribute__((aligned(16))) float fx[kKnnBlock / 64][64], fy[kKnnBlock / 64][64],
@@ -901,7 +933,7 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
     if (f32) {
         if (near)
             wave_scan32_near<K, MASK>(win0, win1, base, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv],
-                                      fy[wv], fz[wv], lane, x, y, z, C.T);
+                                      fy[wv], fz[wv], lane, x, y, z, C.T, fill && k == K);
         else
             wave_scan32<K, MASK>(win0, win1, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv], fy[wv],
                                  fz[wv], lane, x, y, z, C.T);
@@ -1228,6 +1260,8 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     const bool mask = getenv("ASP_KNN_MASK") ? atoi(getenv("ASP_KNN_MASK")) != 0 : kMaskTest;
     // the window pass's chunk order: nearest to the wave's own first (1) or in array order (0)
     const int near = getenv("ASP_KNN_NEAR") ? atoi(getenv("ASP_KNN_NEAR")) : kNearFirst;
+    // the window's first k entries sorted into the empty top-k (k == 32 / 64 only)
+    const int fill = getenv("ASP_KNN_FILL") ? atoi(getenv("ASP_KNN_FILL")) : 1;
     const int uq = getenv("ASP_KNN_UNION") ? std::min(64, std::max(0, atoi(getenv("ASP_KNN_UNION")))) : kUnionQ;
     // ASP_KNN_COUNT: count the distances the search evaluates (bench.py's k-NN roofline;
     // one atomic per lane, so off in timed runs) -> asp_last_stats [9] window, [10] cells,
@@ -1251,13 +1285,13 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
                                dim3(kKnnBlock), 0, st, (const double*)xs, (const double*)ys,      \
                                (const double*)zs, (const unsigned long long*)kout,                \
                                (const int*)iout, (long long)n, k, (const KGrid*)dg, dh, diag,     \
-                               whalf, fine, CT, f32, uq, near, evc);                              \
+                               whalf, fine, CT, f32, uq, near, fill, evc);                        \
         else                                                                                      \
             hipLaunchKernelGGL((k_knn_wave<KN, false>), dim3((unsigned)((n + 255) / 256)),         \
                                dim3(kKnnBlock), 0, st, (const double*)xs, (const double*)ys,      \
                                (const double*)zs, (const unsigned long long*)kout,                \
                                (const int*)iout, (long long)n, k, (const KGrid*)dg, dh, diag,     \
-                               whalf, fine, CT, f32, uq, near, evc);                              \
+                               whalf, fine, CT, f32, uq, near, fill, evc);                        \
     } while (0)
     if (k <= 32)
         ASP_KNN(32);

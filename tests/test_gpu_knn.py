@@ -115,10 +115,11 @@ def test_knn_fp32_window_prefilter_far_coordinates(gpu, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("uq,mask,near", [("0", "0", "0"), ("0", "1", "0"), ("32", "1", "0"),
-                                          ("56", "1", "0"), ("64", "1", "0"), ("56", "0", "0"),
-                                          ("0", "0", "1")])
-def test_knn_shared_cell_pass(gpu, monkeypatch, uq, mask, near):
+@pytest.mark.parametrize("uq,mask,near,fill", [("0", "0", "0", "1"), ("0", "1", "0", "1"),
+                                               ("32", "1", "0", "1"), ("56", "1", "0", "1"),
+                                               ("64", "1", "0", "1"), ("56", "0", "0", "1"),
+                                               ("0", "0", "1", "1"), ("64", "1", "1", "0")])
+def test_knn_shared_cell_pass(gpu, monkeypatch, uq, mask, near, fill):
     """The search's switches off their defaults (the defaults -- shared cell pass over all
     lanes, bit-mask entry test, nearest-chunks-first window -- run in every other test):
     the shared cell pass at other lane quantiles (ASP_KNN_UNION, 0 = the per-lane cell pass
@@ -130,6 +131,7 @@ def test_knn_shared_cell_pass(gpu, monkeypatch, uq, mask, near):
     monkeypatch.setenv("ASP_KNN_UNION", uq)
     monkeypatch.setenv("ASP_KNN_MASK", mask)
     monkeypatch.setenv("ASP_KNN_NEAR", near)
+    monkeypatch.setenv("ASP_KNN_FILL", fill)
     rng = np.random.default_rng(11)
     g = np.arange(30.0) * 0.5
     sets = [rng.uniform(0.0, 25.0, (60_000, 3)), _plummer(200_000, 5),
