@@ -956,9 +956,11 @@ static int cube_pass(Workspace& ws, const Grid3& g, const float* dx, const float
     long long n_recs = 0;
     int n_items = 0, n_merges = 0, n_slabs = 0;
     ASP_TRY(ensure_morton3(ws, g, st));
-    // count workgroups (scatter workgroups: half as many): ASP_CUBE_BLOCKS overrides the 512
-    // (read per call; fewer scatter workgroups keep fewer (workgroup, brick) runs open)
-    const long long max_blk = getenv("ASP_CUBE_BLOCKS") ? std::max(2, atoi(getenv("ASP_CUBE_BLOCKS"))) : 512;
+    // count workgroups (scatter workgroups: half as many), at most 384 (round 6, same process
+    // at 10^8: 512 / 384 / 256 / 128 -> cube 13.92-13.96 / 13.86-13.87 / 14.46-14.48 / 17.9 ms:
+    // fewer scatter workgroups keep fewer (workgroup, brick) runs open, scatter 3.61 -> 3.44,
+    // count 0.41 -> 0.54); ASP_CUBE_BLOCKS overrides (read per call)
+    const long long max_blk = getenv("ASP_CUBE_BLOCKS") ? std::max(2, atoi(getenv("ASP_CUBE_BLOCKS"))) : 384;
     long long nblk = std::min<long long>(max_blk, std::max<long long>(1, (n + 8191) / 8192));
     // batch-interleaved count / scatter (ASP_CUBE_INTERLEAVE=0: contiguous ranges per block)
     static const int inter = getenv("ASP_CUBE_INTERLEAVE") ? atoi(getenv("ASP_CUBE_INTERLEAVE")) : 1;
