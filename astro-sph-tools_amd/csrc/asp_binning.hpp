@@ -202,7 +202,10 @@ constexpr int kScanPer = 16;  // max tiles per scan thread held in registers (<=
 
 constexpr int kOrderBuckets = 33;  // log2 classes of counts < 2^31, plus empty items
 
-template <int PER>  // tiles per thread held in registers: ntiles <= PER * kScanThreads
+// PART 0: everything; 1: the tile starts and the record counters only (what the scatter
+// needs); 2: the rest (work items, merge list, dispatch order and their counters: what the
+// deposit needs) -- the 2-D map runs part 2 on its side stream beside the scatter (round 6)
+template <int PER, int PART = 0>  // tiles per thread held in registers: ntiles <= PER * kScanThreads
 static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     const int* __restrict__ tile_total, const int* __restrict__ morton, int ntiles, int nstream,
     long long* __restrict__ tile_start, Item* __restrict__ items, Merge* __restrict__ merges,
@@ -233,6 +236,21 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     block_scan_multi<2>(sa, ta, tid);
     const long long total = ta[0], total1 = ta[1];
     const long long base0 = sa[0];
+    if (PART == 1) {
+        long long b = base0;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            if (r0 + q >= r1) continue;
+            tile_start[tt[q]] = b;
+            if (nstream == 2) tile_start[tt[q] + ntiles] = b + cs_[q];
+            b += span(cs_[q], cl_[q]);
+        }
+        if (tid == kScanThreads - 1) {
+            ctr[cRecs] = (int)min(total, (long long)0x7fffffff);
+            ctr[cLarge] = (int)min(total1, (long long)0x7fffffff);
+        }
+        return;
+    }
     int ch = (int)max((long long)kMinItemRecords,
                       (total - total1 + target - 1) / target);
     int chl = (int)max((long long)kMinItemRecords1, (total1 + kTargetItems1 - 1) / kTargetItems1);
@@ -242,8 +260,10 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     for (int q = 0; q < PER; ++q) {
         if (r0 + q >= r1) continue;
         int t = tt[q], cs = cs_[q], cl = cl_[q];
-        tile_start[t] = base;
-        if (nstream == 2) tile_start[t + ntiles] = base + cs;
+        if (PART == 0) {
+            tile_start[t] = base;
+            if (nstream == 2) tile_start[t + ntiles] = base + cs;
+        }
         base += span(cs, cl);
         int ks, kl;
         tile_items(cs, cl, ch, chl, ks, kl);
@@ -331,11 +351,13 @@ static __global__ __launch_bounds__(kScanThreads) void k_tilescan(
     }
     if (tid == kScanThreads - 1) {
         ctr[cItems] = (int)tb[0];
-        ctr[cRecs] = (int)min(total, (long long)0x7fffffff);
         ctr[cChunk] = ch;
         ctr[cSlabs] = (int)tb[1];
         ctr[cMerges] = (int)tb[2];
-        ctr[cLarge] = (int)min(total1, (long long)0x7fffffff);
+        if (PART == 0) {
+            ctr[cRecs] = (int)min(total, (long long)0x7fffffff);
+            ctr[cLarge] = (int)min(total1, (long long)0x7fffffff);
+        }
     }
 }
 

@@ -1992,6 +1992,11 @@ struct Plan {
 
 // items / merges in the work-list buffers
 // Deposit items in tilescan order (ASP_ITEM_ORDER=0, an A/B switch) instead of largest first.
+static bool split_scan_on() {  // read per call (tests switch it)
+    const char* e = getenv("ASP_SPLIT_SCAN");
+    return e ? atoi(e) != 0 : true;
+}
+
 static int item_order_identity() {
     static const int identity = [] {
         const char* e = getenv("ASP_ITEM_ORDER");
@@ -2270,12 +2275,23 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
         ASP_LAUNCHED();
         m.done();
     }
+    // The tile scan in two parts (round 6, ASP_SPLIT_SCAN=0: one launch): the tile starts
+    // the scatter needs, on st; the work items, merge list and dispatch order the deposit
+    // needs, on the side stream beside the scatter (a one-workgroup kernel off the critical
+    // path).
+    const bool split = split_scan_on();
     {
         StageMark m(ws, kSTilescan, st);
-        hipLaunchKernelGGL(k_tilescan<4>, dim3(1), dim3(kScanThreads), 0, st,
-                           (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles, 2,
-                           (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p, dc,
-                           (int*)ws.iorder.p, item_order_identity(), item_target());
+        if (split)
+            hipLaunchKernelGGL((k_tilescan<4, 1>), dim3(1), dim3(kScanThreads), 0, st,
+                               (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles, 2,
+                               (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p,
+                               dc, (int*)ws.iorder.p, item_order_identity(), item_target());
+        else
+            hipLaunchKernelGGL((k_tilescan<4>), dim3(1), dim3(kScanThreads), 0, st,
+                               (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles, 2,
+                               (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p,
+                               dc, (int*)ws.iorder.p, item_order_identity(), item_target());
         ASP_LAUNCHED();
         m.done();
     }
@@ -2289,6 +2305,13 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
     int gate_dev = -1;  // ASP_SCATTER_GATE: this map's scatter after the last map's deposit
     if (scatter_gate_on() && hipGetDevice(&gate_dev) == hipSuccess) ASP_TRY(gate_wait(gate_dev, st));
     ASP_HIP(hipStreamWaitEvent(ws.side, ws.scan_ev, 0));
+    if (split) {
+        hipLaunchKernelGGL((k_tilescan<4, 2>), dim3(1), dim3(kScanThreads), 0, ws.side,
+                           (const int*)ws.tile_total.p, (const int*)ws.morton.p, g.ntiles, 2,
+                           (long long*)ws.tile_start.p, (Item*)ws.items.p, (Merge*)ws.merges.p,
+                           dc, (int*)ws.iorder.p, item_order_identity(), item_target());
+        ASP_LAUNCHED();
+    }
     ASP_HIP(hipMemcpyAsync(ws.h_counters, dc, (size_t)cNum * sizeof(int), hipMemcpyDeviceToHost,
                            ws.side));
     ASP_HIP(hipEventRecord(ws.cnt_ev, ws.side));
@@ -2307,6 +2330,7 @@ int project2d_device(Workspace& ws, const Grid& gin, const Src64& s, const float
 #undef ASP_SC
     }
     ASP_HIP(hipEventSynchronize(ws.cnt_ev));
+    if (split) ASP_HIP(hipStreamWaitEvent(st, ws.cnt_ev, 0));  // the deposit reads part 2's output
     const int* hc = ws.h_counters;
     pl.n_recs = hc[cRecs];
     pl.n_items = hc[cItems];

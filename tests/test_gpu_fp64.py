@@ -259,3 +259,28 @@ def test_sharded_host_arrays_single_rank_hip_path(gpu):
     # separate fp64-accumulated calls: LDS-atomic order moves the fp32 maps by an ulp or so
     np.testing.assert_array_equal(got == 0, want == 0)
     np.testing.assert_allclose(got, want, rtol=2e-6, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("h_law,G", [("pixel", 4096), ("physical", 1024)])
+def test_split_tile_scan_same_maps(gpu, monkeypatch, h_law, G):
+    """The tile scan in two parts (ASP_SPLIT_SCAN, default on: tile starts on the map's
+    stream, work items / merge list / dispatch order on the side stream beside the scatter)
+    gives the one-launch scan's maps bit for bit in the deterministic (fixed-point) mode,
+    small and mid items, gathered large stream and split tiles included."""
+    from asp_amd.device import project2d_f64, stats
+    n = 400_000
+    p = _plummer(n, 47, h_law, G)
+    pos, h, m, T = p["pos"], p["h"], p["m"], p["T"]
+    kw = dict(image_size=(G, G), extent=(-4.0, 4.0, -4.0, 4.0), chunk_size=64, kernel="cubic",
+              deterministic=True)
+    monkeypatch.setenv("ASP_SPLIT_SCAN", "0")
+    a0, a1 = project2d_f64(pos, h, m * T, m, **kw)
+    one = stats(0)
+    monkeypatch.setenv("ASP_SPLIT_SCAN", "1")
+    b0, b1 = project2d_f64(pos, h, m * T, m, **kw)
+    two = stats(0)
+    assert np.array_equal(a0, b0) and np.array_equal(a1, b1)
+    assert one["items"] == two["items"] and one["merges"] == two["merges"]
+    if h_law == "physical":
+        assert two["large"] > 0 and two["merges"] > 0
