@@ -675,7 +675,7 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
                                               const double* __restrict__ zs, double* lx, double* ly,
                                               double* lz, float* fx, float* fy, float* fz, int lane,
                                               double x, double y, double z, bool part, TopK<K>& T,
-                                              bool fill = false) {
+                                              bool fill = false, int sdiag = 0) {
     const double ox = __shfl(x, 0, 64), oy = __shfl(y, 0, 64), oz = __shfl(z, 0, 64);
     const double rx = x - ox, ry = y - oy, rz = z - oz;
     const float qx = (float)rx, qy = (float)ry, qz = (float)rz;
@@ -771,7 +771,8 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
                 tb = bound();
                 gstart = K;
             }
-            for (int g0 = gstart; g0 < m; g0 += GRP) {
+            // sdiag (timing only): 1 = the chunks staged but not tested, 2 = tested, no walks
+            for (int g0 = sdiag == 1 ? m : gstart; g0 < m; g0 += GRP) {
                 unsigned pm = 0;
 #pragma unroll 1
                 for (int u = 0; u < GRP; u += 4) {
@@ -789,6 +790,10 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
                         pm |= (d.x <= tb ? 1u : 0u) << (u + v);
                         pm |= (d.y <= tb ? 1u : 0u) << (u + v + 1);
                     }
+                }
+                if (sdiag == 2) {
+                    asm volatile("" ::"v"(pm));
+                    pm = 0;
                 }
                 if (__builtin_amdgcn_ballot_w64(pm != 0)) {
                     while (pm) {
@@ -946,7 +951,8 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
     const unsigned long long khi = win1 == n ? ~0ULL : keys[win1 - 1];
     bool shared = false;  // this lane's ball is covered by the shared cell pass
     // diag (timing only, wrong results): 2 = the shared pass's cell list and lookups without
-    // its stream, 3 = the shared pass without the per-lane pass, 4 = the cell list alone
+    // its stream, 3 = the shared pass without the per-lane pass, 4 = the cell list alone,
+    // 5 = the stream's chunks staged but not tested, 6 = tested without candidate walks
     if (uq > 0 && f32 && n >= k && (diag == 0 || diag >= 2)) {  // wave-uniform
         const bool ok = act && C.T.mx < INFINITY;
         const double R = sqrt(C.T.mx) * (1.0 + 0x1p-40);
@@ -1091,7 +1097,7 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                     return o < la ? j0 + o : max(j0, win1) + (o - la);
                 };
                 wave_stream32<K, MASK, kUGroup>(tot, at, xs, ys, zs, sx[wv], sy[wv], sz[wv], fx[wv], fy[wv], fz[wv],
-                                 lane, x, y, z, rg, C.T);
+                                 lane, x, y, z, rg, C.T, false, diag >= 5 ? diag - 4 : 0);
                 shared = rg;
                 if (evc && lane == 0) atomicAdd(&evc[2], (unsigned long long)tot);
             }
