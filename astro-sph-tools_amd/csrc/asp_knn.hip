@@ -739,7 +739,7 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
             // (every slot of the chunk is written, NaN past its end), the passing ones as a
             // bit mask, then each lane walks its own bits (exact fp64 distance, insert) --
             // the wave pays one walk per group in which any lane has a candidate
-            static_assert(GRP == 16 || GRP == 32, "group of 16 or 32 entries");
+            static_assert(GRP == 16 || GRP == 32 || GRP == 64, "group of 16, 32 or 64 entries");
             int gstart = 0;
             if (fill && c == 0 && m >= K) {
                 // the first K entries straight into the empty top-k (k == K: no -inf slots):
@@ -772,15 +772,15 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
                 gstart = K;
             }
             // sdiag (timing only): 1 = the chunks staged but not tested, 2 = tested, no walks
-            for (int g0 = sdiag == 1 ? m : gstart; g0 < m; g0 += GRP) {
-                unsigned pm = 0;
+            // entries [off, off + 32) of the chunk (at most GRP) into a 32-bit mask
+            auto test32 = [&](int off, int cnt, unsigned& pm) {
 #pragma unroll 1
-                for (int u = 0; u < GRP; u += 4) {
+                for (int u = 0; u < cnt; u += 4) {
                     // entries (u, u + 1) and (u + 2, u + 3) as packed pairs: the same
                     // roundings as the scalar form, half the instructions
-                    const kf4 X = *(const kf4*)(fx + g0 + u);
-                    const kf4 Y = *(const kf4*)(fy + g0 + u);
-                    const kf4 Z = *(const kf4*)(fz + g0 + u);
+                    const kf4 X = *(const kf4*)(fx + off + u);
+                    const kf4 Y = *(const kf4*)(fy + off + u);
+                    const kf4 Z = *(const kf4*)(fz + off + u);
 #pragma unroll
                     for (int v = 0; v < 4; v += 2) {
                         const kf2 ex = v == 0 ? X.xy : X.zw, ey = v == 0 ? Y.xy : Y.zw,
@@ -791,14 +791,26 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
                         pm |= (d.y <= tb ? 1u : 0u) << (u + v + 1);
                     }
                 }
+            };
+            // sdiag (timing only): 1 = the chunks staged but not tested, 2 = tested, no walks
+            for (int g0 = sdiag == 1 ? m : gstart; g0 < m; g0 += GRP) {
+                unsigned pm = 0, pm2 = 0;  // entries g0 + [0, 32), g0 + 32 + [0, 32) (GRP 64)
+                test32(g0, GRP < 32 ? GRP : 32, pm);
+                if (GRP == 64 && g0 + 32 < m) test32(g0 + 32, 32, pm2);
                 if (sdiag == 2) {
-                    asm volatile("" ::"v"(pm));
-                    pm = 0;
+                    asm volatile("" ::"v"(pm), "v"(pm2));
+                    pm = pm2 = 0;
                 }
-                if (__builtin_amdgcn_ballot_w64(pm != 0)) {
-                    while (pm) {
-                        const int q = g0 + __builtin_ctz(pm);
-                        pm &= pm - 1;
+                if (__builtin_amdgcn_ballot_w64((pm | pm2) != 0)) {
+                    while (pm | pm2) {
+                        int q;
+                        if (pm) {
+                            q = g0 + __builtin_ctz(pm);
+                            pm &= pm - 1;
+                        } else {
+                            q = g0 + 32 + __builtin_ctz(pm2);
+                            pm2 &= pm2 - 1;
+                        }
                         T.insert(dist2(x, y, z, lx[q], ly[q], lz[q]));
                     }
                     tb = bound();
