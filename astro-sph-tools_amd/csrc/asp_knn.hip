@@ -536,10 +536,10 @@ constexpr bool kMaskTest = true;  // the entry test's form (wave_stream32 MASK)
 constexpr int kUnionQ = 64;
 constexpr int kNearFirst = 1;  // window chunks nearest first (wave_scan32_near)
 #ifndef ASP_KNN_WGROUP
-#define ASP_KNN_WGROUP 16
+#define ASP_KNN_WGROUP 32
 #endif
 #ifndef ASP_KNN_UGROUP
-#define ASP_KNN_UGROUP 32
+#define ASP_KNN_UGROUP 64
 #endif
 constexpr int kWGroup = ASP_KNN_WGROUP;  // mask test: entries per candidate walk, window pass
 constexpr int kUGroup = ASP_KNN_UGROUP;  // ... and shared pass     // the shared cell pass's lane quantile (of 64; 0: off)
