@@ -529,7 +529,7 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn(const double* __restrict__ xs
 // nothing.
 // ----------------------------------------------------------------------------------
 constexpr int kBufSlots = 8;
-constexpr int kWinHalf = 192;  // W: curve window each side of the wave (round 6, with the shared pass: 64-320 swept)
+constexpr int kWinHalf = 256;  // W: curve window each side of the wave (round 6, with the shared pass: 64-448 swept)
 constexpr int kCellFine = 1;   // verification cells >= half the ball radius (swept: 0-3)
 constexpr int kWindowF32 = 1;  // the window pass with the fp32 prefilter (wave_scan32)
 constexpr bool kMaskTest = true;  // the entry test's form (wave_stream32 MASK)
