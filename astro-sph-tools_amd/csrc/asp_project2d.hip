@@ -1992,9 +1992,21 @@ struct Plan {
 
 // items / merges in the work-list buffers
 // Deposit items in tilescan order (ASP_ITEM_ORDER=0, an A/B switch) instead of largest first.
-static bool split_scan_on() {  // read per call (tests switch it)
-    const char* e = getenv("ASP_SPLIT_SCAN");
-    return e ? atoi(e) != 0 : true;
+// The split tile scan pays when maps run one after another on one stream (the side
+// kernel runs beside this map's scatter, a free CU slot away).  With maps on two streams
+// (two workspace slots in use) the device is already full of the other map's work: the
+// side kernel, and the host's wait for the counters behind it, start late and the
+// two-stream overlap loses more than the split saves (1.25e7 share: 0.592 vs 0.540 ms), so
+// the one-launch scan is used there.  ASP_SPLIT_SCAN=0 / 1 forces either (read per call).
+static bool split_scan_on() {
+    if (const char* e = getenv("ASP_SPLIT_SCAN")) return atoi(e) != 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    SlotTable& T = g_slots[dev];
+    std::lock_guard<std::mutex> lock(T.mu);
+    for (int k = 1; k < kMapSlots; ++k)
+        if (T.used[k]) return false;
+    return true;
 }
 
 static int item_order_identity() {
