@@ -535,9 +535,6 @@ constexpr int kWindowF32 = 1;  // the window pass with the fp32 prefilter (wave_
 constexpr bool kMaskTest = true;  // the entry test's form (wave_stream32 MASK)
 constexpr int kUnionQ = 64;
 constexpr int kNearFirst = 1;  // window chunks nearest first (wave_scan32_near)
-#ifndef ASP_KNN_TEST_FMA
-#define ASP_KNN_TEST_FMA 0  // 1: the mask test's fp32 distance with packed fma (A/B switch)
-#endif
 #ifndef ASP_KNN_WGROUP
 #define ASP_KNN_WGROUP 32
 #endif
@@ -779,8 +776,7 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
             auto test32 = [&](int off, int cnt, unsigned& pm) {
 #pragma unroll 1
                 for (int u = 0; u < cnt; u += 4) {
-                    // entries (u, u + 1) and (u + 2, u + 3) as packed pairs: the same
-                    // roundings as the scalar form, half the instructions
+                    // entries (u, u + 1) and (u + 2, u + 3) as packed pairs
                     const kf4 X = *(const kf4*)(fx + off + u);
                     const kf4 Y = *(const kf4*)(fy + off + u);
                     const kf4 Z = *(const kf4*)(fz + off + u);
@@ -789,13 +785,11 @@ __device__ __forceinline__ void wave_stream32(long long nent, At at, const doubl
                         const kf2 ex = v == 0 ? X.xy : X.zw, ey = v == 0 ? Y.xy : Y.zw,
                                   ez = v == 0 ? Z.xy : Z.zw;
                         const kf2 dx = qx2 - ex, dy = qy2 - ey, dz = qz2 - ez;
-#if ASP_KNN_TEST_FMA
-                        // fused: fewer roundings than the bound's (1 + 5u) allows for
+                        // fused (v_pk_fma_f32): three roundings instead of five, inside the
+                        // (1 + 5u) the bound allows for the sum of squares (same box, 10^7:
+                        // 17.49-17.56 -> 17.10-17.17 ms)
                         const kf2 d = __builtin_elementwise_fma(
                             dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
-#else
-                        const kf2 d = (dx * dx + dy * dy) + dz * dz;
-#endif
                         pm |= (d.x <= tb ? 1u : 0u) << (u + v);
                         pm |= (d.y <= tb ? 1u : 0u) << (u + v + 1);
                     }
