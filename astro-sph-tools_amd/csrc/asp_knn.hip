@@ -1099,13 +1099,22 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
             }
             if (!ovf && tot <= kUMaxEnt && diag != 2 && diag != 4) {
                 const unsigned long long* L = ucl[wv];
-                auto at = [&](long long f) -> long long {  // the last entry starting at or before f
-                    int lo = 0, hi = nc - 1;
+                int cur = 0;  // this lane's range of its previous entry (entries come in order)
+                auto at = [&](long long f) -> long long {  // the last range starting at or before f
+                    // exponential search forward from the previous entry's range (a chunk
+                    // advances a lane by 64 entries, a few ranges), then binary search
+                    int lo = cur, step = 1;
+                    while (lo + step < nc && (long long)(L[lo + step] >> 47) <= f) {
+                        lo += step;
+                        step <<= 1;
+                    }
+                    int hi = min(lo + step, nc) - 1;
                     while (lo < hi) {
                         const int mid = (lo + hi + 1) >> 1;
                         if ((long long)(L[mid] >> 47) <= f) lo = mid;
                         else hi = mid - 1;
                     }
+                    cur = lo;
                     const unsigned long long e = L[lo];
                     const long long o = f - (long long)(e >> 47), la = (long long)((e >> 31) & 0xffff);
                     const long long j0 = (long long)(e & 0x7fffffffULL);
