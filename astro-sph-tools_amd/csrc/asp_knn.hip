@@ -37,8 +37,13 @@
 namespace asp {
 
 constexpr int kKnnBlock = 256;
-constexpr int kQBits = 21;                       // quantisation bits per axis
+#ifndef ASP_KNN_QBITS
+#define ASP_KNN_QBITS 21
+#endif
+constexpr int kQBits = ASP_KNN_QBITS;            // quantisation bits per axis
+constexpr int kKeyBits = 3 * kQBits;             // Morton key bits (keys < 2^kKeyBits)
 constexpr long long kQMax = (1LL << kQBits) - 1;
+static_assert(kQBits >= 12 && kQBits <= 21, "3 x kQBits key bits in 64; >= the tables' 12 levels");
 constexpr int kRedBlocks = 1024;                 // bounding-box partial reductions
 
 __device__ __forceinline__ unsigned long long spread21(unsigned long long v) {
@@ -237,7 +242,7 @@ struct CellTab {
     const int* tab;
     const int* sub;     // per level-L cell: its sub-table, or -1
     const int* subtab;  // sub-tables, kSubCells + 1 entries each
-    int sh;  // 63 - 3 L: key >> sh = the level-L cell
+    int sh;  // kKeyBits - 3 L: key >> sh = the level-L cell
 };
 
 // Built in two steps (round 5): each occupied cell's first particle writes its index, then a
@@ -340,7 +345,7 @@ __global__ __launch_bounds__(kKnnBlock) void k_sub_table(const unsigned long lon
         for (int r = q + 1; r <= kSubCells; ++r) st[r] = end;
 }
 
-// First index with key >= k0 (k0 < 2^63), through the tables.
+// First index with key >= k0 (k0 < 2^kKeyBits), through the tables.
 __device__ __forceinline__ long long cell_lower(const unsigned long long* __restrict__ keys,
                                                 long long n, const CellTab& T,
                                                 unsigned long long k0) {
@@ -427,8 +432,8 @@ __device__ __forceinline__ double knn_thread(long long i, const double* __restri
     if (n >= k + 1) {
         const unsigned long long key = keys[i];
         for (int sh = 0; sh <= 3 * kQBits; sh += 3) {
-            const unsigned long long pre = sh >= 63 ? 0ULL : key >> sh;
-            auto same = [&](long long j) { return sh >= 63 || (keys[j] >> sh) == pre; };
+            const unsigned long long pre = sh >= kKeyBits ? 0ULL : key >> sh;
+            auto same = [&](long long j) { return sh >= kKeyBits || (keys[j] >> sh) == pre; };
             // grow w0 down: gallop, then bisect
             long long step = 1;
             while (w0 - step >= 0 && same(w0 - step)) { w0 -= step; step <<= 1; }
@@ -483,10 +488,10 @@ __device__ __forceinline__ double knn_thread(long long i, const double* __restri
                         }
                         if (md * (1.0 - 0x1p-40) > T.mx) continue;
                         unsigned long long p = morton3(cx, cy, cz);
-                        unsigned long long k0 = sh3 >= 63 ? 0ULL : p << sh3;
-                        unsigned long long k1 = sh3 >= 63 ? ~0ULL : (p + 1) << sh3;
+                        unsigned long long k0 = sh3 >= kKeyBits ? 0ULL : p << sh3;
+                        unsigned long long k1 = sh3 >= kKeyBits ? ~0ULL : (p + 1) << sh3;
                         long long j0 = lower_bound(keys, n, k0);
-                        long long j1 = sh3 >= 63 ? n : lower_bound(keys + j0, n - j0, k1) + j0;
+                        long long j1 = sh3 >= kKeyBits ? n : lower_bound(keys + j0, n - j0, k1) + j0;
                         // [w0, w1) is in already
                         for (long long j = j0; j < std::min(j1, w0); ++j)
                             T.insert(dist2(x, y, z, xs[j], ys[j], zs[j]));
@@ -1008,8 +1013,8 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
             int nc = 0, ncol = 0;
             // cells p with k0 = p << sh3 >= klo and k1 = (p + 1) << sh3 <= khi lie inside the
             // window's key span: p >= ceil(klo / 2^sh3), p < floor(khi / 2^sh3)
-            const unsigned long long plo = sh3 >= 63 ? 1ULL : (klo >> sh3) + ((klo & ((1ULL << sh3) - 1)) != 0);
-            const unsigned long long phi = sh3 >= 63 ? 0ULL : (khi >> sh3);
+            const unsigned long long plo = sh3 >= kKeyBits ? 1ULL : (klo >> sh3) + ((klo & ((1ULL << sh3) - 1)) != 0);
+            const unsigned long long phi = sh3 >= kKeyBits ? 0ULL : (khi >> sh3);
             bool ovf = (long long)(B[0] - A[0] + 1) * (B[1] - A[1] + 1) > kUScan;
             for (int cx = A[0]; cx <= B[0] && !ovf; ++cx) {
                 const double gx = gapq(0, cx), sx2 = gx * gx;
@@ -1049,7 +1054,7 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                             break;
                         }
                         if (start) {
-                            ucl[wv][idx] = sh3 >= 63 ? 0ULL : p << sh3;
+                            ucl[wv][idx] = sh3 >= kKeyBits ? 0ULL : p << sh3;
                             ucn[wv][idx] = (unsigned short)(1 + ((cz & 1) == 0 && next));
                         }
                         nc += cnt;
@@ -1075,9 +1080,9 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                     if (c < nc) {
                         const unsigned long long k0 = ucl[wv][c];
                         const unsigned long long span = (unsigned long long)ucn[wv][c] << sh3;
-                        const unsigned long long k1 = sh3 >= 63 ? ~0ULL : k0 + span;
+                        const unsigned long long k1 = sh3 >= kKeyBits ? ~0ULL : k0 + span;
                         long long j1;
-                        if (sh3 >= 63 || (k1 >> 63)) {  // the range runs to the end of the keys
+                        if (sh3 >= kKeyBits || (k1 >> kKeyBits)) {  // the range runs to the end of the keys
                             j0 = cell_lower(keys, n, CT, k0);
                             j1 = n;
                         } else {
@@ -1156,13 +1161,13 @@ __global__ __launch_bounds__(kKnnBlock, (K == 32 ? 3 : 1)) ASP_KNN_OCC void k_kn
                     }
                     if (md * (1.0 - 0x1p-40) > C.T.mx) continue;  // beyond the k-th distance
                     unsigned long long p = morton3(cx, cy, cz);
-                    unsigned long long k0 = sh3 >= 63 ? 0ULL : p << sh3;
-                    unsigned long long k1 = sh3 >= 63 ? ~0ULL : (p + 1) << sh3;  // exclusive
+                    unsigned long long k0 = sh3 >= kKeyBits ? 0ULL : p << sh3;
+                    unsigned long long k1 = sh3 >= kKeyBits ? ~0ULL : (p + 1) << sh3;  // exclusive
                     if (k0 >= klo && k1 <= khi) continue;  // inside the window already
                     // a cell adjacent in key order to the last one looked up (the z pairs
                     // of a column, ...) starts where that one ended: one lookup instead of two
                     const long long j0 = k0 == pk1 ? pj1 : cell_lower(keys, n, CT, k0);
-                    const long long j1 = sh3 >= 63 || (k1 >> 63) ? n : cell_lower(keys, n, CT, k1);
+                    const long long j1 = sh3 >= kKeyBits || (k1 >> kKeyBits) ? n : cell_lower(keys, n, CT, k1);
                     pk1 = k1;
                     pj1 = j1;
                     scan_range<K>(j0, min(j1, win0), xs, ys, zs, x, y, z, C.T);
@@ -1244,7 +1249,7 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
     int* tab = (int*)ws.knn[7].p;
     ASP_HIP(hipMemsetD32Async((hipDeviceptr_t)tab, (int)n, (size_t)(ncell + 1), st));
     hipLaunchKernelGGL(k_cell_starts, dim3(grid), dim3(kKnnBlock), 0, st,
-                       (const unsigned long long*)kout, (long long)n, 63 - 3 * L, tab);
+                       (const unsigned long long*)kout, (long long)n, kKeyBits - 3 * L, tab);
     ASP_LAUNCHED();
     {  // the empty cells: suffix minimum over the ncell + 1 entries
         const long long m = ncell + 1;
@@ -1272,10 +1277,10 @@ static int knn(const double* pos, long long n, int k, double* h, int flags, int 
                        dim3(kKnnBlock), 0, st, (const int*)tab, ncell, submin, sub, nslot);
     ASP_LAUNCHED();
     hipLaunchKernelGGL(k_sub_table, dim3(grid), dim3(kKnnBlock), 0, st,
-                       (const unsigned long long*)kout, (long long)n, 63 - 3 * L,
+                       (const unsigned long long*)kout, (long long)n, kKeyBits - 3 * L,
                        (const int*)tab, (const int*)sub, subtab);
     ASP_LAUNCHED();
-    const CellTab CT{tab, sub, subtab, 63 - 3 * L};
+    const CellTab CT{tab, sub, subtab, kKeyBits - 3 * L};
     mprep.done();
     // diagnostics only: ASP_KNN_THREAD = one lane per particle throughout;
     // ASP_KNN_DIAG = 1: the window pass alone (wrong results, timing)
